@@ -1,0 +1,366 @@
+"""CPU oracle for the Longitudinal-VAE GP-prior ELBO hot path -- TEST INFRASTRUCTURE ONLY.
+
+A plain torch-fp64-on-CPU restatement of the reference's algorithm (SidRama/Longitudinal-VAE),
+written op-for-op from the formulas so that autograd yields the same gradients the reference's
+autograd yields.  Pinned against golden vectors produced by running the reference itself
+(``tests/golden/gen_golden.py`` -> ``tests/golden/*.npz``; see ``tests/test_oracle_golden.py``).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker / CPU baseline.  The product path
+(``longitudinal-vae_amd/lvae_amd``) never imports it.
+
+Kernel specification.  A kernel is an ordered list of additive components; a component is a
+scale times a product of factors.  Factor kinds (GP_model.py:31-85, kernel_spec.py:9-69):
+  ("cat", d)      1[x1_d == x2_d]                 (GP_model.py:52-53)
+  ("bin", d)      1[x1_d + x2_d == 2]             (GP_model.py:40-41)
+  ("rbf", d)      exp(-(x1_d - x2_d)^2 / (2 l^2)) (GP_model.py:80-85)  -- one lengthscale
+  ("per", d)      exp(-2 sin^2(pi |x1_d - x2_d| / p) / l^2)   extension, parity unpinned
+  ("lin", d)      x1_d * x2_d                                  extension, parity unpinned
+Parameters of one component, in this order: scale, then per factor its own lengthscale (rbf),
+lengthscale + period (per).  This is the order GP_model's ``named_parameters`` yields.
+Positivity: value = exp(m + softplus(raw - m)), m = -16 (GP_model.py:65-73, 97-105).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+MIN_LOG = -16.0
+N_PARAMS = {"cat": 0, "bin": 0, "rbf": 1, "per": 2, "lin": 0}
+
+
+# ------------------------------------------------------------------------------------------
+# kernel specification from config lists
+# ------------------------------------------------------------------------------------------
+def _masked(factor, d, missing):
+    """covariate_missing_val: multiply by Bin(mask) (GP_model.py:173-178, 187-189)."""
+    for dm in missing:
+        if dm["covariate"] == d:
+            return [factor, ("bin", dm["mask"])]
+    return [factor]
+
+
+def spec_split(cat_kernel, bin_kernel, sqexp_kernel, cat_int_kernel, bin_int_kernel,
+               covariate_missing_val, id_covariate):
+    """(non-id, id) component lists, in GP_model.generate_kernel_batched order (GP_model.py:146-236)."""
+    k0, k1 = [], []
+    for d in cat_kernel:
+        (k1 if d == id_covariate else k0).append(_masked(("cat", d), d, covariate_missing_val))
+    for d in sqexp_kernel:
+        k0.append(_masked(("rbf", d), d, covariate_missing_val))
+    for d in bin_kernel:
+        k0.append(_masked(("bin", d), d, covariate_missing_val))
+    for di in cat_int_kernel:
+        c, x = di["cat_covariate"], di["cont_covariate"]
+        comp = _masked(("cat", c), c, covariate_missing_val) + _masked(("rbf", x), x, covariate_missing_val)
+        (k1 if c == id_covariate else k0).append(comp)
+    for di in bin_int_kernel:
+        b, x = di["bin_covariate"], di["cont_covariate"]
+        k0.append(_masked(("bin", b), b, covariate_missing_val) + _masked(("rbf", x), x, covariate_missing_val))
+    return k0, k1
+
+
+def spec_full(cat_kernel, bin_kernel, sqexp_kernel, cat_int_kernel, bin_int_kernel, covariate_missing_val):
+    """One additive kernel in kernel_gen.generate_kernel order (kernel_gen.py:28-92)."""
+    k = []
+    for d in cat_kernel:
+        k.append(_masked(("cat", d), d, covariate_missing_val))
+    for d in sqexp_kernel:
+        k.append(_masked(("rbf", d), d, covariate_missing_val))
+    for d in bin_kernel:
+        k.append(_masked(("bin", d), d, covariate_missing_val))
+    for di in cat_int_kernel:
+        c, x = di["cat_covariate"], di["cont_covariate"]
+        k.append(_masked(("cat", c), c, covariate_missing_val) + _masked(("rbf", x), x, covariate_missing_val))
+    for di in bin_int_kernel:
+        b, x = di["bin_covariate"], di["cont_covariate"]
+        k.append(_masked(("bin", b), b, covariate_missing_val) + _masked(("rbf", x), x, covariate_missing_val))
+    return k
+
+
+def n_params(spec):
+    return sum(1 + sum(N_PARAMS[f[0]] for f in comp) for comp in spec)
+
+
+def constrain(raw):
+    return torch.exp(MIN_LOG + F.softplus(raw - MIN_LOG))
+
+
+def unconstrain(val):
+    return torch.log(val - math.exp(MIN_LOG))
+
+
+# ------------------------------------------------------------------------------------------
+# Gram evaluation.  params: [P] (one latent dim) or [L, P] (batch over L, right-aligned like
+# gpytorch batch_shape=[L]: output [..., L, n1, n2] for inputs [..., L, n, Q] / [L, n, Q] / [n, Q]).
+# ------------------------------------------------------------------------------------------
+def _bcast(v, nd):
+    """[L] parameter -> [L, 1, 1] (right-aligned against an output of rank nd)."""
+    if v.dim() == 0:
+        return v
+    return v.reshape(v.shape + (1, 1))
+
+
+def gram(spec, params, x1, x2):
+    out = None
+    j = 0
+    for comp in spec:
+        s = params[..., j]
+        j += 1
+        val = None
+        for f in comp:
+            kind, d = f
+            a = x1[..., d].unsqueeze(-1)
+            b = x2[..., d].unsqueeze(-2)
+            if kind == "cat":
+                v = (a - b == 0).to(x1.dtype)
+            elif kind == "bin":
+                v = (a + b == 2).to(x1.dtype)
+            elif kind == "rbf":
+                ell = _bcast(params[..., j], 0)
+                j += 1
+                v = torch.exp(-((a - b) ** 2) / (2 * ell ** 2))
+            elif kind == "per":
+                ell = _bcast(params[..., j], 0)
+                per = _bcast(params[..., j + 1], 0)
+                j += 2
+                v = torch.exp(-2 * torch.sin(math.pi * torch.abs(a - b) / per) ** 2 / ell ** 2)
+            elif kind == "lin":
+                v = a * b
+            else:
+                raise ValueError(kind)
+            val = v if val is None else val * v
+        term = _bcast(s, 0) * val
+        out = term if out is None else out + term
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Regime B: exact KL (elbo_functions.py:8-34)
+#   KL = 1/2 ( tr(K^-1 V) + mu^T K^-1 mu - N + log|K| - sum log v ),  K = Gram + noise I
+# ------------------------------------------------------------------------------------------
+def kl_closed(spec, params, x, noise, mu, logv):
+    n = x.shape[0]
+    K = gram(spec, params, x, x) + noise * torch.eye(n, dtype=x.dtype)
+    L = torch.linalg.cholesky(K)
+    Kinv = torch.cholesky_solve(torch.eye(n, dtype=x.dtype), L)
+    logdetK = 2 * torch.log(torch.diagonal(L)).sum()
+    quad = (mu * (Kinv @ mu)).sum()
+    trace = (torch.exp(logv) * torch.diagonal(Kinv)).sum()
+    return 0.5 * (trace + quad - n + logdetK - logv.sum())
+
+
+# ------------------------------------------------------------------------------------------
+# Regime A: Hensman mini-batch KL upper bound (elbo_functions.py:144-216)
+#   per latent dim l, subject p of the batch:
+#   r = K0xz iK m - mu;  A = sum_p r_p^T iB_p r_p;  Bt = sum diag(iB) v;  C = sum log|B_p|
+#   Q = sum_p K0xz_p^T iB_p K0xz_p;  D = sum tr(iB_p K0_p) - tr(Q iK);  E = tr(iK H iK Q)
+#   F = sum log v;  kl_u = 1/2 (tr(iK H) + m^T iK m - M + log|K0zz| - log|H|)
+#   kld = P_tot/P_b * 1/2 (A + Bt + C + D + E - F) + kl_u  (summed over l) - L P_tot T / 2
+# ------------------------------------------------------------------------------------------
+def hensman_kld(spec0, params0, spec1, params1, noise, m, H, x, mu, logv, z, P_tot, P_b, T,
+                natural_gradient, eps):
+    Lh, M = H.shape[0], H.shape[-1]
+    dt = x.dtype
+    xs = x.reshape(P_b, T, x.shape[-1])
+    K0xz = gram(spec0, params0, x, z)                                  # [L, B, M]
+    K0zz = gram(spec0, params0, z, z) + eps * torch.eye(M, dtype=dt)   # [L, M, M]
+    xs_l = xs.unsqueeze(1).expand(P_b, Lh, T, xs.shape[-1])
+    K0 = gram(spec0, params0, xs_l, xs_l).transpose(0, 1)              # [L, P_b, T, T]
+    Bm = (gram(spec1, params1, xs_l, xs_l) + torch.eye(T, dtype=dt) * noise.reshape(Lh, 1, 1)).transpose(0, 1)
+    LK = torch.linalg.cholesky(K0zz)
+    iK = torch.cholesky_solve(torch.eye(M, dtype=dt), LK)
+    LB = torch.linalg.cholesky(Bm)
+    iB = torch.cholesky_solve(torch.eye(T, dtype=dt), LB)
+    Kst = K0xz.reshape(Lh, P_b, T, M)
+    iBK = iB @ Kst
+    Q = K0xz.transpose(1, 2) @ iBK.reshape(Lh, P_b * T, M)
+    LH = torch.linalg.cholesky(H)
+    iH = torch.cholesky_solve(torch.eye(M, dtype=dt), LH)
+    r = ((K0xz @ (iK @ m)).squeeze(-1) - mu.T).reshape(Lh, P_b, T, 1)
+    A = (r.transpose(2, 3) @ iB @ r).sum()
+    Bt = (torch.diagonal(iB, dim1=-2, dim2=-1).reshape(Lh, -1) * torch.exp(logv.T)).sum()
+    C = 2 * torch.log(torch.diagonal(LB, dim1=-2, dim2=-1)).sum()
+    D = (iB * K0).sum() - (Q * iK).sum()
+    E = ((iK @ H @ iK).transpose(-1, -2) * Q).sum()
+    Fs = logv.sum()
+    kl_u = 0.5 * ((iK * H.transpose(-1, -2)).sum() + (m * (iK @ m)).sum() - Lh * M
+                  + 2 * torch.log(torch.diagonal(LK, dim1=-2, dim2=-1)).sum()
+                  - 2 * torch.log(torch.diagonal(LH, dim1=-2, dim2=-1)).sum())
+    kld = P_tot / P_b * 0.5 * (A + Bt + C + D + E - Fs) + kl_u - Lh * P_tot * T / 2
+    gm = gH = None
+    if natural_gradient:
+        mu_st = mu.T.reshape(Lh, P_b, T, 1)
+        K0zx = Kst.transpose(-1, -2)
+        a = (iK.unsqueeze(1) @ K0zx @ (iB @ mu_st)).sum(1)
+        Bn = iK @ Q @ iK + iK
+        gm = -a + Bn @ m
+        gH = 0.5 * (-iH + Bn)
+    return kld, gm, gH
+
+
+def natural_gradient_update(m, H, grad_m, grad_H, lr):
+    """training.py:129-135."""
+    M = H.shape[-1]
+    I = torch.eye(M, dtype=H.dtype)
+    iH = torch.cholesky_solve(I, torch.linalg.cholesky(H))
+    iH_new = iH + lr * (grad_H + grad_H.transpose(-1, -2))
+    H_new = torch.cholesky_solve(I, torch.linalg.cholesky(iH_new))
+    m_new = H_new @ (iH @ m - lr * (grad_m - 2 * grad_H @ m))
+    return m_new, H_new
+
+
+# ------------------------------------------------------------------------------------------
+# per-dim GPapprox ELBO (elbo_functions.py:36-84) and DUBO (86-142)
+# ------------------------------------------------------------------------------------------
+def _gpapprox_common(spec0, params0, spec1, params1, noise, x, z, P, T, eps):
+    dt = x.dtype
+    M = z.shape[0]
+    xs = x.reshape(P, T, x.shape[-1])
+    K0xz = gram(spec0, params0, x, z)
+    K0zz = gram(spec0, params0, z, z) + eps * torch.eye(M, dtype=dt)
+    LK = torch.linalg.cholesky(K0zz)
+    iK = torch.cholesky_solve(torch.eye(M, dtype=dt), LK)
+    K0 = gram(spec0, params0, xs, xs)
+    Bm = gram(spec1, params1, xs, xs) + torch.eye(T, dtype=dt) * noise
+    LB = torch.linalg.cholesky(Bm)
+    iB = torch.cholesky_solve(torch.eye(T, dtype=dt), LB)
+    iBK = iB @ K0xz.reshape(P, T, M)
+    Q = K0xz.T @ iBK.reshape(P * T, M)
+    W = K0zz + Q
+    W = 0.5 * (W + W.T)
+    LW = torch.linalg.cholesky(W)
+    logdet = (-2 * torch.log(torch.diagonal(LK)).sum() + 2 * torch.log(torch.diagonal(LB, dim1=-2, dim2=-1)).sum()
+              + 2 * torch.log(torch.diagonal(LW)).sum())
+    tr = (iB * K0).sum() - (Q * iK).sum()
+    return dict(K0xz=K0xz, Bm=Bm, iB=iB, iBK=iBK, LW=LW, logdet=logdet, tr=tr, M=M)
+
+
+def _quad(c, y, P, T):
+    iBy = torch.linalg.solve(c["Bm"], y.reshape(P, T, 1))
+    q1 = (y.reshape(P, T, 1) * iBy).sum()
+    p = c["K0xz"].T @ iBy.reshape(P * T)
+    q2 = (torch.linalg.solve_triangular(c["LW"], p[:, None], upper=False) ** 2).sum()
+    return q1 - q2
+
+
+def gpapprox_elbo(spec0, params0, spec1, params1, noise, x, y, z, P, T, eps):
+    c = _gpapprox_common(spec0, params0, spec1, params1, noise, x, z, P, T, eps)
+    loglike = -0.5 * T * P * math.log(2 * math.pi) - 0.5 * (c["logdet"] + _quad(c, y, P, T))
+    return loglike - 0.5 * c["tr"]
+
+
+def deviance_upper_bound(spec0, params0, spec1, params1, noise, x, mu, logv, z, P, T, eps):
+    c = _gpapprox_common(spec0, params0, spec1, params1, noise, x, z, P, T, eps)
+    v = torch.exp(logv)
+    vs = v.reshape(P, T)
+    tr_iB_D = (torch.diagonal(c["iB"], dim1=-2, dim2=-1) * vs).sum()
+    Dh = (c["iBK"] * torch.sqrt(vs)[:, :, None]).reshape(P * T, c["M"])
+    S = Dh.T @ Dh
+    tr2 = torch.diagonal(torch.cholesky_solve(S, c["LW"])).sum()
+    return 0.5 * ((tr_iB_D - tr2) + _quad(c, mu, P, T) - P * T + c["logdet"] - torch.log(v).sum() + c["tr"])
+
+
+# ------------------------------------------------------------------------------------------
+# ConvVAE (VAE.py:16-162), fp64, dropout disabled
+# ------------------------------------------------------------------------------------------
+class ConvVAE(nn.Module):
+    def __init__(self, latent_dim, num_dim=1296, vy_init=1.0):
+        super().__init__()
+        self.latent_dim, self.num_dim = latent_dim, num_dim
+        self._log_vy = nn.Parameter(torch.full((num_dim,), math.log(vy_init - math.exp(-8.0))))
+        self.conv1 = nn.Conv2d(1, 16, 3, 1, 1)
+        self.conv2 = nn.Conv2d(16, 32, 3, 1, 1)
+        self.fc1 = nn.Linear(32 * 9 * 9, 300)
+        self.fc21 = nn.Linear(300, 30)
+        self.fc211 = nn.Linear(30, latent_dim)
+        self.fc221 = nn.Linear(30, latent_dim)
+        self.fc3 = nn.Linear(latent_dim, 30)
+        self.fc31 = nn.Linear(30, 300)
+        self.fc4 = nn.Linear(300, 32 * 9 * 9)
+        self.deconv1 = nn.ConvTranspose2d(32, 16, 4, 2, 1)
+        self.deconv2 = nn.ConvTranspose2d(16, 1, 4, 2, 1)
+        self.register_buffer("min_log_vy", torch.full((1,), -8.0))
+
+    def encode(self, x):
+        h = F.max_pool2d(F.relu(self.conv1(x)), 2, 2)
+        h = F.max_pool2d(F.relu(self.conv2(h)), 2, 2)
+        h = F.relu(self.fc21(F.relu(self.fc1(h.reshape(-1, 32 * 81)))))
+        return self.fc211(h), self.fc221(h)
+
+    def decode(self, z):
+        h = F.relu(self.fc4(F.relu(self.fc31(F.relu(self.fc3(z))))))
+        h = F.relu(self.deconv1(h.reshape(-1, 32, 9, 9)))
+        return torch.sigmoid(self.deconv2(h))
+
+    def loss_function(self, recon, x, mask):
+        se = (recon.reshape(-1, self.num_dim) - x.reshape(-1, self.num_dim)) ** 2 * mask.reshape(-1, self.num_dim)
+        msum = mask.reshape(-1, self.num_dim).sum(1)
+        msum = torch.where(msum == 0, torch.ones_like(msum), msum)
+        mse = se.sum(1) / msum
+        nll = se / (2 * torch.exp(self._log_vy)) + 0.5 * (math.log(2 * math.pi) + self._log_vy)
+        return mse, nll.sum(1)
+
+
+def vae_weights(model, seed):
+    """Deterministic weights (same formula as tests/golden/gen_golden.py:vae_weights)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for name, p in model.state_dict().items():
+        if name == "min_log_vy":
+            sd[name] = p.clone()
+        elif name == "_log_vy":
+            sd[name] = torch.tensor(0.1 * rng.standard_normal(p.shape))
+        else:
+            fan = p[0].numel() if p.dim() > 1 else p.numel()
+            sd[name] = torch.tensor(rng.standard_normal(p.shape) / math.sqrt(max(fan, 1)))
+    return sd
+
+
+# ------------------------------------------------------------------------------------------
+# full steps (step composition a11: training.py:103-135 / 499-575) -- CPU baseline legs
+# ------------------------------------------------------------------------------------------
+def closed_step(vae, spec, raw_params, noise, x_img, mask, cov, eps_noise, weight, opt=None):
+    """One standard_training step with type_KL='closed', loss='mse' (training.py:484-589)."""
+    if opt is not None:
+        opt.zero_grad()
+    mu, logv = vae.encode(x_img)
+    z = mu + eps_noise * torch.exp(0.5 * logv)
+    recon = vae.decode(z)
+    mse, _ = vae.loss_function(recon, x_img, mask)
+    recon_loss = mse.sum()
+    params = constrain(raw_params)
+    Ld = mu.shape[1]
+    gp = 0
+    for l in range(Ld):
+        gp = gp + kl_closed(spec, params[l], cov, noise[l], mu[:, l], logv[:, l])
+    loss = recon_loss + weight * gp / Ld
+    loss.backward()
+    if opt is not None:
+        opt.step()
+    return loss.detach(), recon_loss.detach(), (gp / Ld).detach()
+
+
+def hensman_step(vae, spec0, raw0, spec1, raw1, noise, m, H, x_img, mask, cov, z, eps_noise,
+                 P_tot, T, weight, ng_lr, eps=1e-6, opt=None):
+    """One hensman_training batch, natural gradient, loss='mse' (training.py:91-135)."""
+    if opt is not None:
+        opt.zero_grad()
+    mu, logv = vae.encode(x_img)
+    zz = mu + eps_noise * torch.exp(0.5 * logv)
+    recon = vae.decode(zz)
+    mse, _ = vae.loss_function(recon, x_img, mask)
+    P_b = x_img.shape[0] // T
+    Ld = mu.shape[1]
+    kld, gm, gH = hensman_kld(spec0, constrain(raw0), spec1, constrain(raw1), noise, m, H, cov, mu, logv, z,
+                              P_tot, P_b, T, True, eps)
+    recon_loss = mse.sum() * P_tot / P_b
+    kld = kld / Ld
+    loss = recon_loss + weight * kld
+    loss.backward()
+    if opt is not None:
+        opt.step()
+    m2, H2 = natural_gradient_update(m, H, gm.detach(), gH.detach(), ng_lr)
+    return loss.detach(), recon_loss.detach(), kld.detach(), m2, H2

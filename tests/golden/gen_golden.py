@@ -1,0 +1,375 @@
+"""Generate golden input/output vectors by running the REFERENCE code (/root/reference).
+
+Test infrastructure only.  Runs in the build container (where /root/reference exists); the
+GPU box never runs it -- it only reads the committed ``*.npz`` fixtures this script writes.
+
+The reference is imported read-only with the harness shims SURVEY.md §8(c) lists:
+  * ``torchvision`` stub (``transforms`` is only used for dataset construction),
+  * ``torch.solve`` (removed in torch 2.x; used at elbo_functions.py:75,129),
+  * ``np.Inf`` (training.py:82),
+  * kernel adapter: GP_model.py kernels left-align their ``[L]`` parameters while gpytorch
+    (the path LVAE.py really runs, kernel_gen.py:199-310) right-aligns ``batch_shape=[L]``;
+    for 4-D inputs the adapter evaluates ``k(a.T01, b.T01).T01`` which is the gpytorch
+    semantics ``elbo_functions.py:173-174`` rely on,
+  * likelihood stub exposing ``.noise`` and ``.noise_covar.noise``.
+
+Every fixture holds inputs and expected outputs only (data, not reference source).
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+import math
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_shims():
+    import torch
+    tv = types.ModuleType("torchvision")
+    tv.transforms = types.SimpleNamespace(ToTensor=lambda: None)
+    sys.modules.setdefault("torchvision", tv)
+    sys.modules.setdefault("torchvision.transforms", tv.transforms)
+    torch.solve = lambda B, A: (torch.linalg.solve(A, B), None)  # present-but-raising in torch 2.x
+    if not hasattr(np, "Inf"):
+        np.Inf = np.inf
+    sys.dont_write_bytecode = True
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+
+
+_install_shims()
+import torch  # noqa: E402
+from torch import nn  # noqa: E402
+
+import GP_model as R  # noqa: E402  (reference)
+import elbo_functions as EF  # noqa: E402  (reference)
+import VAE as RV  # noqa: E402  (reference)
+
+torch.set_default_dtype(torch.float64)
+
+
+# ----------------------------------------------------------------------------------------------
+# adapters
+# ----------------------------------------------------------------------------------------------
+class _Lazy:
+    def __init__(self, t):
+        self.t = t
+
+    def evaluate(self):
+        return self.t
+
+
+class KernelAdapter(nn.Module):
+    """gpytorch call convention over a GP_model kernel (see module docstring)."""
+
+    def __init__(self, k):
+        super().__init__()
+        self.k = k
+
+    def forward(self, a, b):
+        if a.dim() == 4:
+            return _Lazy(self.k(a.transpose(0, 1), b.transpose(0, 1)).transpose(0, 1))
+        return _Lazy(self.k(a, b))
+
+
+class LikStub:
+    def __init__(self, noise):
+        self.noise = noise
+        self.noise_covar = types.SimpleNamespace(noise=noise)
+
+
+# ----------------------------------------------------------------------------------------------
+# synthetic Health-MNIST covariates (Health_MNIST_generate.py:89-154)
+# columns: time_age, disease_time, subject, gender, disease, location  (dataset_def.py:213)
+# ----------------------------------------------------------------------------------------------
+def covariates(P, T, seed):
+    rng = np.random.default_rng(seed)
+    sick = rng.binomial(1, 0.5, size=P)
+    loc = rng.binomial(1, 0.5, size=P)
+    X = np.zeros((P * T, 6))
+    for p in range(P):
+        for t in range(T):
+            r = p * T + t
+            X[r, 0] = t
+            X[r, 1] = (t - 9) if sick[p] else 0.0
+            X[r, 2] = p
+            X[r, 3] = 0.0 if p < P // 2 else 1.0
+            X[r, 4] = sick[p]
+            X[r, 5] = loc[p]
+    return X
+
+
+# sample config (config/LVAE_config_sample.txt:40-45)
+CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+           cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                           {'cont_covariate': 0, 'cat_covariate': 3},
+                           {'cont_covariate': 1, 'cat_covariate': 4}],
+           bin_int_kernel=[], covariate_missing_val=[], id_covariate=2)
+
+
+def full_kernel_ref(L):
+    """The non-split additive kernel in kernel_gen.generate_kernel order (kernel_gen.py:28-92),
+    built from the reference's own gpytorch-free GP_model classes."""
+    ks = [R.ScaleKernel(R.CatKernel(2), L),
+          R.ScaleKernel(R.RbfKernel(0, L), L),
+          R.ScaleKernel(R.ProductKernel(R.CatKernel(2), R.RbfKernel(0, L)), L),
+          R.ScaleKernel(R.ProductKernel(R.CatKernel(3), R.RbfKernel(0, L)), L),
+          R.ScaleKernel(R.ProductKernel(R.CatKernel(4), R.RbfKernel(1, L)), L)]
+    return R.AdditiveKernel(ks)
+
+
+def randomise(module, rng, lo_s=0.3, hi_s=1.5, lo_l=1.0, hi_l=4.0):
+    """Set every scale / lengthscale to a random constrained value (per latent dim)."""
+    for name, p in module.named_parameters():
+        n = p.numel()
+        if name.endswith("_log_scale"):
+            v = torch.tensor(rng.uniform(lo_s, hi_s, n))
+        elif name.endswith("_log_lengthscale"):
+            v = torch.tensor(rng.uniform(lo_l, hi_l, n))
+        else:
+            continue
+        with torch.no_grad():
+            p.copy_(torch.log(v - math.exp(-16.0)))
+
+
+def raw_params(module):
+    """Raw parameters in module traversal order, as (names, [L] arrays)."""
+    names, vals = [], []
+    for name, p in module.named_parameters():
+        names.append(name)
+        vals.append(p.detach().numpy().copy())
+    return names, vals
+
+
+def raw_grads(module):
+    return [(p.grad.detach().numpy().copy() if p.grad is not None else np.zeros(p.shape))
+            for _, p in module.named_parameters()]
+
+
+def save(name, **arrs):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
+    print("wrote", path, sum(np.asarray(v).nbytes for v in arrs.values()), "bytes")
+
+
+# ----------------------------------------------------------------------------------------------
+# 1. KL_closed (elbo_functions.py:8-34), per latent dim, value + autograd grads
+# ----------------------------------------------------------------------------------------------
+def gen_kl_closed(P, T, L, seed, noise, store_gram):
+    rng = np.random.default_rng(seed)
+    X = covariates(P, T, seed)
+    N = P * T
+    mu = rng.standard_normal((N, L))
+    logv = 0.1 * rng.standard_normal((N, L))
+    out = dict(X=X, mu=mu, logv=logv, noise=np.full(L, noise), P=P, T=T, L=L)
+    kls, dmus, dlogvs, draws, grams, rawvals = [], [], [], [], [], []
+    for l in range(L):
+        k = full_kernel_ref(1)
+        randomise(k, rng)
+        names, vals = raw_params(k)
+        rawvals.append(np.concatenate(vals))
+        x = torch.tensor(X)
+        m_ = torch.tensor(mu[:, l], requires_grad=True)
+        lv_ = torch.tensor(logv[:, l], requires_grad=True)
+        lik = LikStub(torch.tensor([noise]))
+        kl = EF.KL_closed(KernelAdapter(k), x, lik, x, m_, lv_)
+        kl.backward()
+        kls.append(kl.item())
+        dmus.append(m_.grad.numpy().copy())
+        dlogvs.append(lv_.grad.numpy().copy())
+        draws.append(np.concatenate(raw_grads(k)))
+        if store_gram:
+            with torch.no_grad():
+                grams.append(k(x, x).numpy().copy())
+    out.update(kl=np.array(kls), dmu=np.stack(dmus, 1), dlogv=np.stack(dlogvs, 1),
+               raw=np.stack(rawvals), draw=np.stack(draws), param_names=np.array(names))
+    if store_gram:
+        out["gram"] = np.stack(grams)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# 2. minibatch_KLD_upper_bound (elbo_functions.py:144-216) + _iter (219-307)
+# ----------------------------------------------------------------------------------------------
+def batched_kernels(L):
+    return R.generate_kernel_batched(L, CFG['cat_kernel'], CFG['bin_kernel'], CFG['sqexp_kernel'],
+                                     CFG['cat_int_kernel'], CFG['bin_int_kernel'],
+                                     CFG['covariate_missing_val'], CFG['id_covariate'])
+
+
+def gen_hensman(P_tot, T, L, M, P_b, seed, natural_gradient, benign=False, noise=1.0):
+    rng = np.random.default_rng(seed)
+    X = covariates(P_tot, T, seed)
+    N = P_tot * T
+    k0, k1 = batched_kernels(L)
+    randomise(k0, rng)
+    randomise(k1, rng)
+    perm = rng.permutation(P_tot)[:P_b]
+    idx = np.concatenate([np.arange(T * s, T * (s + 1)) for s in perm])
+    xb = X[idx]
+    half = M // 2
+    zrows = np.concatenate([np.arange(0, half), np.arange(N // 2, N // 2 + half)])
+    Z = np.stack([X[zrows]] * L)
+    B = P_b * T
+    mu = rng.standard_normal((B, L))
+    logv = 0.1 * rng.standard_normal((B, L))
+    if benign:
+        m = np.zeros((L, M, 1))
+        with torch.no_grad():
+            H = KernelAdapter(k0)(torch.tensor(Z), torch.tensor(Z)).evaluate().numpy().copy()
+        H = H + 1e-6 * np.eye(M)
+    else:
+        m = rng.standard_normal((L, M, 1))
+        Hr = rng.standard_normal((L, M, M)) / 10
+        H = Hr @ np.transpose(Hr, (0, 2, 1))
+    noise_v = np.full((L, 1), noise)
+    out = dict(X_all=X, idx=idx, Z=Z, mu=mu, logv=logv, m=m, H=H, noise=noise_v, P_tot=P_tot,
+               P_b=P_b, T=T, L=L, M=M, natural_gradient=int(natural_gradient), eps=1e-6)
+    n0, v0 = raw_params(k0)
+    n1, v1 = raw_params(k1)
+    out.update(raw0=np.stack(v0, 0), raw1=np.stack(v1, 0), names0=np.array(n0), names1=np.array(n1))
+
+    def run(iter_variant):
+        for p in list(k0.parameters()) + list(k1.parameters()):
+            p.grad = None
+        mu_t = torch.tensor(mu, requires_grad=True)
+        lv_t = torch.tensor(logv, requires_grad=True)
+        m_t = torch.tensor(m, requires_grad=not natural_gradient)
+        H_t = torch.tensor(H, requires_grad=not natural_gradient)
+        lik = LikStub(torch.tensor(noise_v))
+        if iter_variant:
+            kld, gm, gH = EF.minibatch_KLD_upper_bound_iter(
+                KernelAdapter(k0), KernelAdapter(k1), lik, L, m_t, H_t,
+                torch.tensor(xb), mu_t, lv_t, torch.tensor(Z), P_tot, P_b, P_tot * T, natural_gradient, 2, 1e-6)
+        else:
+            kld, gm, gH = EF.minibatch_KLD_upper_bound(
+                KernelAdapter(k0), KernelAdapter(k1), lik, L, m_t, H_t, torch.tensor(xb), mu_t, lv_t,
+                torch.tensor(Z), P_tot, P_b, T, natural_gradient, 1e-6)
+        kld.sum().backward()
+        res = dict(kld=kld.detach().numpy().reshape(-1)[0], dmu=mu_t.grad.numpy().copy(),
+                   dlogv=lv_t.grad.numpy().copy(), draw0=np.stack(raw_grads(k0)),
+                   draw1=np.stack(raw_grads(k1)))
+        if natural_gradient:
+            res["grad_m"] = gm.detach().numpy().copy()
+            res["grad_H"] = gH.detach().numpy().copy()
+        else:
+            res["dm"] = m_t.grad.numpy().copy()
+            res["dH"] = H_t.grad.numpy().copy()
+        return res
+
+    r = run(False)
+    out.update(r)
+    r_it = run(True)
+    out["kld_iter"] = r_it["kld"]
+    if natural_gradient:
+        out["grad_m_iter"] = r_it["grad_m"]
+        out["grad_H_iter"] = r_it["grad_H"]
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# 3. per-dim GPapprox: elbo (36-84) and deviance_upper_bound (86-142)
+# ----------------------------------------------------------------------------------------------
+def gen_gpapprox(P, T, M, seed, noise=1.0):
+    rng = np.random.default_rng(seed)
+    X = covariates(P, T, seed)
+    N = P * T
+    k0, k1 = batched_kernels(1)
+    randomise(k0, rng)
+    randomise(k1, rng)
+    half = M // 2
+    zrows = np.concatenate([np.arange(0, half), np.arange(N // 2, N // 2 + half)])
+    Z = X[zrows]
+    y = rng.standard_normal(N)
+    mu = rng.standard_normal(N)
+    logv = 0.1 * rng.standard_normal(N)
+    lik = LikStub(torch.tensor([noise]))
+    out = dict(X=X, Z=Z, y=y, mu=mu, logv=logv, noise=noise, P=P, T=T, M=M, eps=1e-6)
+    n0, v0 = raw_params(k0)
+    n1, v1 = raw_params(k1)
+    out.update(raw0=np.stack(v0), raw1=np.stack(v1))
+
+    K2 = KernelAdapter  # 2-D / 3-D inputs with [1] params broadcast identically either way
+
+    # elbo
+    for p in list(k0.parameters()) + list(k1.parameters()):
+        p.grad = None
+    y_t = torch.tensor(y, requires_grad=True)
+    el = EF.elbo(K2(k0), K2(k1), lik, torch.tensor(X), y_t, torch.tensor(Z), P, T, 1e-6)
+    el = el.reshape(-1)[0]
+    el.backward()
+    out.update(elbo=el.item(), elbo_dy=y_t.grad.numpy().copy(),
+               elbo_draw0=np.stack(raw_grads(k0)), elbo_draw1=np.stack(raw_grads(k1)))
+    # dubo
+    for p in list(k0.parameters()) + list(k1.parameters()):
+        p.grad = None
+    mu_t = torch.tensor(mu, requires_grad=True)
+    lv_t = torch.tensor(logv, requires_grad=True)
+    du = EF.deviance_upper_bound(K2(k0), K2(k1), lik, torch.tensor(X), mu_t, lv_t, torch.tensor(Z),
+                                 P, T, 1e-6)
+    du = du.reshape(-1)[0]
+    du.backward()
+    out.update(dubo=du.item(), dubo_dmu=mu_t.grad.numpy().copy(), dubo_dlogv=lv_t.grad.numpy().copy(),
+               dubo_draw0=np.stack(raw_grads(k0)), dubo_draw1=np.stack(raw_grads(k1)))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# 4. ConvVAE (VAE.py:16-162): weights from a numpy formula (regenerable), fp64
+# ----------------------------------------------------------------------------------------------
+def vae_weights(model, seed):
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for name, p in model.state_dict().items():
+        if name == "min_log_vy":
+            sd[name] = p.clone()
+        elif name == "_log_vy":
+            sd[name] = torch.tensor(0.1 * rng.standard_normal(p.shape))
+        else:
+            fan = p[0].numel() if p.dim() > 1 else p.numel()
+            sd[name] = torch.tensor(rng.standard_normal(p.shape) / math.sqrt(max(fan, 1)))
+    return sd
+
+
+def gen_vae(L, B, seed):
+    rng = np.random.default_rng(seed)
+    model = RV.ConvVAE(L, 1296, vy_init=1.0, p_input=0.0, p=0.0).double()
+    model.load_state_dict(vae_weights(model, seed))
+    model.eval()
+    x = rng.uniform(0, 1, (B, 1, 36, 36))
+    mask = rng.binomial(1, 0.75, (B, 1, 36, 36)).astype(np.float64)
+    eps = rng.standard_normal((B, L))
+    xt = torch.tensor(x)
+    mu, logv = model.encode(xt)
+    z = mu + torch.tensor(eps) * torch.exp(0.5 * logv)
+    recon = model.decode(z)
+    mse, nll = model.loss_function(recon, xt, torch.tensor(mask))
+    loss = mse.sum() + nll.sum() + (mu ** 2).sum() + logv.sum()
+    loss.backward()
+    grads = {("g_" + n): p.grad.numpy().copy() for n, p in model.named_parameters()
+             if n in ("conv1.weight", "fc1.bias", "fc211.weight", "deconv2.weight", "_log_vy")}
+    return dict(x=x, mask=mask, eps=eps, L=L, seed=seed, mu=mu.detach().numpy(),
+                logv=logv.detach().numpy(), recon=recon.detach().numpy().reshape(B, -1)[:, ::7],
+                mse=mse.detach().numpy(), nll=nll.detach().numpy(), loss=loss.item(), **grads)
+
+
+def main():
+    save("kl_closed_n64.npz", **gen_kl_closed(P=4, T=16, L=2, seed=0, noise=1.0, store_gram=True))
+    save("kl_closed_n256.npz", **gen_kl_closed(P=16, T=16, L=2, seed=1, noise=1.0, store_gram=False))
+    save("kl_closed_n96_noise.npz", **gen_kl_closed(P=6, T=16, L=1, seed=2, noise=0.7, store_gram=False))
+    save("hensman_ng.npz", **gen_hensman(P_tot=32, T=16, L=4, M=60, P_b=5, seed=3, natural_gradient=True))
+    save("hensman_ng_benign.npz", **gen_hensman(P_tot=32, T=16, L=4, M=60, P_b=5, seed=4,
+                                                natural_gradient=True, benign=True))
+    save("hensman_adam.npz", **gen_hensman(P_tot=32, T=16, L=3, M=40, P_b=4, seed=5,
+                                           natural_gradient=False, noise=0.8))
+    save("gpapprox.npz", **gen_gpapprox(P=16, T=16, M=40, seed=6))
+    save("convvae.npz", **gen_vae(L=4, B=6, seed=7))
+
+
+if __name__ == "__main__":
+    main()
