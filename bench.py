@@ -1,0 +1,190 @@
+"""Benchmark: ELBO-steps/s of the L-VAE exact-KL training step (BASELINE.json configs[2]:
+Health-MNIST-shaped N=4096 observations (P=256 subjects x T=16), L=16 latent dims, one MI355X).
+
+One step = full-batch ConvVAE forward/backward over the N images (fp32, PyTorch-ROCm) + the
+exact GP-prior KL of all L latent dims (HIP: Gram, blocked MFMA Cholesky, inverse, reductions)
+forward and backward + Adam (training.py:484-592, type_KL='closed', loss='mse').
+
+Multi-GPU (torchrun, one process per GPU): data parallel over subject mini-batches -- every rank
+runs the step on its own N-observation batch of subjects, gradients all-reduced over RCCL; weak
+scaling, value = total ELBO-steps/s over all ranks.
+
+Prints ONE JSON line on rank 0 (the driver's contract); diagnostics go to stderr.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "longitudinal-vae_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+           cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                           {'cont_covariate': 0, 'cat_covariate': 3},
+                           {'cont_covariate': 1, 'cat_covariate': 4}],
+           bin_int_kernel=[], covariate_missing_val=[])
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA peak
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(ngpu):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def cpu_baseline(P, T, L, dims_timed=1):
+    """Time the CPU oracle (fp64 torch, the reference's op sequence) on a bounded sample of the same
+    step: ConvVAE fwd/bwd on all N images + KL_closed fwd/bwd of `dims_timed` latent dims, then
+    extrapolate the KL part to L dims."""
+    from oracle import lvae_oracle as O
+    from lvae_amd.data import health_mnist_batch
+    img, mask, X = health_mnist_batch(P, T, seed=0, dtype=torch.float64)
+    torch.manual_seed(0)
+    vae = O.ConvVAE(L).double()
+    spec = O.spec_full(**CFG)
+    raw = torch.zeros(L, O.n_params(spec), dtype=torch.float64)
+    raw[:, :] = torch.log(torch.tensor(math.log(2.0)))
+    N = P * T
+    eps = torch.randn(N, L, dtype=torch.float64)
+    t0 = time.perf_counter()
+    mu, logv = vae.encode(img)
+    recon = vae.decode(mu + eps * torch.exp(0.5 * logv))
+    mse, _ = vae.loss_function(recon, img, mask)
+    mse.sum().backward(retain_graph=True)
+    t_vae = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for l in range(dims_timed):
+        r = raw[l].clone().requires_grad_()
+        m_ = mu[:, l].detach().clone().requires_grad_()
+        v_ = logv[:, l].detach().clone().requires_grad_()
+        O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_).backward()
+    t_dim = (time.perf_counter() - t0) / dims_timed
+    t_step = t_vae + L * t_dim
+    return dict(value=1.0 / t_step, unit="ELBO-steps/s", cores=torch.get_num_threads(), kind="port",
+                sample=(f"oracle fp64 torch-CPU: ConvVAE fwd/bwd on all {N} images ({t_vae:.2f} s) + KL_closed "
+                        f"fwd/bwd of {dims_timed} of {L} latent dims ({t_dim:.2f} s/dim), step = vae + L x dim "
+                        f"= {t_step:.1f} s"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--P", type=int, default=256, help="subjects per rank (N = P*T)")
+    ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--L", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-phase-timing", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = setup_dist(args.gpus)
+    dev = torch.device("cuda", local)
+    import lvae_amd as la
+    from lvae_amd import _lib
+    from lvae_amd.data import health_mnist_batch
+    from lvae_amd.steps import ClosedStep
+    from lvae_amd.vae import ConvVAE
+
+    la.set_sync_checks(False)
+    P, T, L = args.P, args.T, args.L
+    N = P * T
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(dev)
+    kernel = la.generate_kernel(**CFG, latent_dim=L).to(dev)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(dev)
+    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3)
+    img, mask, X = health_mnist_batch(P, T, seed=100 + rank, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(7 + rank)
+    eps = torch.randn(N, L, device=dev, generator=gen)
+
+    hook = None
+    if world > 1:
+        from lvae_amd.distributed import GradAllReduce
+        hook = GradAllReduce(list(vae.parameters()) + list(kernel.parameters()), world)
+    step = ClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True,
+                      grad_hook=hook)
+
+    for _ in range(args.warmup):
+        out = step(img, mask, X, eps)
+    torch.cuda.synchronize()
+    la.check_pending()
+
+    phase = {}
+    if not args.no_phase_timing:
+        _lib.prof_enable(True)
+        _lib.prof_collect()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step(img, mask, X, eps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if not args.no_phase_timing:
+        phase = _lib.prof_collect()
+        _lib.prof_enable(False)
+    la.check_pending()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    net, recon, nll, gp = [float(v) for v in out]
+    log(f"rank {rank}: last step net={net:.4f} recon={recon:.4f} gp={gp:.4f}; phases(ms total over {args.steps} "
+        f"steps)={ {k: round(v[0], 3) for k, v in phase.items() if v[1]} }")
+
+    if rank == 0:
+        ms_per_step = 1000.0 * elapsed / args.steps
+        value = world * args.steps / elapsed
+        np_ = _lib.load().lvae_kl_closed_padded_n(N)
+        res = {"metric": "ELBO-steps/sec (exact-KL L-VAE step, Health-MNIST N=4096 L=16)", "value": value,
+               "unit": "ELBO-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "fp32", "data": "synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)",
+               "config": {"workload": f"closed-form KL step, N={N} (P={P} subjects x T={T}) per rank, L={L}, "
+                                      f"R=5 additive components (config/LVAE_config_sample.txt)",
+                          "N": N, "L": L, "parallelism": f"dp{world} over subject batches"}}
+        if phase:
+            potrf_ms = phase["potrf"][0] / args.steps
+            syrk_ms = phase["syrk"][0] / args.steps
+            res["gp_cholesky_gflops"] = L * N ** 3 / 3 / (potrf_ms * 1e-3) / 1e9 if potrf_ms > 0 else None
+            res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
+            # dominant kernel: S = K^-1 V K^-1 (syrk_scaled_kernel, one launch per step):
+            # algorithmic flops per launch = L * N^2 (N+1)  (lower triangle incl. diagonal, 2 flop/FMA)
+            flops = L * N * N * (N + 1)
+            achieved = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
+            res["roofline"] = {"kernel": "syrk_scaled_kernel (K^-1 V K^-1)", "bound": "mfma",
+                               "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
+                               "traffic": None, "padded_n": int(np_)}
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(P, T, L)
+            res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

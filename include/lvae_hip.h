@@ -1,0 +1,200 @@
+/*
+ * lvae_hip.h -- C ABI of the MI355X-native Longitudinal-VAE GP-prior ELBO hot path.
+ *
+ * Every entry point is a plain C function over caller-owned device pointers: no allocation
+ * inside, no global state, all work enqueued asynchronously on the caller's hipStream_t
+ * (passed as void*).  Return value: 0 = ok, <0 = -(index of the bad argument),
+ * LVAE_ERR_LAUNCH on a HIP launch error.  Numerical failure (a non-positive-definite pivot) is
+ * NOT a return code (the call is asynchronous): it is written to the device `info` array,
+ * LAPACK-style (first failing column + 1, 0 = ok), and the Python layer raises
+ * torch.linalg.LinAlgError from it like torch.linalg.cholesky does.
+ *
+ * Reference interfaces replaced (SidRama/Longitudinal-VAE, /root/reference):
+ *   covar_module(x1, x2).evaluate()       -> lvae_gram_*            (GP_model.py:31-144,
+ *                                             kernel_gen.py:9-310, call sites elbo_functions.py:22,56,171-174)
+ *   autograd of that Gram wrt (scale, lengthscale) -> lvae_gram_bwd_*
+ *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_potrf_*, lvae_potri_*
+ *                                             (elbo_functions.py:26-29)
+ *   KL_closed forward + autograd backward -> lvae_kl_closed_fwd_f32 / _bwd_f32 (elbo_functions.py:8-34)
+ *   batched small fp64 factor + inverse   -> lvae_spd_inv_small_f64 (elbo_functions.py:176-186,
+ *                                             training.py:130-134)
+ *   minibatch_KLD_upper_bound + autograd  -> lvae_hensman_fwd_f64 / _bwd_f64 (elbo_functions.py:144-216)
+ *   natural-gradient (m, H) update        -> lvae_natgrad_update_f64 (training.py:129-135)
+ */
+#ifndef LVAE_HIP_H
+#define LVAE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LVAE_MAX_COMP 16   /* additive components per kernel                  */
+#define LVAE_MAX_FAC 4     /* product factors per component                   */
+#define LVAE_ERR_LAUNCH (-1000)
+
+/* factor kinds (GP_model.py:31-85; periodic/linear are extensions, parity unpinned) */
+enum lvae_factor_kind {
+  LVAE_CAT = 0,   /* 1[x1_d == x2_d]                                  GP_model.py:52-53 */
+  LVAE_BIN = 1,   /* 1[x1_d + x2_d == 2]                              GP_model.py:40-41 */
+  LVAE_RBF = 2,   /* exp(-(x1_d-x2_d)^2 / (2 l^2)), param l            GP_model.py:80-85 */
+  LVAE_PER = 3,   /* exp(-2 sin^2(pi|x1_d-x2_d|/p) / l^2), params l, p  (extension)       */
+  LVAE_LIN = 4    /* x1_d * x2_d                                      (extension)       */
+};
+
+/* An additive kernel: sum_r scale_r * prod_f factor_{r,f}.  Parameters are per latent dim
+ * (row-major [L, n_params], constrained values); component r's scale is params[scale_idx[r]],
+ * a factor's first parameter is params[param_idx[r][f]] (-1 when it has none). */
+typedef struct lvae_kernel_spec {
+  int32_t n_comp;
+  int32_t n_params;
+  int32_t n_fac[LVAE_MAX_COMP];
+  int32_t scale_idx[LVAE_MAX_COMP];
+  int32_t kind[LVAE_MAX_COMP][LVAE_MAX_FAC];
+  int32_t dim[LVAE_MAX_COMP][LVAE_MAX_FAC];
+  int32_t param_idx[LVAE_MAX_COMP][LVAE_MAX_FAC];
+} lvae_kernel_spec;
+
+/* Strided operand of a batched Gram: element (b, l, i, q) at
+ *   ptr[b*stride_b + l*stride_l + i*ld + q]     (stride 0 = broadcast)                       */
+typedef struct lvae_xview {
+  const double* ptr;
+  int64_t stride_b;
+  int64_t stride_l;
+  int64_t ld;
+} lvae_xview;
+
+/* ---------------------------------------------------------------------------------------- */
+/* Gram                                                                                      */
+/* ---------------------------------------------------------------------------------------- */
+
+/* out[b, l, i, j] = sum_r s_r prod_f phi(x1[b,l,i], x2[b,l,j]) + (i == j ? diag[l] : 0)
+ * for b < nb, l < L, i < n1, j < n2.  out element (b,l,i,j) at
+ * out[b*ostride_b + l*ostride_l + i*ldo + j].  diag may be NULL.  params: [L, n_params] fp64.
+ * Replaces covar_module(x1, x2).evaluate() (+ noise * I) in elbo_functions.py:22-23,171-174. */
+int lvae_gram_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1,
+                  int n2, const double* params, const double* diag, double* out, int64_t ostride_b,
+                  int64_t ostride_l, int64_t ldo, void* stream);
+int lvae_gram_f32(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1,
+                  int n2, const double* params, const double* diag, float* out, int64_t ostride_b,
+                  int64_t ostride_l, int64_t ldo, void* stream);
+
+/* Adjoint of lvae_gram_*: dparams[l, p] (+)= sum_{b,i,j} G[b,l,i,j] * d out[b,l,i,j] / d params[l,p]
+ * (diag term excluded; d/d diag is returned separately in ddiag[l] = sum_{b,i} G[b,l,i,i] when
+ * ddiag != NULL).  G strided like out.  Results are ADDED to dparams / ddiag (fp64). */
+int lvae_gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1,
+                      int n2, const double* params, const double* G, int64_t gstride_b,
+                      int64_t gstride_l, int64_t ldg, double* dparams, double* ddiag, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Regime B: exact KL over the full N x N covariance (elbo_functions.py:8-34), batched over L */
+/* latent dims, fp32 MFMA.  Covariance padded to Np = lvae_kl_closed_padded_n(n) (identity on  */
+/* the padding).                                                                            */
+/* ---------------------------------------------------------------------------------------- */
+int lvae_kl_closed_padded_n(int n);
+/* bytes of device workspace the fwd+bwd pair needs (kept between the two calls) */
+size_t lvae_kl_closed_workspace_size(int n, int L);
+
+/* kl[l] = 1/2 (tr(K^-1 V) + mu^T K^-1 mu - n + log|K| - sum log v),  K = Gram_l(x, x) + noise_l I.
+ * x: [n, ldx] fp64 covariates; mu, logv: element (i, l) at mu[i*ld_mu + l] (fp64);
+ * params [L, n_params] fp64; noise [L] fp64; kl [L] fp64; info [L] int32.
+ * workspace: lvae_kl_closed_workspace_size(n, L) bytes, 256-B aligned.
+ * need_bwd = 0 skips the K^-1 assembly the backward needs.                                  */
+int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                           const double* params, const double* noise, const double* mu, const double* logv,
+                           int ld_mu, double* kl, int32_t* info, void* workspace, int need_bwd,
+                           void* stream);
+
+/* Backward of lvae_kl_closed_fwd_f32 given dL/dkl[l] = gkl[l]:
+ *   dmu[i,l] = gkl_l (K^-1 mu)_i,  dlogv[i,l] = gkl_l/2 (v_i (K^-1)_ii - 1),
+ *   dparams[l,:] = gkl_l sum_ij G_ij dK_ij/dparams,  dnoise[l] = gkl_l tr(G),
+ *   G = 1/2 (K^-1 - K^-1 V K^-1 - K^-1 mu mu^T K^-1).
+ * Outputs are OVERWRITTEN.  Workspace must be the one the forward filled.                   */
+int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                           const double* params, const double* mu, const double* logv, int ld_mu,
+                           const double* gkl, double* dmu, double* dlogv, double* dparams, double* dnoise,
+                           void* workspace, void* stream);
+
+/* Cholesky of L padded SPD matrices (in place, lower, fp32 MFMA), writing also the inverse of
+ * each 128x128 diagonal block into W's diagonal blocks, log|A_l| into logdet[l] and info[l].
+ * A, W: [L, np, np] row-major, np a multiple of 128.  Replaces torch.cholesky (elbo_functions.py:26). */
+int lvae_potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, void* stream);
+/* W = L^-1 (lower) from the factor in A and the diagonal-block inverses potrf left in W;
+ * then Ainv = L^-T L^-1 (full symmetric).  Replaces cholesky_solve(I, L) (elbo_functions.py:27-28). */
+int lvae_potri_f32(int np_, int L, const float* A, float* W, float* Ainv, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Regime A: Hensman SVI, fp64 (elbo_functions.py:144-216; training.py:129-135)             */
+/* ---------------------------------------------------------------------------------------- */
+
+/* Batched SPD factor + inverse of small matrices (n <= 128), one workgroup per matrix:
+ * Ainv[b] = A[b]^-1, logdet[b] = log|A[b]|, info[b].  A, Ainv element (b,i,j) at [b*stride + i*n + j]. */
+int lvae_spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double* Ainv,
+                           int64_t stride_out, double* logdet, int32_t* info, void* stream);
+
+/* Batched small fp64 GEMM: C[b] = alpha op(A[b]) op(B[b]) + beta C[b],
+ * with b = (b1, b2), b1 < nb1, b2 < nb2, offsets b1*s?1 + b2*s?2.  op = transpose when t? != 0. */
+int lvae_gemm_small_f64(int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda,
+                        int64_t sa1, int64_t sa2, const double* B, int ldb, int64_t sb1, int64_t sb2,
+                        double beta, double* C, int ldc, int64_t sc1, int64_t sc2, int nb1, int nb2,
+                        void* stream);
+
+/* Hensman bound sizes: L latent dims, M inducing points, P_b subjects x T time points, Q covariates */
+typedef struct lvae_hensman_dims {
+  int32_t L, M, P_b, T, Q;
+  double P_tot;            /* subjects in the data set (scale P_tot / P_b)                     */
+  double eps;              /* jitter on K0zz                                                   */
+  int32_t natural_gradient;
+} lvae_hensman_dims;
+
+size_t lvae_hensman_workspace_size(const lvae_hensman_dims* d);
+
+/* Forward of minibatch_KLD_upper_bound: kld (scalar, sum over L), grad_m [L,M], grad_H [L,M,M]
+ * (natural_gradient only; may be NULL otherwise).  x [P_b*T, Q], z [L, M, Q], m [L, M], H [L, M, M],
+ * mu / logv [P_b*T, L] (fp64, row-major), params0 [L, P0], params1 [L, P1], noise [L].          */
+int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1,
+                         const lvae_hensman_dims* d, const double* x, const double* z, const double* m,
+                         const double* H, const double* mu, const double* logv, const double* params0,
+                         const double* params1, const double* noise, double* kld, double* grad_m,
+                         double* grad_H, int32_t* info, void* workspace, void* stream);
+
+/* Backward given dL/dkld = *gkld (device scalar): dmu, dlogv [P_b*T, L]; dparams0 [L,P0],
+ * dparams1 [L,P1], dnoise [L]; dm [L,M], dH [L,M,M] when !natural_gradient (else may be NULL).
+ * Outputs are OVERWRITTEN.                                                                   */
+int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1,
+                         const lvae_hensman_dims* d, const double* x, const double* z, const double* m,
+                         const double* H, const double* mu, const double* logv, const double* params0,
+                         const double* params1, const double* noise, const double* gkld, double* dmu,
+                         double* dlogv, double* dparams0, double* dparams1, double* dnoise, double* dm,
+                         double* dH, void* workspace, void* stream);
+
+/* Natural-gradient update of the inducing posterior (training.py:129-135), in place:
+ *   iH' = H^-1 + lr (gH + gH^T);  H <- iH'^-1;  m <- H (H^-1 m - lr (gm - 2 gH m)).
+ * workspace: lvae_natgrad_workspace_size(L, M) bytes.                                        */
+size_t lvae_natgrad_workspace_size(int L, int M);
+int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m,
+                            const double* grad_H, double lr, int32_t* info, void* workspace, void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Phase timing (profiling aid; the only process-wide state of the library).  When enabled, */
+/* the composite entry points bracket their phases with hipEvents on the caller's stream;  */
+/* lvae_prof_collect synchronises on them, ADDS each phase's elapsed ms into ms[phase],    */
+/* the number of bracketed intervals into count[phase], and forgets them.                  */
+/* ---------------------------------------------------------------------------------------- */
+enum lvae_phase {
+  LVAE_PH_GRAM = 0, LVAE_PH_POTRF = 1, LVAE_PH_POTRI = 2, LVAE_PH_KL_REDUCE = 3, LVAE_PH_SYRK = 4,
+  LVAE_PH_GRAM_BWD = 5, LVAE_PH_BWD_ELEM = 6, LVAE_PH_HENSMAN_FWD = 7, LVAE_PH_HENSMAN_BWD = 8,
+  LVAE_PH_NATGRAD = 9, LVAE_N_PHASES = 10
+};
+int lvae_prof_enable(int on);
+int lvae_prof_collect(double* ms, int32_t* count, int n_phases);
+
+/* library identification: "lvae_hip <version> gfx950" */
+const char* lvae_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LVAE_HIP_H */

@@ -1,0 +1,367 @@
+// gram.hip -- additive-kernel Gram assembly and its adjoint (GP_model.py:31-144; kernel_gen.py:9-310).
+//
+// Forward: one 256-thread workgroup per 64x64 output tile of one (batch, latent-dim) slice; the two
+// covariate row blocks are staged in LDS (coalesced fp64 reads of the [n, Q] index arrays), each
+// thread produces 16 elements of one column (consecutive lanes -> consecutive columns, so the
+// stores are coalesced).  The Gram is HBM-write-bound: per element 4 B (f32) / 8 B (f64) out.
+#include "common.hpp"
+
+namespace lvae {
+
+constexpr int kGT = 64;     // Gram tile edge
+constexpr int kMaxQ = 32;   // staged covariate columns
+
+template <int MC, int MF, typename T>
+__global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lvae_xview x2, int L, int n1, int n2,
+                                                   int qs, const double* __restrict__ params,
+                                                   const double* __restrict__ diag, T* __restrict__ out,
+                                                   int64_t osb, int64_t osl, int64_t ldo) {
+  __shared__ double sx1[kGT * kMaxQ];
+  __shared__ double sx2[kGT * kMaxQ];
+  __shared__ T sp[64];
+  const int bl = blockIdx.z, b = bl / L, l = bl % L;
+  const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * kGT;
+  const int tid = threadIdx.x;
+  if (tid < s.n_params) sp[tid] = T(params[(int64_t)l * s.n_params + tid]);
+  const double* p1 = x1.ptr + b * x1.stride_b + l * x1.stride_l;
+  const double* p2 = x2.ptr + b * x2.stride_b + l * x2.stride_l;
+  for (int e = tid; e < kGT * qs; e += 256) {
+    const int r = e / qs, q = e % qs;
+    sx1[r * kMaxQ + q] = (i0 + r < n1) ? p1[(int64_t)(i0 + r) * x1.ld + q] : 0.0;
+    sx2[r * kMaxQ + q] = (j0 + r < n2) ? p2[(int64_t)(j0 + r) * x2.ld + q] : 0.0;
+  }
+  __syncthreads();
+  const int jj = tid & 63, j = j0 + jj;
+  if (j >= n2) return;
+  const T dg = diag ? T(diag[l]) : T(0);
+  T* o = out + b * osb + l * osl;
+#pragma unroll 4
+  for (int k = 0; k < kGT / 4; ++k) {
+    const int ii = (tid >> 6) + 4 * k, i = i0 + ii;
+    if (i >= n1) continue;
+    T v = kernel_eval<MC, MF, T>(s, &sx1[ii * kMaxQ], &sx2[jj * kMaxQ], sp);
+    if (i == j) v += dg;
+    o[(int64_t)i * ldo + j] = v;
+  }
+}
+
+// Adjoint, generic strided G (fp64): one workgroup per latent dim (deterministic; the
+// Hensman-sized Grams are a few 10^4 elements), accumulating per-slot sums then reducing.
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void gram_bwd_kernel(DevSpec s, lvae_xview x1, lvae_xview x2, int nb, int L,
+                                                       int n1, int n2, const double* __restrict__ params,
+                                                       const double* __restrict__ G, int64_t gsb, int64_t gsl,
+                                                       int64_t ldg, double* __restrict__ dparams,
+                                                       double* __restrict__ ddiag) {
+  __shared__ double sp[64];
+  __shared__ double red[4];
+  const int l = blockIdx.x, tid = threadIdx.x;
+  if (tid < s.n_params) sp[tid] = params[(int64_t)l * s.n_params + tid];
+  __syncthreads();
+  double acc_s[MC];
+  double acc_f[MC][MF][2];
+#pragma unroll
+  for (int r = 0; r < MC; ++r) {
+    acc_s[r] = 0.0;
+#pragma unroll
+    for (int f = 0; f < MF; ++f) acc_f[r][f][0] = acc_f[r][f][1] = 0.0;
+  }
+  double dd = 0.0;
+  const int64_t per_b = (int64_t)n1 * n2, total = per_b * nb;
+  for (int64_t e = tid; e < total; e += 256) {
+    const int b = (int)(e / per_b);
+    const int64_t rem = e - b * per_b;
+    const int i = (int)(rem / n2), j = (int)(rem - (int64_t)i * n2);
+    const double g = G[b * gsb + l * gsl + i * ldg + j];
+    if (g == 0.0) continue;
+    const double* xi = x1.ptr + b * x1.stride_b + l * x1.stride_l + i * x1.ld;
+    const double* xj = x2.ptr + b * x2.stride_b + l * x2.stride_l + j * x2.ld;
+    kernel_grad_acc<MC, MF, double, double>(s, xi, xj, sp, g, acc_s, acc_f);
+    if (i == j) dd += g;
+  }
+#pragma unroll
+  for (int r = 0; r < MC; ++r) {
+    const double v = block_sum<256>(acc_s[r], red);
+    if (tid == 0 && r < s.n_comp) dparams[(int64_t)l * s.n_params + s.scale_idx[r]] += v;
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const double w = block_sum<256>(acc_f[r][f][q], red);
+        if (tid == 0) {
+          const int pi = slot_param<MC, MF>(s, MC + (r * MF + f) * 2 + q);
+          if (pi >= 0) dparams[(int64_t)l * s.n_params + pi] += w;
+        }
+      }
+    }
+  }
+  if (ddiag) {
+    const double v = block_sum<256>(dd, red);
+    if (tid == 0) ddiag[l] += v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Regime B: lower-triangular tiles of the padded [np, np] covariance, f32 out, + noise on the
+// diagonal, identity on the padding rows/cols (keeps log|K| and the leading block of K^-1).
+// Tile t of the lower triangle -> (I, J), I >= J.
+// ------------------------------------------------------------------------------------------
+__device__ inline void tri_index(int t, int& I, int& J) {
+  int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  I = r;
+  J = t - r * (r + 1) / 2;
+}
+
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void gram_sq_fill_kernel(DevSpec s, const double* __restrict__ x, int ldx,
+                                                           int n, int np_, int qs,
+                                                           const double* __restrict__ params,
+                                                           const double* __restrict__ noise,
+                                                           float* __restrict__ K) {
+  __shared__ double sx1[kGT * kMaxQ];
+  __shared__ double sx2[kGT * kMaxQ];
+  __shared__ float sp[64];
+  int I, J;
+  tri_index(blockIdx.x, I, J);
+  const int l = blockIdx.y, tid = threadIdx.x;
+  const int i0 = I * kGT, j0 = J * kGT;
+  if (tid < s.n_params) sp[tid] = float(params[(int64_t)l * s.n_params + tid]);
+  for (int e = tid; e < kGT * qs; e += 256) {
+    const int r = e / qs, q = e % qs;
+    sx1[r * kMaxQ + q] = (i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
+    sx2[r * kMaxQ + q] = (j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
+  }
+  __syncthreads();
+  const float nz = float(noise[l]);
+  const int jj = tid & 63, j = j0 + jj;
+  float* o = K + (int64_t)l * np_ * np_;
+#pragma unroll 4
+  for (int k = 0; k < kGT / 4; ++k) {
+    const int ii = (tid >> 6) + 4 * k, i = i0 + ii;
+    float v;
+    if (i < n && j < n) {
+      v = kernel_eval<MC, MF, float>(s, &sx1[ii * kMaxQ], &sx2[jj * kMaxQ], sp);
+      if (i == j) v += nz;
+    } else {
+      v = (i == j) ? 1.0f : 0.0f;
+    }
+    o[(int64_t)i * np_ + j] = v;
+  }
+}
+
+// Fused adjoint for the exact KL: per lower 64x64 tile, G = 1/2 (Kinv - S - a a^T) is formed on the
+// fly from the symmetric K^-1 (f32), S = K^-1 V K^-1 (f32, lower tiles) and a = K^-1 mu (f64);
+// per-slot partial sums of sum_ij w_ij G_ij dK_ij/dtheta go to part[l][tile][slot]
+// (w = 2 strictly below the diagonal, 1 on it).  Slot NS-1 holds sum_i G_ii (noise).
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double* __restrict__ x, int ldx, int n,
+                                                         int np_, int qs, const double* __restrict__ params,
+                                                         const float* __restrict__ Kinv,
+                                                         const float* __restrict__ S,
+                                                         const double* __restrict__ alpha,
+                                                         double* __restrict__ part, int ntiles) {
+  constexpr int NS = MC + MC * MF * 2 + 1;
+  __shared__ double sx1[kGT * kMaxQ];
+  __shared__ double sx2[kGT * kMaxQ];
+  __shared__ float sp[64];
+  __shared__ double sa1[kGT], sa2[kGT];
+  int I, J;
+  tri_index(blockIdx.x, I, J);
+  const int l = blockIdx.y, tid = threadIdx.x;
+  const int i0 = I * kGT, j0 = J * kGT;
+  if (tid < s.n_params) sp[tid] = float(params[(int64_t)l * s.n_params + tid]);
+  for (int e = tid; e < kGT * qs; e += 256) {
+    const int r = e / qs, q = e % qs;
+    sx1[r * kMaxQ + q] = (i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
+    sx2[r * kMaxQ + q] = (j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
+  }
+  if (tid < kGT) sa1[tid] = alpha[(int64_t)l * np_ + i0 + tid];
+  else if (tid < 2 * kGT) sa2[tid - kGT] = alpha[(int64_t)l * np_ + j0 + tid - kGT];
+  __syncthreads();
+  float acc_s[MC];
+  float acc_f[MC][MF][2];
+#pragma unroll
+  for (int r = 0; r < MC; ++r) {
+    acc_s[r] = 0.f;
+#pragma unroll
+    for (int f = 0; f < MF; ++f) acc_f[r][f][0] = acc_f[r][f][1] = 0.f;
+  }
+  float dd = 0.f;
+  const int jj = tid & 63, j = j0 + jj;
+  const float* ki = Kinv + (int64_t)l * np_ * np_;
+  const float* si = S + (int64_t)l * np_ * np_;
+#pragma unroll 2
+  for (int k = 0; k < kGT / 4; ++k) {
+    const int ii = (tid >> 6) + 4 * k, i = i0 + ii;
+    if (i >= n || j >= n || j > i) continue;
+    const int64_t o = (int64_t)i * np_ + j;
+    float g = 0.5f * (ki[o] - si[o] - float(sa1[ii] * sa2[jj]));
+    if (i == j) dd += g;
+    else g *= 2.f;
+    kernel_grad_acc<MC, MF, float, float>(s, &sx1[ii * kMaxQ], &sx2[jj * kMaxQ], sp, g, acc_s, acc_f);
+  }
+  // wave shuffle per slot -> LDS [4][NS] -> one thread per slot sums the 4 waves
+  __shared__ double wred[4][NS];
+  const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int r = 0; r < MC; ++r) {
+    const double v = wave_sum((double)acc_s[r]);
+    if (lane == 0) wred[w][r] = v;
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const double u = wave_sum((double)acc_f[r][f][q]);
+        if (lane == 0) wred[w][MC + (r * MF + f) * 2 + q] = u;
+      }
+    }
+  }
+  {
+    const double v = wave_sum((double)dd);
+    if (lane == 0) wred[w][NS - 1] = v;
+  }
+  __syncthreads();
+  double* out = part + ((int64_t)l * ntiles + blockIdx.x) * NS;
+  for (int sl = tid; sl < NS; sl += 256) out[sl] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
+}
+
+// Reduce the tile partials: dparams[l, :] = gkl[l] * sum over tiles (slot -> param), dnoise[l].
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void kl_gram_bwd_reduce(DevSpec s, const double* __restrict__ part, int ntiles,
+                                                          const double* __restrict__ gkl,
+                                                          double* __restrict__ dparams,
+                                                          double* __restrict__ dnoise) {
+  constexpr int NS = MC + MC * MF * 2 + 1;
+  __shared__ double red[4];
+  const int l = blockIdx.x, tid = threadIdx.x;
+  const double g = gkl[l];
+  for (int p = tid; p < s.n_params; p += 256) dparams[(int64_t)l * s.n_params + p] = 0.0;
+  __syncthreads();
+  for (int slot = 0; slot < NS; ++slot) {
+    double v = 0.0;
+    for (int t = tid; t < ntiles; t += 256) v += part[((int64_t)l * ntiles + t) * NS + slot];
+    v = block_sum<256>(v, red);
+    if (tid == 0) {
+      if (slot == NS - 1) {
+        if (dnoise) dnoise[l] = g * v;
+      } else {
+        const int pi = slot_param<MC, MF>(s, slot);
+        if (pi >= 0) dparams[(int64_t)l * s.n_params + pi] += g * v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+static int spec_qs(const lvae_kernel_spec* s) {
+  int q = 0;
+  for (int r = 0; r < s->n_comp; ++r)
+    for (int f = 0; f < s->n_fac[r]; ++f) q = s->dim[r][f] + 1 > q ? s->dim[r][f] + 1 : q;
+  return q;
+}
+
+template <typename T>
+static int gram_launch(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
+                       const double* params, const double* diag, T* out, int64_t osb, int64_t osl, int64_t ldo,
+                       void* stream) {
+  const int bucket = spec_bucket(spec);
+  if (!bucket) return -1;
+  const int qs = spec_qs(spec);
+  if (qs > kMaxQ) return -1;
+  if (nb < 1 || L < 1 || n1 < 0 || n2 < 0) return -4;
+  if (n1 == 0 || n2 == 0) return 0;
+  const DevSpec ds = to_dev(spec);
+  dim3 grid(cdiv(n2, kGT), cdiv(n1, kGT), nb * L), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (bucket == 1)
+    gram_kernel<8, 2, T><<<grid, block, 0, st>>>(ds, x1, x2, L, n1, n2, qs, params, diag, out, osb, osl, ldo);
+  else
+    gram_kernel<16, 4, T><<<grid, block, 0, st>>>(ds, x1, x2, L, n1, n2, qs, params, diag, out, osb, osl, ldo);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                 const double* params, const double* noise, float* K, hipStream_t st) {
+  const int bucket = spec_bucket(spec);
+  const int qs = spec_qs(spec);
+  if (!bucket || qs > kMaxQ || qs > ldx) return -1;
+  const DevSpec ds = to_dev(spec);
+  const int nt = np_ / kGT;
+  dim3 grid(nt * (nt + 1) / 2, L);
+  if (bucket == 1)
+    gram_sq_fill_kernel<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K);
+  else
+    gram_sq_fill_kernel<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t kl_gram_bwd_partials_bytes(int np_, int L) {
+  const int nt = np_ / kGT;
+  return (size_t)L * (nt * (nt + 1) / 2) * (16 + 16 * 4 * 2 + 1) * sizeof(double);
+}
+
+int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
+                double* part, double* dparams, double* dnoise, hipStream_t st) {
+  const int bucket = spec_bucket(spec);
+  const int qs = spec_qs(spec);
+  if (!bucket || qs > kMaxQ) return -1;
+  const DevSpec ds = to_dev(spec);
+  const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2;
+  dim3 grid(ntiles, L);
+  if (bucket == 1) {
+    kl_gram_bwd_tiles<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part, ntiles);
+    kl_gram_bwd_reduce<8, 2><<<L, 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
+  } else {
+    kl_gram_bwd_tiles<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part, ntiles);
+    kl_gram_bwd_reduce<16, 4><<<L, 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
+                 const double* params, const double* G, int64_t gsb, int64_t gsl, int64_t ldg, double* dparams,
+                 double* ddiag, hipStream_t st) {
+  const int bucket = spec_bucket(spec);
+  if (!bucket) return -1;
+  if (nb < 1 || L < 1) return -4;
+  const DevSpec ds = to_dev(spec);
+  if (bucket == 1)
+    gram_bwd_kernel<8, 2><<<L, 256, 0, st>>>(ds, x1, x2, nb, L, n1, n2, params, G, gsb, gsl, ldg, dparams, ddiag);
+  else
+    gram_bwd_kernel<16, 4><<<L, 256, 0, st>>>(ds, x1, x2, nb, L, n1, n2, params, G, gsb, gsl, ldg, dparams, ddiag);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace lvae
+
+extern "C" {
+
+int lvae_gram_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
+                  const double* params, const double* diag, double* out, int64_t osb, int64_t osl, int64_t ldo,
+                  void* stream) {
+  return lvae::gram_launch<double>(spec, x1, x2, nb, L, n1, n2, params, diag, out, osb, osl, ldo, stream);
+}
+
+int lvae_gram_f32(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
+                  const double* params, const double* diag, float* out, int64_t osb, int64_t osl, int64_t ldo,
+                  void* stream) {
+  return lvae::gram_launch<float>(spec, x1, x2, nb, L, n1, n2, params, diag, out, osb, osl, ldo, stream);
+}
+
+int lvae_gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
+                      const double* params, const double* G, int64_t gsb, int64_t gsl, int64_t ldg, double* dparams,
+                      double* ddiag, void* stream) {
+  return lvae::gram_bwd_f64(spec, x1, x2, nb, L, n1, n2, params, G, gsb, gsl, ldg, dparams, ddiag,
+                            (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+// kl_closed.hip -- exact GP-prior KL of the Longitudinal-VAE (elbo_functions.py:8-34), forward and
+// analytic backward, batched over the L latent dims (replaces the Python loop at training.py:515-522).
+//
+//   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
+//   K_l = L L^T, logdet                           (potrf_f32, MFMA)
+//   W = L^-1, K^-1 = W^T W                        (potri_f32, MFMA)
+//   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation)
+//   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
+// backward (dL/dkl_l = g_l):
+//   S = K^-1 V K^-1                                (syrk_scaled_f32, MFMA, lower tiles)
+//   G = 1/2 (K^-1 - S - a a^T) -> dtheta, dnoise   (kl_gram_bwd, fused, never materialised)
+//   dmu = g a,  dlogv = g/2 (v d - 1)
+#include "common.hpp"
+#include "prof.hpp"
+
+namespace lvae {
+
+int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                 const double* params, const double* noise, float* K, hipStream_t st);
+size_t kl_gram_bwd_partials_bytes(int np_, int L);
+int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
+                double* part, double* dparams, double* dnoise, hipStream_t st);
+int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, hipStream_t st);
+int potri_f32(int np_, int L, const float* A, float* W, float* Ainv, hipStream_t st);
+int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st);
+
+struct KLWorkspace {
+  float *A, *W, *Kinv, *v;
+  double *mu, *alpha, *kdiag, *logdet, *part;
+  size_t bytes;
+  KLWorkspace(char* base, int np_, int L) {
+    size_t off = 0;
+    auto take = [&](size_t b) {
+      char* p = base ? base + off : nullptr;
+      off += align256(b);
+      return p;
+    };
+    const size_t mat = (size_t)L * np_ * np_ * sizeof(float);
+    A = (float*)take(mat);
+    W = (float*)take(mat);
+    Kinv = (float*)take(mat);
+    v = (float*)take((size_t)L * np_ * sizeof(float));
+    mu = (double*)take((size_t)L * np_ * sizeof(double));
+    alpha = (double*)take((size_t)L * np_ * sizeof(double));
+    kdiag = (double*)take((size_t)L * np_ * sizeof(double));
+    logdet = (double*)take((size_t)L * sizeof(double));
+    part = (double*)take(kl_gram_bwd_partials_bytes(np_, L));
+    bytes = off;
+  }
+};
+
+// mu / v into contiguous per-dim vectors (zero on the padding)
+__global__ void kl_prep_kernel(const double* __restrict__ mu, const double* __restrict__ logv, int ld, int n, int np_,
+                               int L, double* __restrict__ muc, float* __restrict__ v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, l = blockIdx.y;
+  if (i >= np_) return;
+  const bool in = i < n;
+  muc[(int64_t)l * np_ + i] = in ? mu[(int64_t)i * ld + l] : 0.0;
+  v[(int64_t)l * np_ + i] = in ? (float)exp(logv[(int64_t)i * ld + l]) : 0.f;
+}
+
+// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]
+__global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ muc,
+                                                       int np_, double* __restrict__ alpha,
+                                                       double* __restrict__ kdiag) {
+  const int l = blockIdx.y, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= np_) return;
+  const float* row = Kinv + (int64_t)l * np_ * np_ + (int64_t)i * np_;
+  const double* m = muc + (int64_t)l * np_;
+  double acc = 0.0;
+  for (int j = lane * 4; j < np_; j += 256) {
+    const float4 k4 = *reinterpret_cast<const float4*>(row + j);
+    acc += (double)k4.x * m[j] + (double)k4.y * m[j + 1] + (double)k4.z * m[j + 2] + (double)k4.w * m[j + 3];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    alpha[(int64_t)l * np_ + i] = acc;
+    kdiag[(int64_t)l * np_ + i] = (double)row[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void kl_finalize_kernel(const double* __restrict__ muc, const double* __restrict__ logv,
+                                                          int ld, const double* __restrict__ alpha,
+                                                          const double* __restrict__ kdiag,
+                                                          const double* __restrict__ logdet, int n, int np_,
+                                                          double* __restrict__ kl) {
+  __shared__ double red[4];
+  const int l = blockIdx.x, tid = threadIdx.x;
+  double quad = 0.0, tr = 0.0, slv = 0.0;
+  for (int i = tid; i < n; i += 256) {
+    const double lv = logv[(int64_t)i * ld + l];
+    quad += muc[(int64_t)l * np_ + i] * alpha[(int64_t)l * np_ + i];
+    tr += exp(lv) * kdiag[(int64_t)l * np_ + i];
+    slv += lv;
+  }
+  quad = block_sum<256>(quad, red);
+  tr = block_sum<256>(tr, red);
+  slv = block_sum<256>(slv, red);
+  if (tid == 0) kl[l] = 0.5 * (tr + quad - (double)n + logdet[l] - slv);
+}
+
+__global__ void kl_bwd_elem_kernel(const double* __restrict__ logv, int ld, int n, int np_, int L,
+                                   const double* __restrict__ alpha, const double* __restrict__ kdiag,
+                                   const double* __restrict__ gkl, double* __restrict__ dmu,
+                                   double* __restrict__ dlogv) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * L) return;
+  const int i = (int)(e / L), l = (int)(e % L);
+  const double g = gkl[l];
+  dmu[(int64_t)i * ld + l] = g * alpha[(int64_t)l * np_ + i];
+  dlogv[(int64_t)i * ld + l] = 0.5 * g * (exp(logv[(int64_t)i * ld + l]) * kdiag[(int64_t)l * np_ + i] - 1.0);
+}
+
+}  // namespace lvae
+
+using namespace lvae;
+
+extern "C" {
+
+int lvae_kl_closed_padded_n(int n) { return ((n + 127) / 128) * 128; }
+
+size_t lvae_kl_closed_workspace_size(int n, int L) {
+  const int np_ = lvae_kl_closed_padded_n(n);
+  return KLWorkspace(nullptr, np_, L).bytes;
+}
+
+int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,
+                           const double* noise, const double* mu, const double* logv, int ld_mu, double* kl,
+                           int32_t* info, void* workspace, int need_bwd, void* stream) {
+  (void)need_bwd;
+  if (!spec) return -1;
+  if (!x) return -2;
+  if (n <= 0) return -4;
+  if (L <= 0) return -5;
+  if (!params) return -6;
+  if (!noise) return -7;
+  if (!mu || !logv || ld_mu < L) return -8;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -13;
+  hipStream_t st = (hipStream_t)stream;
+  const int np_ = lvae_kl_closed_padded_n(n);
+  KLWorkspace ws((char*)workspace, np_, L);
+  {
+    ProfScope ps(LVAE_PH_GRAM, st);
+    LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
+    kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v);
+  }
+  {
+    ProfScope ps(LVAE_PH_POTRF, st);
+    LVAE_TRY(potrf_f32(np_, L, ws.A, ws.W, ws.logdet, info, st));
+  }
+  {
+    ProfScope ps(LVAE_PH_POTRI, st);
+    LVAE_TRY(potri_f32(np_, L, ws.A, ws.W, ws.Kinv, st));
+  }
+  {
+    ProfScope ps(LVAE_PH_KL_REDUCE, st);
+    kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, np_, ws.alpha, ws.kdiag);
+    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,
+                           const double* mu, const double* logv, int ld_mu, const double* gkl, double* dmu,
+                           double* dlogv, double* dparams, double* dnoise, void* workspace, void* stream) {
+  (void)mu;
+  if (!spec) return -1;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -15;
+  hipStream_t st = (hipStream_t)stream;
+  const int np_ = lvae_kl_closed_padded_n(n);
+  KLWorkspace ws((char*)workspace, np_, L);
+  // S = K^-1 V K^-1 into the (no longer needed) factor buffer
+  {
+    ProfScope ps(LVAE_PH_SYRK, st);
+    LVAE_TRY(syrk_scaled_f32(np_, L, ws.Kinv, ws.v, ws.A, st));
+  }
+  {
+    ProfScope ps(LVAE_PH_GRAM_BWD, st);
+    LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, ws.A, ws.alpha, gkl, ws.part, dparams, dnoise,
+                         st));
+  }
+  {
+    ProfScope ps(LVAE_PH_BWD_ELEM, st);
+    const int64_t tot = (int64_t)n * L;
+    kl_bwd_elem_kernel<<<cdiv(tot, 256), 256, 0, st>>>(logv, ld_mu, n, np_, L, ws.alpha, ws.kdiag, gkl, dmu,
+                                                        dlogv);
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+const char* lvae_version(void) { return "lvae_hip 0.1.0 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,14 @@
+"""lvae_amd -- MI355X-native hot path of the Longitudinal-VAE (SidRama/Longitudinal-VAE).
+
+The GP-prior ELBO term (additive-kernel Gram, blocked Cholesky / inverse, KL reductions, the
+Hensman SVI bound and its natural-gradient update) runs in hand-written HIP kernels for gfx950
+behind the C ABI of include/lvae_hip.h; the conv encoder/decoder runs on PyTorch-ROCm.
+"""
+from . import _lib  # noqa: F401
+from .kernels import (AdditiveKernel, BinKernel, CatKernel, LinearKernel, PeriodicKernel,  # noqa: F401
+                      ProductKernel, RbfKernel, ScaleKernel, generate_kernel, generate_kernel_approx,
+                      generate_kernel_batched, kernel_spec_and_params)
+from .likelihoods import GaussianLikelihood  # noqa: F401
+from .elbo import KL_closed, KL_closed_batched, check_pending, set_sync_checks  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,87 @@
+"""Conv encoder / decoder of the L-VAE (VAE.py:16-162), on PyTorch-ROCm (MIOpen / hipBLASLt).
+
+Same layer names and shapes as the reference's ConvVAE so its state dicts load unchanged.  The
+reference runs it in fp64 (LVAE.py:139-140, 152); here it runs in the dtype of its parameters
+(fp32 by default: mu / logvar drift ~1e-7 relative vs fp64).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+class ConvVAE(nn.Module):
+    def __init__(self, latent_dim, num_dim=1296, vy_init=1.0, vy_fixed=False, p_input=0.2, p=0.5):
+        super().__init__()
+        self.latent_dim = latent_dim
+        self.num_dim = num_dim
+        self.p_input = p_input
+        self.p = p
+        log_vy_init = math.log(vy_init - math.exp(-8.0))
+        self._log_vy = nn.Parameter(torch.full((num_dim,), log_vy_init))
+        if vy_fixed:
+            self._log_vy.requires_grad_(False)
+        # encoder (VAE.py:44-60)
+        self.conv1 = nn.Conv2d(1, 16, kernel_size=3, stride=1, padding=1)
+        self.pool1 = nn.MaxPool2d(kernel_size=2, stride=2, padding=0)
+        self.dropout2d_1 = nn.Dropout2d(p=p)
+        self.conv2 = nn.Conv2d(16, 32, kernel_size=3, stride=1, padding=1)
+        self.pool2 = nn.MaxPool2d(kernel_size=2, stride=2, padding=0)
+        self.dropout2d_2 = nn.Dropout2d(p=p)
+        self.fc1 = nn.Linear(32 * 9 * 9, 300)
+        self.dropout1 = nn.Dropout(p=p)
+        self.fc21 = nn.Linear(300, 30)
+        self.dropout2 = nn.Dropout(p=p)
+        self.fc211 = nn.Linear(30, latent_dim)
+        self.fc221 = nn.Linear(30, latent_dim)
+        # decoder (VAE.py:62-75)
+        self.fc3 = nn.Linear(latent_dim, 30)
+        self.dropout3 = nn.Dropout(p=p)
+        self.fc31 = nn.Linear(30, 300)
+        self.dropout4 = nn.Dropout(p=p)
+        self.fc4 = nn.Linear(300, 32 * 9 * 9)
+        self.dropout2d_3 = nn.Dropout2d(p=p)
+        self.deconv1 = nn.ConvTranspose2d(32, 16, kernel_size=4, stride=2, padding=1)
+        self.dropout2d_4 = nn.Dropout2d(p=p)
+        self.deconv2 = nn.ConvTranspose2d(16, 1, kernel_size=4, stride=2, padding=1)
+        self.register_buffer("min_log_vy", torch.full((1,), -8.0))
+
+    @property
+    def vy(self):
+        return torch.exp(self.min_log_vy + F.softplus(self._log_vy - self.min_log_vy))
+
+    def encode(self, x):
+        z = self.dropout2d_1(self.pool1(F.relu(self.conv1(x))))
+        z = self.dropout2d_2(self.pool2(F.relu(self.conv2(z))))
+        h1 = self.dropout1(F.relu(self.fc1(z.reshape(-1, 32 * 9 * 9))))
+        h2 = self.dropout2(F.relu(self.fc21(h1)))
+        return self.fc211(h2), self.fc221(h2)
+
+    def decode(self, z):
+        x = self.dropout3(F.relu(self.fc3(z)))
+        x = self.dropout4(F.relu(self.fc31(x)))
+        x = F.relu(self.fc4(x))
+        x = self.dropout2d_3(x.reshape(-1, 32, 9, 9))
+        x = self.dropout2d_4(F.relu(self.deconv1(x)))
+        return torch.sigmoid(self.deconv2(x))
+
+    def sample_latent(self, mu, log_var, eps=None):
+        std = torch.exp(0.5 * log_var)
+        if eps is None:
+            eps = torch.randn_like(std)
+        return mu + eps * std
+
+    def forward(self, x, eps=None):
+        mu, log_var = self.encode(x)
+        return self.decode(self.sample_latent(mu, log_var, eps)), mu, log_var
+
+    def loss_function(self, recon_x, x, mask):
+        """(per-image masked MSE, per-image NLL) -- VAE.py:144-162."""
+        d = self.num_dim
+        se = (recon_x.reshape(-1, d) - x.reshape(-1, d)) ** 2 * mask.reshape(-1, d)
+        msum = mask.reshape(-1, d).sum(1)
+        msum = torch.where(msum == 0, torch.ones_like(msum), msum)
+        mse = se.sum(1) / msum
+        nll = se / (2 * torch.exp(self._log_vy)) + 0.5 * (math.log(2 * math.pi) + self._log_vy)
+        return mse, nll.sum(1)

@@ -1,0 +1,172 @@
+"""HIP exact-KL path (Regime B) against the oracle and the reference's golden vectors.
+
+Tolerance (north star): ELBO / KL terms within 1e-4 relative in fp32; gradients within 1e-4
+relative to their max-norm.  Everything runs through the C ABI (liblvae_hip.so).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import lvae_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+           cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                           {'cont_covariate': 0, 'cat_covariate': 3},
+                           {'cont_covariate': 1, 'cat_covariate': 4}],
+           bin_int_kernel=[], covariate_missing_val=[])
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().cpu().double().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().cpu().double().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def set_raw(module, raw_rows):
+    """raw_rows: [L, P] raw parameters in named_parameters order."""
+    ps = [p for _, p in module.named_parameters()]
+    with torch.no_grad():
+        for j, p in enumerate(ps):
+            p.copy_(torch.as_tensor(raw_rows[:, j], dtype=p.dtype))
+
+
+@pytest.mark.parametrize("name", ["kl_closed_n64.npz", "kl_closed_n256.npz", "kl_closed_n96_noise.npz"])
+def test_kl_closed_golden(hip, name):
+    import lvae_amd as la
+    g = golden(name)
+    L = int(g["L"])
+    k = la.generate_kernel(**CFG, latent_dim=L).double()
+    set_raw(k, g["raw"])
+    k = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=float(g["noise"][0])).to(DEV)
+    X = torch.tensor(g["X"], device=DEV)
+    mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+    lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+    kl = la.KL_closed_batched(k, X, lik, mu, lv)
+    kl.sum().backward()
+    assert rel(kl, g["kl"]) < 1e-4
+    assert rel(mu.grad, g["dmu"]) < 1e-4
+    assert rel(lv.grad, g["dlogv"]) < 1e-4
+    draw = torch.stack([p.grad for _, p in k.named_parameters()], 1)
+    assert rel(draw, g["draw"]) < 1e-4
+
+
+def test_kl_closed_single_dim_api(hip):
+    """Drop-in signature KL_closed(covar_module, train_x, likelihoods, data, mu, log_var)."""
+    import lvae_amd as la
+    g = golden("kl_closed_n64.npz")
+    k = la.generate_kernel(**CFG).double()
+    set_raw(k, g["raw"][:1])
+    k = k.to(DEV)
+    lik = la.GaussianLikelihood(1, noise=1.0).to(DEV)
+    X = torch.tensor(g["X"], device=DEV)
+    kl = la.KL_closed(k, X, lik, X, torch.tensor(g["mu"][:, 0], device=DEV), torch.tensor(g["logv"][:, 0], device=DEV))
+    assert abs(kl.item() - g["kl"][0]) < 1e-4 * abs(g["kl"][0])
+
+
+@pytest.mark.parametrize("P,L", [(64, 2), (13, 3), (9, 1)])  # N = 1024, 208 (padded), 144 (padded)
+def test_kl_closed_vs_oracle(hip, P, L):
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    T = 16
+    X = torch.tensor(health_mnist_covariates(P, T, seed=P))
+    gen = torch.Generator().manual_seed(P)
+    mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    k = la.generate_kernel(**CFG, latent_dim=L).double()
+    rng = np.random.default_rng(P)
+    raw = np.stack([np.log(rng.uniform(0.3, 1.5, L)) if "scale" in n else np.log(rng.uniform(1, 4, L))
+                    for n, _ in k.named_parameters()], 1)
+    set_raw(k, raw)
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    mu_d, lv_d = mu.to(DEV).requires_grad_(), lv.to(DEV).requires_grad_()
+    kl = la.KL_closed_batched(kd, X.to(DEV), lik, mu_d, lv_d)
+    (kl * torch.arange(1, L + 1, device=DEV)).sum().backward()
+    spec = O.spec_full(**CFG)
+    for l in range(L):
+        r = torch.tensor(raw[l], requires_grad=True)
+        m_, v_ = mu[:, l].clone().requires_grad_(), lv[:, l].clone().requires_grad_()
+        ref = O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_)
+        ((l + 1) * ref).backward()
+        assert rel(kl[l], ref) < 1e-4
+        assert rel(mu_d.grad[:, l], m_.grad) < 1e-4
+        assert rel(lv_d.grad[:, l], v_.grad) < 1e-4
+        draw = torch.stack([p.grad[l] for _, p in kd.named_parameters()])
+        assert rel(draw, r.grad) < 1e-4
+
+
+def test_potrf_potri(hip):
+    """Blocked MFMA Cholesky + inverse on random SPD matrices vs fp64 torch on the host."""
+    import lvae_amd as la
+    lib = hip
+    L, n = 2, 384
+    gen = torch.Generator().manual_seed(1)
+    Xm = torch.randn(L, n, n, generator=gen, dtype=torch.float64) / n ** 0.5
+    A = Xm @ Xm.transpose(1, 2) + torch.eye(n, dtype=torch.float64)
+    Ad = A.float().to(DEV).contiguous()
+    W = torch.zeros_like(Ad)
+    Ai = torch.zeros_like(Ad)
+    logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
+    info = torch.zeros(L, dtype=torch.int32, device=DEV)
+    P = la._lib
+    P.check(lib.lvae_potrf_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(logdet), P.ptr(info), P.stream_ptr()), "potrf")
+    P.check(lib.lvae_potri_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(Ai), P.stream_ptr()), "potri")
+    torch.cuda.synchronize()
+    Lref = torch.linalg.cholesky(A)
+    assert int(info.abs().sum()) == 0
+    assert rel(torch.tril(Ad.cpu()), Lref) < 1e-5
+    assert rel(torch.tril(W.cpu()), torch.linalg.inv(Lref)) < 1e-4
+    assert rel(Ai.cpu(), torch.linalg.inv(A)) < 1e-4
+    assert rel(logdet.cpu(), torch.logdet(A)) < 1e-5
+
+
+def test_not_positive_definite_raises(hip):
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    X = torch.tensor(health_mnist_covariates(4, 16), device=DEV)
+    k = la.generate_kernel(**CFG, latent_dim=1).double().to(DEV)
+    lik = la.GaussianLikelihood(1, noise=1.0).to(DEV)
+    with torch.no_grad():
+        lik._log_noise.fill_(-30.0)       # noise ~ 1e-7: rank-deficient Gram -> fp32 pivot failure
+        for _, p in k.named_parameters():
+            p.fill_(5.0)
+    mu = torch.zeros(64, 1, dtype=torch.float64, device=DEV)
+    with pytest.raises(torch.linalg.LinAlgError):
+        la.KL_closed_batched(k, X, lik, mu, mu.clone())
+
+
+def test_gram_batched_semantics(hip):
+    """covar(x1, x2).evaluate() shapes/values of the Hensman call sites (elbo_functions.py:171-174)."""
+    import lvae_amd as la
+    L, P_b, T, M = 3, 2, 16, 20
+    from lvae_amd.data import health_mnist_covariates
+    X = torch.tensor(health_mnist_covariates(P_b, T, 3))
+    Z = torch.stack([X[:M]] * L)
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    k0 = k0.double()
+    rng = np.random.default_rng(0)
+    set_raw(k0, np.log(rng.uniform(0.5, 3.0, (L, len(list(k0.parameters()))))))
+    s0, s1 = O.spec_split(**CFG, id_covariate=2)
+    _, p0 = la.kernel_spec_and_params(k0)
+    p0c = p0.detach()
+    k0 = k0.to(DEV)
+    xst = X.reshape(P_b, T, 6)
+    sx = torch.stack([xst] * L, 1)
+    for a, b, shape in [(X, Z, (L, P_b * T, M)), (Z, Z, (L, M, M)), (sx, sx, (P_b, L, T, T))]:
+        got = k0(a.to(DEV), b.to(DEV)).evaluate()
+        ref = O.gram(s0, p0c, a, b)
+        assert tuple(got.shape) == shape
+        assert rel(got, ref) < 1e-13
+    # adjoint
+    G = torch.randn(L, P_b * T, M, dtype=torch.float64)
+    k0.zero_grad()
+    (k0(X.to(DEV), Z.to(DEV)).evaluate() * G.to(DEV)).sum().backward()
+    raw = torch.stack([p.detach().cpu() for _, p in k0.named_parameters()], 1).requires_grad_()
+    (O.gram(s0, O.constrain(raw), X, Z) * G).sum().backward()
+    got = torch.stack([p.grad.cpu() for _, p in k0.named_parameters()], 1)
+    assert rel(got, raw.grad) < 1e-12
