@@ -92,11 +92,17 @@ def main():
     ap.add_argument("--P", type=int, default=256, help="subjects per rank (N = P*T)")
     ap.add_argument("--T", type=int, default=16)
     ap.add_argument("--L", type=int, default=16)
+    ap.add_argument("--regime", choices=["closed", "hensman"], default="closed",
+                    help="closed: exact-KL step (headline, configs[2]); hensman: SVI mini-batch step (configs[3])")
+    ap.add_argument("--P_b", type=int, default=5, help="hensman: subjects per batch per rank")
+    ap.add_argument("--M", type=int, default=120, help="hensman: inducing points")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-timing", action="store_true")
     args = ap.parse_args()
 
     world, rank, local = setup_dist(args.gpus)
+    if args.regime == "hensman":
+        return main_hensman(args, world, rank, local)
     dev = torch.device("cuda", local)
     import lvae_amd as la
     from lvae_amd import _lib
@@ -180,6 +186,126 @@ def main():
                                "traffic": None, "padded_n": int(np_)}
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(P, T, L)
+            res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_hensman(P, T, L, M, P_b, steps=12):
+    """The oracle's Hensman step (training.py:91-135 restated, fp64 torch-CPU) on the same shapes."""
+    from oracle import lvae_oracle as O
+    from lvae_amd.data import health_mnist_batch
+    img, mask, X = health_mnist_batch(P, T, seed=0, dtype=torch.float64)
+    torch.manual_seed(0)
+    vae = O.ConvVAE(L).double()
+    s0, s1 = O.spec_split(**CFG, id_covariate=2)
+    raw0 = torch.full((L, O.n_params(s0)), math.log(2.0), dtype=torch.float64, requires_grad=True)
+    raw1 = torch.full((L, O.n_params(s1)), math.log(2.0), dtype=torch.float64, requires_grad=True)
+    N = P * T
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
+    m = torch.zeros(L, M, 1, dtype=torch.float64)
+    H = O.gram(s0, O.constrain(raw0.detach()), z, z) + 1e-6 * torch.eye(M, dtype=torch.float64)
+    opt = torch.optim.Adam([raw0, raw1] + list(vae.parameters()), lr=1e-3)
+    noise = torch.ones(L, dtype=torch.float64)
+    B = P_b * T
+    times = []
+    for it in range(steps):
+        rows = torch.arange(B) + (it * B) % (N - B)
+        t0 = time.perf_counter()
+        eps = torch.randn(B, L, dtype=torch.float64)
+        _, _, _, m, H = O.hensman_step(vae, s0, raw0, s1, raw1, noise, m, H, img[rows], mask[rows], X[rows], z, eps,
+                                       P, T, 0.15, 0.01, opt=opt)
+        times.append(time.perf_counter() - t0)
+    t = sorted(times[2:])[len(times[2:]) // 2]
+    return dict(value=1.0 / t, unit="ELBO-steps/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"oracle fp64 torch-CPU Hensman step (L={L}, M={M}, P_b={P_b}, T={T}), median of "
+                       f"{steps - 2} steps after 2 warm-up: {1000 * t:.1f} ms/step")
+
+
+def main_hensman(args, world, rank, local):
+    """Hensman SVI training steps (training.py:91-135), data parallel over subject mini-batches."""
+    dev = torch.device("cuda", local)
+    import lvae_amd as la
+    from lvae_amd import _lib
+    from lvae_amd.data import health_mnist_batch
+    from lvae_amd.samplers import hensman_batches, SubjectSampler
+    from lvae_amd.steps import HensmanStep
+    from lvae_amd.vae import ConvVAE
+
+    la.set_sync_checks(False)
+    P, T, L, M, P_b = args.P, args.T, args.L, args.M, args.P_b
+    N = P * T
+    torch.manual_seed(1234)
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(dev)
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    k0, k1 = k0.to(dev), k1.to(dev)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(dev)
+    img, mask, X = health_mnist_batch(P, T, seed=100, device=dev)  # one data set, sharded by subject
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)  # LVAE.py:199-203 pattern
+    with torch.no_grad():
+        H = k0(z, z).evaluate() + 1e-6 * torch.eye(M, dtype=torch.float64, device=dev)
+    m = torch.zeros(L, M, 1, dtype=torch.float64, device=dev)
+    opt = torch.optim.Adam([{"params": k0.parameters()}, {"params": k1.parameters()},
+                            {"params": vae.parameters()}], lr=1e-3)
+    hook = ngr = None
+    if world > 1:
+        from lvae_amd.distributed import GradAllReduce, allreduce_tensors
+        hook = GradAllReduce(list(vae.parameters()) + list(k0.parameters()) + list(k1.parameters()), world)
+        ngr = lambda ts: allreduce_tensors(ts, average=False)
+    step = HensmanStep(vae, k0, k1, lik, opt, m, H, z, P, T, weight=0.15, natural_gradient=True,
+                       natural_gradient_lr=0.01, world=world, grad_hook=hook, ng_reduce=ngr)
+    perm = SubjectSampler(P, T, seed=0).permutation()
+    batches = [b.to(dev) for b in hensman_batches(perm, P_b, T, rank, world) if b is not None and len(b) == P_b * T]
+    gen = torch.Generator(device=dev).manual_seed(7 + rank)
+    eps = torch.randn(P_b * T, L, device=dev, generator=gen)
+
+    def run(n):
+        out = None
+        for i in range(n):
+            rows = batches[i % len(batches)]
+            out = step(img.index_select(0, rows), mask.index_select(0, rows), X.index_select(0, rows), eps)
+        return out
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    la.check_pending()
+    if not args.no_phase_timing:
+        _lib.prof_enable(True)
+        _lib.prof_collect()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    phase = {}
+    if not args.no_phase_timing:
+        phase = _lib.prof_collect()
+        _lib.prof_enable(False)
+    la.check_pending()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    log(f"rank {rank}: last step (net, recon, nll, kld) = {[round(float(v), 4) for v in out]}")
+    if rank == 0:
+        value = world * args.steps / elapsed
+        res = {"metric": "ELBO-steps/sec (Hensman SVI L-VAE step, Health-MNIST N=4096 L=16)", "value": value,
+               "unit": "ELBO-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "fp64 GP / fp32 conv",
+               "data": "synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)",
+               "config": {"workload": f"Hensman step: P_tot={P} subjects x T={T} (N={N}), L={L}, M={M}, "
+                                      f"P_b={P_b} subjects per rank per step",
+                          "samples_per_sec": value * P_b * T, "parallelism": f"dp{world} over subject batches"}}
+        if phase:
+            res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_hensman(P, T, L, M, P_b)
             res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]
         print(json.dumps(res), flush=True)
     if world > 1:

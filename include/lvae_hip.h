@@ -147,6 +147,9 @@ typedef struct lvae_hensman_dims {
   double P_tot;            /* subjects in the data set (scale P_tot / P_b)                     */
   double eps;              /* jitter on K0zz                                                   */
   int32_t natural_gradient;
+  double ng_prior_share;   /* weight of the data-independent part (iK m, iK, iH) in grad_m /   */
+                           /* grad_H: 1 for one process; 1/world under data parallelism, so a  */
+                           /* SUM all-reduce of the per-rank directions equals the union batch */
 } lvae_hensman_dims;
 
 size_t lvae_hensman_workspace_size(const lvae_hensman_dims* d);

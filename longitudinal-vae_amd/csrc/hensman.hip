@@ -1,0 +1,455 @@
+// hensman.hip -- Hensman mini-batch KL upper bound of the L-VAE (elbo_functions.py:144-216), its
+// analytic adjoint (what autograd computes through it), and the natural-gradient update of the
+// inducing posterior (training.py:129-135).  fp64 throughout; batched over the L latent dims.
+//
+// Per latent dim (B = P_b T rows, subject blocks p of T rows):
+//   K0xz = k0(x, z) [B,M]  K0zz = k0(z, z) + eps I  K0_p = k0(x_p, x_p)  B_p = k1(x_p, x_p) + noise I
+//   iK = K0zz^-1, iB_p = B_p^-1, iH = H^-1 (+ log-dets)         spd_inv_small
+//   t = iK m, r = K0xz t - mu, s = iB r, iBK = iB K0xz, Q = K0xz^T iBK, Y = iK H iK
+//   A = r.s, Bt = sum diag(iB) v, C = sum log|B_p|, D = sum iB.K0 - sum Q.iK, E = sum Y.Q, F = sum logv
+//   kl_u = 1/2 (sum iK.H + m.t - M + log|K0zz| - log|H|)
+//   kld = sum_l [P_tot/P_b 1/2 (A+Bt+C+D+E-F) + kl_u] - L P_tot T / 2
+//   natural gradient: grad_m = -iK K0xz^T iB mu + Bn m, grad_H = 1/2(-iH + Bn), Bn = iK Q iK + iK
+// Adjoint (g = dL/dkld, c = g P_tot / (2 P_b), h = g / 2):
+//   dmu = -2c s, dlogv = c (diag(iB) v - 1), Xq = c (Y - iK)
+//   dK0xz = 2c s t^T + 2 iBK Xq
+//   G_iK = c (2 (K0xz^T s) m^T - Q + Z + Z^T) + h (H + m m^T),  Z = Q iK H
+//   dK0zz = -iK G_iK iK + h iK
+//   dK0_p = c iB_p
+//   dB_p = c (iB - s s^T - iB V iB - iB K0 iB)_p - iBK_p Xq iBK_p^T
+//   (Adam path) dm = 2c iK K0xz^T s + g t,  dH = c iK Q iK + h (iK - iH)
+#include "common.hpp"
+#include "prof.hpp"
+
+namespace lvae {
+
+int gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
+                 const double* params, const double* G, int64_t gsb, int64_t gsl, int64_t ldg, double* dparams,
+                 double* ddiag, hipStream_t st);
+int spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double* Ainv, int64_t stride_out,
+                      double* logdet, int32_t* info, hipStream_t st);
+int gemm_small_f64(int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda, int64_t sa1,
+                   int64_t sa2, const double* B, int ldb, int64_t sb1, int64_t sb2, double beta, double* C, int ldc,
+                   int64_t sc1, int64_t sc2, int nb1, int nb2, hipStream_t st);
+
+namespace {
+
+struct HWs {
+  // [L,B,M]
+  double *K0xz, *iBK, *dK0xz, *tBM;
+  // [L,M,M]
+  double *K0zz, *iK, *iH, *Q, *iKH, *Y, *Xq, *Z, *GiK, *T1, *dK0zz, *Bn, *iKQ, *tMM;
+  // [L,P_b,T,T]
+  double *K0st, *Bst, *iB, *VB, *iBVB, *K0iB, *iBK0iB, *QB, *GB, *GK0;
+  // vectors
+  double *t, *v1, *w, *a, *tM;  // [L,M]
+  double *y, *r, *s, *u;        // [L,B]
+  double *ldK, *ldB, *ldH, *epsv, *part;
+  int32_t* info;
+  size_t bytes;
+  HWs(char* base, const lvae_hensman_dims& d) {
+    size_t off = 0;
+    auto take = [&](size_t n) {
+      double* p = base ? (double*)(base + off) : nullptr;
+      off += align256(n * sizeof(double));
+      return p;
+    };
+    const size_t L = d.L, M = d.M, B = (size_t)d.P_b * d.T, TT = (size_t)d.P_b * d.T * d.T;
+    K0xz = take(L * B * M); iBK = take(L * B * M); dK0xz = take(L * B * M); tBM = take(L * B * M);
+    double** mm[] = {&K0zz, &iK, &iH, &Q, &iKH, &Y, &Xq, &Z, &GiK, &T1, &dK0zz, &Bn, &iKQ, &tMM};
+    for (auto p : mm) *p = take(L * M * M);
+    double** tt[] = {&K0st, &Bst, &iB, &VB, &iBVB, &K0iB, &iBK0iB, &QB, &GB, &GK0};
+    for (auto p : tt) *p = take(L * TT);
+    double** vm[] = {&t, &v1, &w, &a, &tM};
+    for (auto p : vm) *p = take(L * M);
+    double** vb[] = {&y, &r, &s, &u};
+    for (auto p : vb) *p = take(L * B);
+    ldK = take(L);
+    ldB = take(L * d.P_b);
+    ldH = take(L);
+    epsv = take(L);
+    part = take(L * 16);
+    info = (int32_t*)take(L * (2 + d.P_b));
+    bytes = off;
+  }
+};
+
+__global__ void fill_kernel(double* p, int n, double v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// r[l][i] = y[l][i] - mu[i][l]
+__global__ void resid_kernel(const double* __restrict__ y, const double* __restrict__ mu, int B, int L,
+                             double* __restrict__ r) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * L) return;
+  const int l = e / B, i = e % B;
+  r[e] = y[e] - mu[(int64_t)i * L + l];
+}
+
+// per-dim partial sums: part[l][0..] = A, Bt, C, D1, D2, E, F, tr1, qf1, ldK, ldH
+__global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, int L, const double* __restrict__ r,
+                                                        const double* __restrict__ s, const double* __restrict__ iB,
+                                                        const double* __restrict__ logv,
+                                                        const double* __restrict__ ldB,
+                                                        const double* __restrict__ K0st,
+                                                        const double* __restrict__ Q, const double* __restrict__ iK,
+                                                        const double* __restrict__ Y, const double* __restrict__ H,
+                                                        const double* __restrict__ m, const double* __restrict__ t,
+                                                        const double* __restrict__ ldK,
+                                                        const double* __restrict__ ldH, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int l = blockIdx.x, tid = threadIdx.x;
+  const int B = P_b * T;
+  const int64_t MM = (int64_t)M * M, TT = (int64_t)P_b * T * T;
+  double A = 0, Bt = 0, C = 0, D1 = 0, D2 = 0, E = 0, F = 0, tr1 = 0, qf1 = 0;
+  for (int i = tid; i < B; i += 256) {
+    A += r[(int64_t)l * B + i] * s[(int64_t)l * B + i];
+    const int p = i / T, q = i % T;
+    const double lv = logv[(int64_t)i * L + l];
+    Bt += iB[l * TT + (int64_t)p * T * T + q * T + q] * exp(lv);
+    F += lv;
+  }
+  for (int p = tid; p < P_b; p += 256) C += ldB[(int64_t)l * P_b + p];
+  for (int64_t e = tid; e < TT; e += 256) D1 += iB[l * TT + e] * K0st[l * TT + e];
+  for (int64_t e = tid; e < MM; e += 256) {
+    const double q = Q[l * MM + e], ik = iK[l * MM + e];
+    D2 += q * ik;
+    // E = sum Y^T .* Q = sum Y .* Q (Y symmetric up to rounding: use the transposed element as the reference)
+    const int i = (int)(e / M), j = (int)(e % M);
+    E += Y[l * MM + (int64_t)j * M + i] * q;
+    tr1 += ik * H[l * MM + (int64_t)j * M + i];
+  }
+  for (int i = tid; i < M; i += 256) qf1 += m[(int64_t)l * M + i] * t[(int64_t)l * M + i];
+  double vals[9] = {A, Bt, C, D1, D2, E, F, tr1, qf1};
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const double v = block_sum<256>(vals[q], red);
+    if (tid == 0) part[l * 16 + q] = v;
+  }
+  if (tid == 0) {
+    part[l * 16 + 9] = ldK[l];
+    part[l * 16 + 10] = ldH[l];
+  }
+}
+
+__global__ void hn_final_kernel(int L, int M, double P_tot, int P_b, int T, const double* __restrict__ part,
+                                double* __restrict__ kld) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double tot = 0.0;
+  const double c0 = P_tot / (double)P_b;
+  for (int l = 0; l < L; ++l) {
+    const double* p = part + l * 16;
+    const double inner = p[0] + p[1] + p[2] + (p[3] - p[4]) + p[5] - p[6];
+    const double klu = 0.5 * (p[7] + p[8] - (double)M + p[9] - p[10]);
+    tot += c0 * 0.5 * inner + klu;
+  }
+  kld[0] = tot - (double)L * P_tot * (double)T / 2.0;
+}
+
+// y = alpha * x + beta * y  (n elements), optional scale from device scalar: alpha *= *g, beta *= *g
+__global__ void axpby_kernel(int64_t n, double alpha, const double* __restrict__ x, double beta,
+                             double* __restrict__ y, const double* __restrict__ ga, const double* __restrict__ gb) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double al = ga ? alpha * ga[0] : alpha;
+  const double be = gb ? beta * gb[0] : beta;
+  y[e] = al * x[e] + (be == 0.0 ? 0.0 : be * y[e]);
+}
+
+// z = ax * x + ay * y (+ az * w), coefficients optionally scaled by device scalar g
+__global__ void lincomb_kernel(int64_t n, double ax, const double* x, double ay, const double* y, double* z,
+                               const double* __restrict__ g,
+                               int scale_x, int scale_y) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double gg = g ? g[0] : 1.0;
+  const double cx = scale_x ? ax * gg : ax, cy = scale_y ? ay * gg : ay;
+  z[e] = cx * x[e] + (y ? cy * y[e] : 0.0);
+}
+
+// dmu[i][l] = -2c s[l][i];  dlogv[i][l] = c (iB_ii v_i - 1)
+__global__ void hn_bwd_vec_kernel(int P_b, int T, int L, double k, const double* __restrict__ g,
+                                  const double* __restrict__ s, const double* __restrict__ iB,
+                                  const double* __restrict__ logv, double* __restrict__ dmu,
+                                  double* __restrict__ dlogv) {
+  const int B = P_b * T;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * L) return;
+  const int l = e / B, i = e % B, p = i / T, q = i % T;
+  const double c = k * g[0];
+  dmu[(int64_t)i * L + l] = -2.0 * c * s[e];
+  const double d = iB[((int64_t)l * P_b + p) * T * T + q * T + q];
+  dlogv[(int64_t)i * L + l] = c * (d * exp(logv[(int64_t)i * L + l]) - 1.0);
+}
+
+// X[l][i][j] += a * u[l][i] * v[l][j]  (a scaled by device g)
+__global__ void outer_add_kernel(int L, int n1, int n2, double a, const double* __restrict__ g,
+                                 const double* __restrict__ u, const double* __restrict__ v,
+                                 double* __restrict__ X) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)L * n1 * n2) return;
+  const int l = (int)(e / ((int64_t)n1 * n2));
+  const int64_t rem = e - (int64_t)l * n1 * n2;
+  const int i = (int)(rem / n2), j = (int)(rem % n2);
+  X[e] += a * g[0] * u[(int64_t)l * n1 + i] * v[(int64_t)l * n2 + j];
+}
+
+// G_iK = c (2 v1 m^T - Q + Z + Z^T) + h (H + m m^T)
+__global__ void giK_kernel(int L, int M, double kc, double kh, const double* __restrict__ g,
+                           const double* __restrict__ v1, const double* __restrict__ m,
+                           const double* __restrict__ Q, const double* __restrict__ Z,
+                           const double* __restrict__ H, double* __restrict__ G) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MM = (int64_t)M * M;
+  if (e >= L * MM) return;
+  const int l = (int)(e / MM);
+  const int i = (int)((e % MM) / M), j = (int)(e % M);
+  const double c = kc * g[0], h = kh * g[0];
+  const double* mm = m + (int64_t)l * M;
+  const int64_t b = l * MM;
+  G[e] = c * (2.0 * v1[(int64_t)l * M + i] * mm[j] - Q[e] + Z[e] + Z[b + (int64_t)j * M + i]) +
+         h * (H[e] + mm[i] * mm[j]);
+}
+
+// VB[l,p][i][j] = v_{l,p,i} iB[l,p][i][j]
+__global__ void rowscale_v_kernel(int P_b, int T, int L, const double* __restrict__ logv,
+                                  const double* __restrict__ iB, double* __restrict__ VB) {
+  const int64_t TT = (int64_t)T * T;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)L * P_b * TT) return;
+  const int lp = (int)(e / TT), l = lp / P_b, p = lp % P_b;
+  const int i = (int)((e % TT) / T);
+  VB[e] = exp(logv[((int64_t)p * T + i) * L + l]) * iB[e];
+}
+
+// GB = c (iB - s s^T - iBVB - iBK0iB) - QB ;  GK0 = c iB
+__global__ void gb_kernel(int P_b, int T, int L, double kc, const double* __restrict__ g,
+                          const double* __restrict__ iB, const double* __restrict__ s,
+                          const double* __restrict__ iBVB, const double* __restrict__ iBK0iB,
+                          const double* __restrict__ QB, double* __restrict__ GB, double* __restrict__ GK0) {
+  const int64_t TT = (int64_t)T * T;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)L * P_b * TT) return;
+  const int lp = (int)(e / TT), l = lp / P_b, p = lp % P_b;
+  const int i = (int)((e % TT) / T), j = (int)(e % T);
+  const double c = kc * g[0];
+  const int B = P_b * T;
+  const double si = s[(int64_t)l * B + p * T + i], sj = s[(int64_t)l * B + p * T + j];
+  GB[e] = c * (iB[e] - si * sj - iBVB[e] - iBK0iB[e]) - QB[e];
+  GK0[e] = c * iB[e];
+}
+
+// Y[l][i][j] += a * X[l][j][i]
+__global__ void add_transpose_kernel(int L, int M, double a, const double* __restrict__ X, double* __restrict__ Y) {
+  const int64_t MM = (int64_t)M * M;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= L * MM) return;
+  const int64_t l = e / MM;
+  const int i = (int)((e % MM) / M), j = (int)(e % M);
+  Y[e] += a * X[l * MM + (int64_t)j * M + i];
+}
+
+// info[l]: first failure among K0zz[l] (10000 + col), B_{l,p} (20000 + col), H[l] (30000 + col)
+__global__ void hn_info_kernel(int L, int P_b, const int32_t* __restrict__ w, int32_t* __restrict__ info) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= L) return;
+  int v = 0;
+  if (w[l]) v = 10000 + w[l];
+  for (int p = 0; p < P_b && !v; ++p)
+    if (w[L + l * P_b + p]) v = 20000 + w[L + l * P_b + p];
+  if (!v && w[L + L * P_b + l]) v = 30000 + w[L + L * P_b + l];
+  info[l] = v;
+}
+
+inline int blocks(int64_t n) { return cdiv(n, 256); }
+
+}  // namespace
+
+
+
+static int hensman_check(const lvae_kernel_spec* s0, const lvae_kernel_spec* s1, const lvae_hensman_dims* d) {
+  if (!s0 || !spec_bucket(s0)) return -1;
+  if (!s1 || !spec_bucket(s1)) return -2;
+  if (!d || d->L < 1 || d->M < 1 || d->M > 128 || d->P_b < 1 || d->T < 1 || d->T > 128 || d->Q < 1) return -3;
+  return 0;
+}
+
+}  // namespace lvae
+
+using namespace lvae;
+
+extern "C" {
+
+size_t lvae_hensman_workspace_size(const lvae_hensman_dims* d) { return HWs(nullptr, *d).bytes; }
+
+int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, const lvae_hensman_dims* dp,
+                         const double* x, const double* z, const double* m, const double* H, const double* mu,
+                         const double* logv, const double* params0, const double* params1, const double* noise,
+                         double* kld, double* grad_m, double* grad_H, int32_t* info, void* workspace, void* stream) {
+  LVAE_TRY(hensman_check(spec0, spec1, dp));
+  if (!workspace || ((uintptr_t)workspace & 255)) return -17;
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope ps(LVAE_PH_HENSMAN_FWD, st);
+  const lvae_hensman_dims& d = *dp;
+  const int L = d.L, M = d.M, P_b = d.P_b, T = d.T, Q = d.Q, B = P_b * T;
+  const int64_t MM = (int64_t)M * M, TT = (int64_t)T * T, BM = (int64_t)B * M;
+  HWs w((char*)workspace, d);
+  // Grams (elbo_functions.py:171-176)
+  fill_kernel<<<blocks(L), 256, 0, st>>>(w.epsv, L, d.eps);
+  const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
+  LVAE_TRY(lvae_gram_f64(spec0, xv, zv, 1, L, B, M, params0, nullptr, w.K0xz, 0, BM, M, stream));
+  LVAE_TRY(lvae_gram_f64(spec0, zv, zv, 1, L, M, M, params0, w.epsv, w.K0zz, 0, MM, M, stream));
+  LVAE_TRY(lvae_gram_f64(spec0, xs, xs, P_b, L, T, T, params0, nullptr, w.K0st, TT, P_b * TT, T, stream));
+  LVAE_TRY(lvae_gram_f64(spec1, xs, xs, P_b, L, T, T, params1, noise, w.Bst, TT, P_b * TT, T, stream));
+  // factor + inverse (177-186)
+  LVAE_TRY(spd_inv_small_f64(M, L, w.K0zz, MM, w.iK, MM, w.ldK, w.info, st));
+  LVAE_TRY(spd_inv_small_f64(T, L * P_b, w.Bst, TT, w.iB, TT, w.ldB, w.info + L, st));
+  LVAE_TRY(spd_inv_small_f64(M, L, H, MM, w.iH, MM, w.ldH, w.info + L + L * P_b, st));
+  // t = iK m ; r = K0xz t - mu ; s = iB r ; iBK = iB K0xz ; Q = K0xz^T iBK ; Y = iK H iK
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, m, 1, M, 0, 0.0, w.t, 1, M, 0, L, 1, st));
+  LVAE_TRY(gemm_small_f64(0, 0, B, 1, M, 1.0, w.K0xz, M, BM, 0, w.t, 1, M, 0, 0.0, w.y, 1, B, 0, L, 1, st));
+  resid_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(w.y, mu, B, L, w.r);
+  LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, w.r, 1, B, T, 0.0, w.s, 1, B, T, L, P_b, st));
+  LVAE_TRY(gemm_small_f64(0, 0, T, M, T, 1.0, w.iB, T, P_b * TT, TT, w.K0xz, M, BM, (int64_t)T * M, 0.0, w.iBK, M,
+                          BM, (int64_t)T * M, L, P_b, st));
+  LVAE_TRY(gemm_small_f64(1, 0, M, M, B, 1.0, w.K0xz, M, BM, 0, w.iBK, M, BM, 0, 0.0, w.Q, M, MM, 0, L, 1, st));
+  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, H, M, MM, 0, 0.0, w.iKH, M, MM, 0, L, 1, st));
+  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKH, M, MM, 0, w.iK, M, MM, 0, 0.0, w.Y, M, MM, 0, L, 1, st));
+  // partial sums + total (189-204)
+  hn_reduce_kernel<<<L, 256, 0, st>>>(M, P_b, T, L, w.r, w.s, w.iB, logv, w.ldB, w.K0st, w.Q, w.iK, w.Y, H, m, w.t,
+                                      w.ldK, w.ldH, w.part);
+  hn_final_kernel<<<1, 64, 0, st>>>(L, M, d.P_tot, P_b, T, w.part, kld);
+  // natural-gradient directions (208-214)
+  if (d.natural_gradient && grad_m && grad_H) {
+    LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, mu, L, 1, (int64_t)T * L, 0.0, w.u, 1, B, T,
+                            L, P_b, st));
+    LVAE_TRY(gemm_small_f64(1, 0, M, 1, B, 1.0, w.K0xz, M, BM, 0, w.u, 1, B, 0, 0.0, w.w, 1, M, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, w.w, 1, M, 0, 0.0, w.a, 1, M, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, w.Q, M, MM, 0, 0.0, w.iKQ, M, MM, 0, L, 1, st));
+    // Bn = iK Q iK + share iK ; grad_m = Bn m - a ; grad_H = 1/2 (Bn - share iH)
+    const double share = d.ng_prior_share;
+    axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, share, w.iK, 0.0, w.Bn, nullptr, nullptr);
+    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKQ, M, MM, 0, w.iK, M, MM, 0, 1.0, w.Bn, M, MM, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.Bn, M, MM, 0, m, 1, M, 0, 0.0, w.tM, 1, M, 0, L, 1, st));
+    lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 1.0, w.tM, -1.0, w.a, grad_m, nullptr,
+                                                            0, 0);
+    lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 0.5, w.Bn, -0.5 * share, w.iH, grad_H, nullptr, 0, 0);
+  }
+  // info: first failing matrix (K0zz, then B_p, then H) per latent dim
+  if (info) hn_info_kernel<<<blocks(L), 256, 0, st>>>(L, P_b, w.info, info);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, const lvae_hensman_dims* dp,
+                         const double* x, const double* z, const double* m, const double* H, const double* mu,
+                         const double* logv, const double* params0, const double* params1, const double* noise,
+                         const double* gkld, double* dmu, double* dlogv, double* dparams0, double* dparams1,
+                         double* dnoise, double* dm, double* dH, void* workspace, void* stream) {
+  (void)mu;
+  (void)noise;
+  LVAE_TRY(hensman_check(spec0, spec1, dp));
+  if (!workspace || ((uintptr_t)workspace & 255)) return -21;
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope ps(LVAE_PH_HENSMAN_BWD, st);
+  const lvae_hensman_dims& d = *dp;
+  const int L = d.L, M = d.M, P_b = d.P_b, T = d.T, Q = d.Q, B = P_b * T;
+  const int64_t MM = (int64_t)M * M, TT = (int64_t)T * T, BM = (int64_t)B * M, LTT = (int64_t)L * P_b * TT;
+  const double kc = d.P_tot / (2.0 * P_b), kh = 0.5;
+  HWs w((char*)workspace, d);
+  // mu / logv
+  hn_bwd_vec_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(P_b, T, L, kc, gkld, w.s, w.iB, logv, dmu, dlogv);
+  // Xq = c (Y - iK)
+  lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, kc, w.Y, -kc, w.iK, w.Xq, gkld, 1, 1);
+  // dK0xz = 2 iBK Xq + 2c s t^T
+  LVAE_TRY(gemm_small_f64(0, 0, B, M, M, 2.0, w.iBK, M, BM, 0, w.Xq, M, MM, 0, 0.0, w.dK0xz, M, BM, 0, L, 1, st));
+  outer_add_kernel<<<blocks((int64_t)L * BM), 256, 0, st>>>(L, B, M, 2.0 * kc, gkld, w.s, w.t, w.dK0xz);
+  // v1 = K0xz^T s ; Z = Q iK H ; G_iK ; dK0zz = -iK G_iK iK + h iK
+  LVAE_TRY(gemm_small_f64(1, 0, M, 1, B, 1.0, w.K0xz, M, BM, 0, w.s, 1, B, 0, 0.0, w.v1, 1, M, 0, L, 1, st));
+  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.Q, M, MM, 0, w.iKH, M, MM, 0, 0.0, w.Z, M, MM, 0, L, 1, st));
+  giK_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, kc, kh, gkld, w.v1, m, w.Q, w.Z, H, w.GiK);
+  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, w.GiK, M, MM, 0, 0.0, w.T1, M, MM, 0, L, 1, st));
+  lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, kh, w.iK, 0.0, nullptr, w.dK0zz, gkld, 1, 0);
+  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, -1.0, w.T1, M, MM, 0, w.iK, M, MM, 0, 1.0, w.dK0zz, M, MM, 0, L, 1, st));
+  // dB_p and dK0_p
+  rowscale_v_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, logv, w.iB, w.VB);
+  LVAE_TRY(gemm_small_f64(0, 0, T, T, T, 1.0, w.iB, T, P_b * TT, TT, w.VB, T, P_b * TT, TT, 0.0, w.iBVB, T,
+                          P_b * TT, TT, L, P_b, st));
+  LVAE_TRY(gemm_small_f64(0, 0, T, T, T, 1.0, w.K0st, T, P_b * TT, TT, w.iB, T, P_b * TT, TT, 0.0, w.K0iB, T,
+                          P_b * TT, TT, L, P_b, st));
+  LVAE_TRY(gemm_small_f64(0, 0, T, T, T, 1.0, w.iB, T, P_b * TT, TT, w.K0iB, T, P_b * TT, TT, 0.0, w.iBK0iB, T,
+                          P_b * TT, TT, L, P_b, st));
+  LVAE_TRY(gemm_small_f64(0, 0, T, M, M, 1.0, w.iBK, M, BM, (int64_t)T * M, w.Xq, M, MM, 0, 0.0, w.tBM, M, BM,
+                          (int64_t)T * M, L, P_b, st));
+  LVAE_TRY(gemm_small_f64(0, 1, T, T, M, 1.0, w.tBM, M, BM, (int64_t)T * M, w.iBK, M, BM, (int64_t)T * M, 0.0, w.QB,
+                          T, P_b * TT, TT, L, P_b, st));
+  gb_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, kc, gkld, w.iB, w.s, w.iBVB, w.iBK0iB, w.QB, w.GB, w.GK0);
+  // hyper-parameter gradients through the four Grams
+  (void)hipMemsetAsync(dparams0, 0, sizeof(double) * L * spec0->n_params, st);
+  (void)hipMemsetAsync(dparams1, 0, sizeof(double) * L * spec1->n_params, st);
+  if (dnoise) (void)hipMemsetAsync(dnoise, 0, sizeof(double) * L, st);
+  const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
+  LVAE_TRY(gram_bwd_f64(spec0, xv, zv, 1, L, B, M, params0, w.dK0xz, 0, BM, M, dparams0, nullptr, st));
+  LVAE_TRY(gram_bwd_f64(spec0, zv, zv, 1, L, M, M, params0, w.dK0zz, 0, MM, M, dparams0, nullptr, st));
+  LVAE_TRY(gram_bwd_f64(spec0, xs, xs, P_b, L, T, T, params0, w.GK0, TT, P_b * TT, T, dparams0, nullptr, st));
+  LVAE_TRY(gram_bwd_f64(spec1, xs, xs, P_b, L, T, T, params1, w.GB, TT, P_b * TT, T, dparams1, dnoise, st));
+  // Adam path: gradients wrt m and H
+  if (!d.natural_gradient && dm && dH) {
+    LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, w.v1, 1, M, 0, 0.0, w.tM, 1, M, 0, L, 1, st));
+    lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 2.0 * kc, w.tM, 1.0, w.t, dm, gkld, 1, 1);
+    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, w.Q, M, MM, 0, 0.0, w.iKQ, M, MM, 0, L, 1, st));
+    lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, kh, w.iK, -kh, w.iH, dH, gkld, 1, 1);
+    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKQ, M, MM, 0, w.iK, M, MM, 0, 0.0, w.tMM, M, MM, 0, L, 1, st));
+    axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, kc, w.tMM, 1.0, dH, gkld, nullptr);
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// natural-gradient update (training.py:129-135)
+// ------------------------------------------------------------------------------------------
+size_t lvae_natgrad_workspace_size(int L, int M) {
+  const size_t mm = align256((size_t)L * M * M * sizeof(double)), v = align256((size_t)L * M * sizeof(double));
+  return 3 * mm + 3 * v + align256((size_t)L * sizeof(double)) + align256((size_t)2 * L * sizeof(int32_t));
+}
+
+int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m, const double* grad_H, double lr,
+                            int32_t* info, void* workspace, void* stream) {
+  if (L < 1) return -1;
+  if (M < 1 || M > 128) return -2;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -9;
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope ps(LVAE_PH_NATGRAD, st);
+  const int64_t MM = (int64_t)M * M;
+  const size_t mmb = align256((size_t)L * MM * sizeof(double)), vb = align256((size_t)L * M * sizeof(double));
+  char* base = (char*)workspace;
+  double* iH = (double*)base;
+  double* iHn = (double*)(base + mmb);
+  double* Hn = (double*)(base + 2 * mmb);
+  double* v = (double*)(base + 3 * mmb);
+  double* gw = (double*)(base + 3 * mmb + vb);
+  double* y = (double*)(base + 3 * mmb + 2 * vb);
+  double* ld = (double*)(base + 3 * mmb + 3 * vb);
+  int32_t* inf = (int32_t*)(base + 3 * mmb + 3 * vb + align256((size_t)L * sizeof(double)));
+  LVAE_TRY(spd_inv_small_f64(M, L, H, MM, iH, MM, ld, inf, st));
+  // iH' = iH + lr (gH + gH^T)
+  axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 1.0, iH, 0.0, iHn, nullptr, nullptr);
+  lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, lr, grad_H, 1.0, iHn, iHn, nullptr, 0, 0);
+  add_transpose_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, grad_H, iHn);
+  LVAE_TRY(spd_inv_small_f64(M, L, iHn, MM, Hn, MM, ld, inf + L, st));
+  // v = iH m ; gw = gH m ; y = v - lr gm + 2 lr gw ; m = Hn y ; H = Hn
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, iH, M, MM, 0, m, 1, M, 0, 0.0, v, 1, M, 0, L, 1, st));
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, grad_H, M, MM, 0, m, 1, M, 0, 0.0, gw, 1, M, 0, L, 1, st));
+  lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 1.0, v, -lr, grad_m, y, nullptr, 0, 0);
+  lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 2.0 * lr, gw, 1.0, y, y, nullptr, 0, 0);
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, Hn, M, MM, 0, y, 1, M, 0, 0.0, m, 1, M, 0, L, 1, st));
+  (void)hipMemcpyAsync(H, Hn, sizeof(double) * L * MM, hipMemcpyDeviceToDevice, st);
+  if (info) (void)hipMemcpyAsync(info, inf, sizeof(int32_t) * L, hipMemcpyDeviceToDevice, st);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

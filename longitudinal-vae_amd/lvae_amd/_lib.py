@@ -40,7 +40,7 @@ class XView(ctypes.Structure):
 class HensmanDims(ctypes.Structure):
     _fields_ = [("L", ctypes.c_int32), ("M", ctypes.c_int32), ("P_b", ctypes.c_int32), ("T", ctypes.c_int32),
                 ("Q", ctypes.c_int32), ("P_tot", ctypes.c_double), ("eps", ctypes.c_double),
-                ("natural_gradient", ctypes.c_int32)]
+                ("natural_gradient", ctypes.c_int32), ("ng_prior_share", ctypes.c_double)]
 
 
 def make_spec(components):
@@ -113,15 +113,13 @@ def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"lvae_amd: HIP library {path} not built (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)
-    missing = []
+    missing = [name for name in SIGNATURES if not hasattr(lib, name)]
+    if missing:
+        raise RuntimeError(f"lvae_amd: {path} lacks declared symbols {missing} (stale build?)")
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name, None)
-        if fn is None:
-            missing.append(name)
-            continue
+        fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    lib.missing = missing
     _lib = lib
     return lib
 

@@ -116,3 +116,103 @@ def KL_closed(covar_module, train_x, likelihoods, data, mu, log_var):
     """Closed-form KL for one latent dim (elbo_functions.py:8-34); ``data`` only gives N."""
     n = data.shape[0]
     return KL_closed_batched(covar_module, train_x[:n], likelihoods, mu.reshape(n, 1), log_var.reshape(n, 1))[0]
+
+
+# ------------------------------------------------------------------------------------------
+# Regime A: Hensman mini-batch KL upper bound (elbo_functions.py:144-216), fp64
+# ------------------------------------------------------------------------------------------
+class _HensmanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, params0, params1, noise, mu, logv, m, H, x, z, spec0, spec1, dims, want_ng):
+        lib = _lib.lib()
+        dev = mu.device
+        f64 = lambda t: t.detach().to(torch.float64).contiguous()
+        p0, p1, nz = f64(params0), f64(params1), f64(noise).reshape(-1)
+        mu64, lv64, m64, H64, x64, z64 = f64(mu), f64(logv), f64(m), f64(H), f64(x), f64(z)
+        L, M = dims.L, dims.M
+        ws = torch.empty(int(lib.lvae_hensman_workspace_size(dims)), dtype=torch.uint8, device=dev)
+        kld = torch.empty((), dtype=torch.float64, device=dev)
+        gm = torch.empty(L, M, 1, dtype=torch.float64, device=dev) if want_ng else None
+        gH = torch.empty(L, M, M, dtype=torch.float64, device=dev) if want_ng else None
+        info = torch.empty(L, dtype=torch.int32, device=dev)
+        rc = lib.lvae_hensman_fwd_f64(spec0, spec1, dims, _lib.ptr(x64), _lib.ptr(z64), _lib.ptr(m64),
+                                      _lib.ptr(H64), _lib.ptr(mu64), _lib.ptr(lv64), _lib.ptr(p0), _lib.ptr(p1),
+                                      _lib.ptr(nz), _lib.ptr(kld), _lib.ptr(gm), _lib.ptr(gH), _lib.ptr(info),
+                                      _lib.ptr(ws), _lib.stream_ptr())
+        _lib.check(rc, "hensman_fwd")
+        _check_info(info, "minibatch_KLD_upper_bound cholesky (10000+col: K0zz, 20000+col: B_st, 30000+col: H)")
+        ctx.save_for_backward(p0, p1, nz, mu64, lv64, m64, H64, x64, z64, ws)
+        ctx.spec0, ctx.spec1, ctx.dims = spec0, spec1, dims
+        ctx.dtypes = (params0.dtype, params1.dtype, noise.dtype, noise.shape, mu.dtype, logv.dtype, m.dtype, H.dtype)
+        if want_ng:
+            ctx.mark_non_differentiable(gm, gH)
+            return kld, gm, gH
+        return kld, None, None
+
+    @staticmethod
+    def backward(ctx, gkld, _gm=None, _gH=None):
+        lib = _lib.lib()
+        p0, p1, nz, mu64, lv64, m64, H64, x64, z64, ws = ctx.saved_tensors
+        d = ctx.dims
+        g = gkld.detach().to(torch.float64).reshape(1).contiguous()
+        dmu, dlv = torch.empty_like(mu64), torch.empty_like(lv64)
+        dp0, dp1 = torch.empty_like(p0), torch.empty_like(p1)
+        dnz = torch.empty_like(nz)
+        adam = not d.natural_gradient
+        dm = torch.empty_like(m64) if adam else None
+        dH = torch.empty_like(H64) if adam else None
+        rc = lib.lvae_hensman_bwd_f64(ctx.spec0, ctx.spec1, d, _lib.ptr(x64), _lib.ptr(z64), _lib.ptr(m64),
+                                      _lib.ptr(H64), _lib.ptr(mu64), _lib.ptr(lv64), _lib.ptr(p0), _lib.ptr(p1),
+                                      _lib.ptr(nz), _lib.ptr(g), _lib.ptr(dmu), _lib.ptr(dlv), _lib.ptr(dp0),
+                                      _lib.ptr(dp1), _lib.ptr(dnz), _lib.ptr(dm), _lib.ptr(dH), _lib.ptr(ws),
+                                      _lib.stream_ptr())
+        _lib.check(rc, "hensman_bwd")
+        t0, t1, tn, nshape, tmu, tlv, tm, tH = ctx.dtypes
+        return (dp0.to(t0), dp1.to(t1), dnz.to(tn).reshape(nshape), dmu.to(tmu), dlv.to(tlv),
+                None if dm is None else dm.to(tm), None if dH is None else dH.to(tH),
+                None, None, None, None, None, None)
+
+
+def minibatch_KLD_upper_bound(covar_module0, covar_module1, likelihood, latent_dim, m, H, train_xt, mu, log_v, z,
+                              P_tot, P_batch, T, natural_gradient, eps, ng_prior_share=1.0):
+    """Unbiased mini-batch estimate of the KL upper bound and (natural_gradient) its natural-gradient
+    directions wrt (m, H) -- same signature and return as elbo_functions.py:144-216.
+
+    ng_prior_share (extension): weight of the data-independent part of grad_m / grad_H; 1/world
+    under data parallelism so that the SUM over ranks equals the union batch's directions."""
+    spec0, params0 = kernel_spec_and_params(covar_module0)
+    spec1, params1 = kernel_spec_and_params(covar_module1)
+    L, M = latent_dim, H.shape[-1]
+    if params0.shape[0] == 1 and L > 1:
+        params0 = params0.expand(L, -1)
+    if params1.shape[0] == 1 and L > 1:
+        params1 = params1.expand(L, -1)
+    noise = likelihood.noise_covar.noise.reshape(-1)
+    if noise.numel() == 1 and L > 1:
+        noise = noise.expand(L)
+    Q = train_xt.shape[-1]
+    if train_xt.shape[0] != P_batch * T:
+        raise ValueError(f"train_xt has {train_xt.shape[0]} rows, expected P_batch*T = {P_batch * T}")
+    zz = z if z.dim() == 3 else z.unsqueeze(0).expand(L, -1, -1)
+    dims = _lib.HensmanDims(L, M, int(P_batch), int(T), int(Q), float(P_tot), float(eps), int(bool(natural_gradient)),
+                            float(ng_prior_share))
+    kld, gm, gH = _HensmanFn.apply(params0, params1, noise, mu, log_v, m, H, train_xt, zz, spec0, spec1, dims,
+                                   bool(natural_gradient))
+    return kld, gm, gH
+
+
+def natural_gradient_update(m, H, grad_m, grad_H, natural_gradient_lr):
+    """training.py:129-135 on the device: returns the updated (m, H) (new tensors, detached)."""
+    lib = _lib.lib()
+    L, M = H.shape[0], H.shape[-1]
+    m2 = m.detach().to(torch.float64).contiguous().clone()
+    H2 = H.detach().to(torch.float64).contiguous().clone()
+    gm = grad_m.detach().to(torch.float64).contiguous()
+    gH = grad_H.detach().to(torch.float64).contiguous()
+    ws = torch.empty(int(lib.lvae_natgrad_workspace_size(L, M)), dtype=torch.uint8, device=H.device)
+    info = torch.empty(L, dtype=torch.int32, device=H.device)
+    rc = lib.lvae_natgrad_update_f64(L, M, _lib.ptr(m2), _lib.ptr(H2), _lib.ptr(gm), _lib.ptr(gH),
+                                     float(natural_gradient_lr), _lib.ptr(info), _lib.ptr(ws), _lib.stream_ptr())
+    _lib.check(rc, "natgrad_update")
+    _check_info(info, "natural-gradient update cholesky")
+    return m2.reshape(m.shape), H2

@@ -72,8 +72,8 @@ class RbfKernel(_Factor):
         super().__init__()
         self.dim = dim
         self.latent_dim = latent_dim
-        self._log_lengthscale = nn.Parameter(torch.full((latent_dim,), _raw_from(lengthscale, MIN_LOG)))
-        self.register_buffer("min_log_lengthscale", torch.full((1,), MIN_LOG))
+        self._log_lengthscale = nn.Parameter(torch.full((latent_dim,), _raw_from(lengthscale, MIN_LOG), dtype=torch.float64))
+        self.register_buffer("min_log_lengthscale", torch.full((1,), MIN_LOG, dtype=torch.float64))
 
     @property
     def lengthscale(self):
@@ -98,9 +98,9 @@ class PeriodicKernel(_Factor):
         super().__init__()
         self.dim = dim
         self.latent_dim = latent_dim
-        self._log_lengthscale = nn.Parameter(torch.full((latent_dim,), _raw_from(lengthscale, MIN_LOG)))
-        self._log_period = nn.Parameter(torch.full((latent_dim,), _raw_from(period, MIN_LOG)))
-        self.register_buffer("min_log_lengthscale", torch.full((1,), MIN_LOG))
+        self._log_lengthscale = nn.Parameter(torch.full((latent_dim,), _raw_from(lengthscale, MIN_LOG), dtype=torch.float64))
+        self._log_period = nn.Parameter(torch.full((latent_dim,), _raw_from(period, MIN_LOG), dtype=torch.float64))
+        self.register_buffer("min_log_lengthscale", torch.full((1,), MIN_LOG, dtype=torch.float64))
 
     @property
     def lengthscale(self):
@@ -145,8 +145,8 @@ class ScaleKernel(nn.Module):
         super().__init__()
         self.latent_dim = latent_dim
         self.kernel = kernel
-        self._log_scale = nn.Parameter(torch.full((latent_dim,), _raw_from(scale, MIN_LOG)))
-        self.register_buffer("min_log_scale", torch.full((1,), MIN_LOG))
+        self._log_scale = nn.Parameter(torch.full((latent_dim,), _raw_from(scale, MIN_LOG), dtype=torch.float64))
+        self.register_buffer("min_log_scale", torch.full((1,), MIN_LOG, dtype=torch.float64))
 
     @property
     def scale(self):

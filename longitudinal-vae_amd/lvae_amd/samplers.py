@@ -1,0 +1,84 @@
+"""Subject-contiguous batching (utils.py:40-113; training.py:70-75), as index arithmetic.
+
+A Hensman batch is P_b whole subjects: a shuffled subject order, each subject's T rows kept
+contiguous, cut into batches of P_b*T rows (BatchSampler(SubjectSampler, P_b*T, drop_last=False)).
+The reference draws the order with an unseeded np.random.shuffle (utils.py:53); here the order is
+an explicit, seedable permutation so runs are reproducible and ranks agree on it.
+"""
+import numpy as np
+import torch
+
+
+class SubjectSampler:
+    """Row indices of the shuffled subject order (utils.py:40-59)."""
+
+    def __init__(self, P, T, seed=None):
+        self.P, self.T = P, T
+        self.rng = np.random.default_rng(seed)
+
+    def permutation(self):
+        r = np.arange(self.P)
+        self.rng.shuffle(r)
+        return r
+
+    def __iter__(self):
+        r = self.permutation()
+        return iter((r[:, None] * self.T + np.arange(self.T)[None, :]).reshape(-1).tolist())
+
+    def __len__(self):
+        return self.P * self.T
+
+
+def subject_rows(subjects, T):
+    """[subjects] -> contiguous row indices (subject-major, time-minor)."""
+    s = torch.as_tensor(subjects, dtype=torch.int64)
+    return (s[:, None] * T + torch.arange(T, dtype=torch.int64, device=s.device)[None, :]).reshape(-1)
+
+
+def hensman_batches(perm, P_b, T, rank=0, world=1):
+    """Batches of one epoch for one rank: the global batch of world*P_b consecutive subjects of the
+    permutation is split into contiguous per-rank slices of P_b subjects (the last global batch may be
+    short, as with drop_last=False; ranks whose slice is empty get no batch in that step)."""
+    perm = np.asarray(perm)
+    G = world * P_b
+    out = []
+    for g0 in range(0, len(perm), G):
+        sl = perm[g0 + rank * P_b: min(g0 + (rank + 1) * P_b, g0 + G, len(perm))]
+        out.append(subject_rows(sl, T) if len(sl) else None)
+    return out
+
+
+class VaryingLengthSubjectSampler:
+    """(row, subject) pairs in shuffled subject order for subjects of varying length (utils.py:61-87);
+    subjects are contiguous runs of the id column."""
+
+    def __init__(self, subject_ids, seed=None):
+        ids = np.asarray(subject_ids)
+        change = np.flatnonzero(np.r_[True, ids[1:] != ids[:-1]])
+        self.start = change
+        self.end = np.r_[change[1:], len(ids)]
+        self.P = len(change)
+        self.rng = np.random.default_rng(seed)
+
+    def __iter__(self):
+        r = np.arange(self.P)
+        self.rng.shuffle(r)
+        for s in r:
+            for i in range(self.start[s], self.end[s]):
+                yield i, s
+
+    def __len__(self):
+        return self.P
+
+
+def varying_length_batches(sampler, subjects_per_batch):
+    """VaryingLengthBatchSampler (utils.py:89-113): batches of `subjects_per_batch` whole subjects."""
+    batch, subj = [], set()
+    for idx, s in sampler:
+        if s not in subj:
+            if len(subj) == subjects_per_batch:
+                yield batch
+                batch, subj = [], set()
+            subj.add(s)
+        batch.append(idx)
+    yield batch

@@ -1,0 +1,239 @@
+"""HIP Hensman SVI path (Regime A, fp64) against the reference's golden vectors and the oracle.
+
+K0zz carries a 1e-6 jitter (cond ~1e8), so fp64 results depend on the op order at the cond*eps
+level.  Tolerances: KL 1e-8 relative; gradients 1e-6 relative to their max-norm, except
+  * gradients flowing through B_p (k1 hyper-parameters, noise): they contain Xq = c (iK H iK - iK),
+    a difference of two O(|iK|) terms; two fp64 evaluations of the reference formula (autograd
+    through elbo_functions.py:144-216 vs the closed-form adjoint, both on the CPU) already differ by
+    1.1e-5 relative here, so the bound is 1e-4;
+  * grad_H = 1/2 (iK Q iK + iK - iH) at the benign init H = K0zz, where iK - iH cancels 5 orders of
+    magnitude: compared at 1e-7 of max|iH| (cond(K0zz) * eps ~ 1e-8).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import lvae_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+           cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                           {'cont_covariate': 0, 'cat_covariate': 3},
+                           {'cont_covariate': 1, 'cat_covariate': 4}],
+           bin_int_kernel=[], covariate_missing_val=[])
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().cpu().double().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().cpu().double().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def set_raw(module, raw_rows):
+    with torch.no_grad():
+        for j, (_, p) in enumerate(module.named_parameters()):
+            p.copy_(torch.as_tensor(raw_rows[:, j], dtype=p.dtype))
+
+
+def build(g):
+    import lvae_amd as la
+    L = int(g["L"])
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    set_raw(k0, g["raw0"].T)
+    set_raw(k1, g["raw1"].T)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    lik.noise = torch.tensor(g["noise"][:, 0], device=DEV)
+    return k0.to(DEV), k1.to(DEV), lik
+
+
+@pytest.mark.parametrize("name", ["hensman_ng.npz", "hensman_ng_benign.npz", "hensman_adam.npz"])
+def test_hensman_golden(hip, name):
+    import lvae_amd as la
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    g = golden(name)
+    k0, k1, lik = build(g)
+    ng = bool(g["natural_gradient"])
+    X = torch.tensor(g["X_all"][g["idx"]], device=DEV)
+    mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+    lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+    m = torch.tensor(g["m"], device=DEV, requires_grad=not ng)
+    H = torch.tensor(g["H"], device=DEV, requires_grad=not ng)
+    kld, gm, gH = minibatch_KLD_upper_bound(k0, k1, lik, int(g["L"]), m, H, X, mu, lv, torch.tensor(g["Z"], device=DEV),
+                                            int(g["P_tot"]), int(g["P_b"]), int(g["T"]), ng, float(g["eps"]))
+    kld.backward()
+    assert rel(kld, g["kld"]) < 1e-8
+    assert rel(mu.grad, g["dmu"]) < 1e-6
+    assert rel(lv.grad, g["dlogv"]) < 1e-6
+    d0 = torch.stack([p.grad for _, p in k0.named_parameters()])
+    d1 = torch.stack([p.grad for _, p in k1.named_parameters()])
+    assert rel(d0, g["draw0"]) < 1e-6
+    assert rel(d1, g["draw1"]) < 1e-4
+    if ng:
+        assert rel(gm, g["grad_m"]) < 1e-6
+        scale = max(np.abs(g["grad_H"]).max(), np.abs(np.linalg.inv(g["H"])).max())
+        assert np.abs(gH.cpu().numpy() - g["grad_H"]).max() < 1e-7 * scale
+    else:
+        assert rel(m.grad, g["dm"]) < 1e-6
+        assert rel(H.grad, g["dH"]) < 1e-6
+
+
+def test_hensman_noise_gradient(hip):
+    """A trainable noise (constrain_scales=False) gets d kld / d noise = sum_p tr(dB_p) (vs oracle)."""
+    import lvae_amd as la
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    g = golden("hensman_adam.npz")
+    k0, k1, lik = build(g)
+    L, M = int(g["L"]), int(g["M"])
+    X = torch.tensor(g["X_all"][g["idx"]])
+    Z = torch.tensor(g["Z"])
+    args = (torch.tensor(g["m"]), torch.tensor(g["H"]))
+    kld, _, _ = minibatch_KLD_upper_bound(k0, k1, lik, L, args[0].to(DEV), args[1].to(DEV), X.to(DEV),
+                                          torch.tensor(g["mu"], device=DEV), torch.tensor(g["logv"], device=DEV),
+                                          Z.to(DEV), int(g["P_tot"]), int(g["P_b"]), int(g["T"]), False, 1e-6)
+    kld.backward()
+    s0, s1 = O.spec_split(**CFG, id_covariate=2)
+    nz = torch.tensor(g["noise"][:, 0], requires_grad=True)
+    ref, _, _ = O.hensman_kld(s0, O.constrain(torch.tensor(g["raw0"].T.copy())), s1,
+                              O.constrain(torch.tensor(g["raw1"].T.copy())), nz, args[0], args[1], X,
+                              torch.tensor(g["mu"]), torch.tensor(g["logv"]), Z, int(g["P_tot"]), int(g["P_b"]),
+                              int(g["T"]), False, 1e-6)
+    ref.backward()
+    # lik noise = exp(m + softplus(raw - m)) -> chain rule factor
+    with torch.no_grad():
+        raw = lik._log_noise.detach().cpu()
+        dnoise_draw = torch.sigmoid(raw + 16.0) * torch.exp(-16.0 + torch.nn.functional.softplus(raw + 16.0))
+    assert rel(lik._log_noise.grad.cpu(), nz.grad * dnoise_draw) < 1e-4
+
+
+def test_natural_gradient_update(hip):
+    from lvae_amd.elbo import natural_gradient_update
+    g = golden("hensman_ng_benign.npz")
+    m, H = torch.tensor(g["m"]), torch.tensor(g["H"])
+    gm, gH = torch.tensor(g["grad_m"]), torch.tensor(g["grad_H"])
+    m_ref, H_ref = O.natural_gradient_update(m, H, gm, gH, 0.01)
+    m2, H2 = natural_gradient_update(m.to(DEV), H.to(DEV), gm.to(DEV), gH.to(DEV), 0.01)
+    assert rel(H2, H_ref) < 1e-7
+    assert rel(m2, m_ref) < 1e-7
+
+
+def test_spd_inv_small_and_gemm(hip):
+    import lvae_amd as la
+    P = la._lib
+    lib = hip
+    gen = torch.Generator().manual_seed(3)
+    for n, b in [(120, 3), (16, 7), (1, 2), (128, 1)]:
+        X = torch.randn(b, n, n, generator=gen, dtype=torch.float64)
+        A = X @ X.transpose(1, 2) + n * torch.eye(n, dtype=torch.float64)
+        Ad = A.to(DEV)
+        Ai = torch.empty_like(Ad)
+        ld = torch.empty(b, dtype=torch.float64, device=DEV)
+        info = torch.empty(b, dtype=torch.int32, device=DEV)
+        P.check(lib.lvae_spd_inv_small_f64(n, b, P.ptr(Ad), n * n, P.ptr(Ai), n * n, P.ptr(ld), P.ptr(info),
+                                           P.stream_ptr()), "spd_inv")
+        assert int(info.abs().sum()) == 0
+        assert rel(Ai, torch.linalg.inv(A)) < 1e-12
+        assert rel(ld, torch.logdet(A)) < 1e-12
+    # gemm: C = 0.5 A^T B + 2 C over a (2, 3) batch with broadcast B
+    m_, n_, k_ = 37, 45, 70
+    A = torch.randn(2, 3, k_, m_, generator=gen, dtype=torch.float64)
+    B = torch.randn(n_, k_, generator=gen, dtype=torch.float64)
+    C = torch.randn(2, 3, m_, n_, generator=gen, dtype=torch.float64)
+    ref = 0.5 * A.transpose(-1, -2) @ B.T + 2 * C
+    Ad, Bd, Cd = A.to(DEV), B.to(DEV), C.to(DEV)
+    P.check(lib.lvae_gemm_small_f64(1, 1, m_, n_, k_, 0.5, P.ptr(Ad), m_, 3 * k_ * m_, k_ * m_, P.ptr(Bd), k_, 0, 0,
+                                    2.0, P.ptr(Cd), n_, 3 * m_ * n_, m_ * n_, 2, 3, P.stream_ptr()), "gemm")
+    assert rel(Cd, ref) < 1e-13
+    # non-PD detection
+    A = -torch.eye(4, dtype=torch.float64).unsqueeze(0).to(DEV)
+    Ai = torch.empty_like(A)
+    ld = torch.empty(1, dtype=torch.float64, device=DEV)
+    info = torch.empty(1, dtype=torch.int32, device=DEV)
+    lib.lvae_spd_inv_small_f64(4, 1, P.ptr(A), 16, P.ptr(Ai), 16, P.ptr(ld), P.ptr(info), P.stream_ptr())
+    assert int(info[0]) == 1
+
+
+def test_dp_contract_simulated_ranks(hip):
+    """Two simulated ranks (sequential, one GPU): the mean of per-rank Adam gradients and the SUM of
+    per-rank natural-gradient directions (ng_prior_share = 1/2) equal the union batch's."""
+    import lvae_amd as la
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    from lvae_amd.data import health_mnist_covariates
+    L, M, T, P_tot = 3, 24, 16, 40
+    X = torch.tensor(health_mnist_covariates(P_tot, T, seed=9), device=DEV)
+    gen = torch.Generator().manual_seed(2)
+    mu = torch.randn(P_tot * T, L, generator=gen, dtype=torch.float64).to(DEV)
+    lv = (0.1 * torch.randn(P_tot * T, L, generator=gen, dtype=torch.float64)).to(DEV)
+    N = P_tot * T
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    k0, k1 = k0.to(DEV), k1.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+    with torch.no_grad():
+        H = k0(z, z).evaluate() + 1e-3 * torch.eye(M, dtype=torch.float64, device=DEV)
+    m = torch.randn(L, M, 1, generator=gen, dtype=torch.float64).to(DEV)
+    subjects = [5, 17, 2, 30, 11, 8]
+    rows = lambda ss: torch.cat([torch.arange(s * T, (s + 1) * T) for s in ss]).to(DEV)
+
+    def run(ss, share):
+        for p in list(k0.parameters()) + list(k1.parameters()):
+            p.grad = None
+        r = rows(ss)
+        kld, gm, gH = minibatch_KLD_upper_bound(k0, k1, lik, L, m, H, X[r], mu[r], lv[r], z, P_tot, len(ss), T,
+                                                True, 1e-6, ng_prior_share=share)
+        kld.backward()
+        return (kld.detach(), gm, gH, [p.grad.clone() for p in list(k0.parameters()) + list(k1.parameters())])
+
+    u = run(subjects, 1.0)
+    a = run(subjects[:3], 0.5)
+    b = run(subjects[3:], 0.5)
+    assert rel((a[0] + b[0]) / 2, u[0]) < 1e-10
+    for ga, gb, gu in zip(a[3], b[3], u[3]):
+        assert rel((ga + gb) / 2, gu) < 1e-8
+    assert rel(a[1] + b[1], u[1]) < 1e-8
+    assert rel(a[2] + b[2], u[2]) < 1e-8
+
+
+def test_hensman_step_vs_oracle(hip):
+    """One full hensman_training batch (ConvVAE fwd/bwd, bound, Adam, natural-gradient update;
+    training.py:91-135) against the oracle step: fp32 conv vs fp64 reference -> 1e-4."""
+    import lvae_amd as la
+    from lvae_amd.steps import HensmanStep
+    from lvae_amd.vae import ConvVAE
+    from lvae_amd.data import health_mnist_batch
+    L, M, T, P_tot, P_b = 4, 40, 16, 32, 5
+    img, mask, X = health_mnist_batch(P_tot, T, seed=4, dtype=torch.float64)
+    N = P_tot * T
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
+    ref_vae = O.ConvVAE(L).double()
+    ref_vae.load_state_dict(O.vae_weights(ref_vae, 11))
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).double()
+    vae.load_state_dict(ref_vae.state_dict())
+    vae = vae.float().to(DEV)
+    s0, s1 = O.spec_split(**CFG, id_covariate=2)
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    raw0 = torch.stack([p.detach().clone() for _, p in k0.named_parameters()], 1).requires_grad_()
+    raw1 = torch.stack([p.detach().clone() for _, p in k1.named_parameters()], 1).requires_grad_()
+    k0, k1 = k0.to(DEV), k1.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+    with torch.no_grad():
+        H = O.gram(s0, O.constrain(raw0), z, z) + 1e-6 * torch.eye(M, dtype=torch.float64)
+    m = torch.zeros(L, M, 1, dtype=torch.float64)
+    rows = torch.cat([torch.arange(s * T, (s + 1) * T) for s in [3, 9, 20, 1, 27]])
+    eps = torch.randn(P_b * T, L, generator=torch.Generator().manual_seed(0), dtype=torch.float64)
+    # oracle step (no optimiser: compare the losses and the natural-gradient update)
+    loss, recon, kld, m_ref, H_ref = O.hensman_step(ref_vae, s0, raw0, s1, raw1, torch.ones(L), m, H, img[rows],
+                                                    mask[rows], X[rows], z, eps, P_tot, T, 0.15, 0.01)
+    opt = torch.optim.SGD(list(vae.parameters()) + list(k0.parameters()) + list(k1.parameters()), lr=0.0)
+    step = HensmanStep(vae, k0, k1, lik, opt, m.to(DEV), H.to(DEV), z.to(DEV), P_tot, T)
+    net, rl, _, kl = step(img[rows].float().to(DEV), mask[rows].float().to(DEV), X[rows].to(DEV),
+                          eps.float().to(DEV))
+    assert rel(net, loss) < 1e-4
+    assert rel(rl, recon) < 1e-4
+    assert rel(kl, kld) < 1e-4
+    assert rel(step.m, m_ref) < 1e-4
+    assert rel(step.H, H_ref) < 1e-4
+    d0 = torch.stack([p.grad for _, p in k0.named_parameters()], 1)
+    assert rel(d0, raw0.grad) < 1e-4
