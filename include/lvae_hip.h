@@ -117,13 +117,15 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
                            const double* gkl, double* dmu, double* dlogv, double* dparams, double* dnoise,
                            void* workspace, void* stream);
 
-/* Cholesky of L padded SPD matrices (in place, lower, fp32 MFMA), writing also the inverse of
- * each 128x128 diagonal block into W's diagonal blocks, log|A_l| into logdet[l] and info[l].
- * A, W: [L, np, np] row-major, np a multiple of 128.  Replaces torch.cholesky (elbo_functions.py:26). */
+/* Blocked factorisation of L padded SPD matrices (in place, fp32 MFMA): right-looking block LDL^T
+ * with 128-wide pivot blocks, K = Lt Dt Lt^T (the Cholesky factor is Lt chol(Dt)).  On return W's
+ * diagonal tiles hold D_k^-1, its strictly-lower tiles Lt; logdet[l] = log|A_l|, info[l] LAPACK-style.
+ * A, W: [L, np, np] row-major, np a multiple of 128; only A's lower triangle is read.
+ * Replaces torch.cholesky + the log-det (elbo_functions.py:26, 29). */
 int lvae_potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, void* stream);
-/* W = L^-1 (lower) from the factor in A and the diagonal-block inverses potrf left in W;
- * then Ainv = L^-T L^-1 (full symmetric).  Replaces cholesky_solve(I, L) (elbo_functions.py:27-28). */
-int lvae_potri_f32(int np_, int L, const float* A, float* W, float* Ainv, void* stream);
+/* Ainv = A^-1 (full symmetric) from lvae_potrf_f32's W; A is used as scratch.
+ * Replaces cholesky_solve(I, L) (elbo_functions.py:27-28). */
+int lvae_potri_f32(int np_, int L, float* A, float* W, float* Ainv, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Regime A: Hensman SVI, fp64 (elbo_functions.py:144-216; training.py:129-135)             */

@@ -2,8 +2,8 @@
 // analytic backward, batched over the L latent dims (replaces the Python loop at training.py:515-522).
 //
 //   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
-//   K_l = L L^T, logdet                           (potrf_f32, MFMA)
-//   W = L^-1, K^-1 = W^T W                        (potri_f32, MFMA)
+//   K_l = Lt Dt Lt^T (block LDL^T), logdet         (potrf_f32, MFMA + MFMA sweep of the pivot blocks)
+//   K^-1 = Lt^-T Dt^-1 Lt^-1                       (potri_f32, MFMA)
 //   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation)
 //   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
 // backward (dL/dkl_l = g_l):
@@ -22,7 +22,7 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
                 const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
                 double* part, double* dparams, double* dnoise, hipStream_t st);
 int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, hipStream_t st);
-int potri_f32(int np_, int L, const float* A, float* W, float* Ainv, hipStream_t st);
+int potri_f32(int np_, int L, float* A, float* W, float* Ainv, hipStream_t st);
 int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st);
 
 struct KLWorkspace {

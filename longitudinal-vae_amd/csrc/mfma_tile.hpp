@@ -82,6 +82,10 @@ struct OpChunk {
       for (int i = 0; i < 4; ++i) v[i] *= s[k0 + (t >> 5) + 8 * i];
     }
   }
+  __device__ inline void negate() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = -v[i];
+  }
   __device__ inline void store(float* __restrict__ lds) const {
     const int t = threadIdx.x;
     if constexpr (KCONT) {
@@ -129,10 +133,10 @@ __device__ inline void mma_chunk(const float* __restrict__ la, const float* __re
   }
 }
 
-// acc += op(A)[128 x K] * op(B)[K x 128] over k in [kbeg, kend) (multiples of BK).
+// acc += op(A)[128 x K] * op(B)[K x 128] over k in [kbeg, kend) (multiples of BK); NEG: acc -= ...
 // A / B point at element (row 0, k 0) of the tile's operand (k offsets are absolute).
 // ascale (nullable): per-k scale applied to op(A) (used for K^-1 V K^-1).
-template <bool AK, bool BKc>
+template <bool AK, bool BKc, bool NEG = false>
 __device__ inline void tile_gemm(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                                  int kbeg, int kend, Frag& f, float* __restrict__ lds,
                                  const float* __restrict__ ascale = nullptr) {
@@ -145,6 +149,7 @@ __device__ inline void tile_gemm(const float* __restrict__ A, int64_t lda, const
   cb.load(B, ldb, kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += kBK) {
     if (ascale) ca.scale_k(ascale, k0);
+    if constexpr (NEG) ca.negate();
     __syncthreads();  // previous chunk fully consumed
     ca.store(la);
     cb.store(lb);
@@ -155,6 +160,22 @@ __device__ inline void tile_gemm(const float* __restrict__ A, int64_t lda, const
     }
     mma_chunk<AK, BKc>(la, lb, f);
   }
+}
+
+// acc = C tile (row-major, ld) -- accumulate-into-C GEMMs start from the old tile.
+__device__ inline void frag_load(Frag& f, const float* __restrict__ C, int64_t ld) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wn + b * 32 + (lane & 31);
+        f.acc[a][b][r] = C[(int64_t)row * ld + col];
+      }
 }
 
 // Visit every accumulator element: fn(row, col, value) with row/col in [0,128).

@@ -1,91 +1,28 @@
 // small.hip -- batched small fp64 linear algebra for the Hensman SVI path (Regime A, fp64 required:
 // K0zz has a 1e-6 jitter and cond ~1e8, fp32 Cholesky fails -- SURVEY.md §0).
 //
-//   spd_inv_small : one workgroup per matrix (n <= 128): Cholesky in LDS, in-place L^-1, then
-//                   A^-1 = L^-T L^-1 straight to global; log|A| and LAPACK-style info.
+//   spd_inv_small : one workgroup per matrix (n <= 128): Cholesky + solves in MFMA f64 accumulators
+//                   (sweep.hpp, chol_inverse) -> A^-1, log|A| (= sum of the block-LDL^T pivots) and LAPACK-style info.
 //                   Replaces torch.cholesky + cholesky_solve(I) at elbo_functions.py:176-186 and
-//                   training.py:130-134 (M = 120 -> 120*121*8 B = 116 KB of LDS).
+//                   training.py:130-134 (M = 120 -> 128: 16 waves x 4 tiles, 32 rank-4 MFMA steps).
 //   gemm_small    : C = alpha op(A) op(B) + beta C over a two-level batch; 32x32 output tile per
 //                   workgroup, K staged through LDS in chunks of 32.
 #include "common.hpp"
+#include "sweep.hpp"
 
 namespace lvae {
 
 constexpr int kSmallMax = 128;
 
-__global__ __launch_bounds__(256) void spd_inv_small_kernel(int n, const double* __restrict__ A, int64_t stride,
-                                                            double* __restrict__ Ainv, int64_t stride_out,
-                                                            double* __restrict__ logdet,
-                                                            int32_t* __restrict__ info) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int ld = n + 1;
-  double* Ls = sm;  // [n][n+1]
-  __shared__ double red[4];
-  __shared__ int fail;
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const double* a = A + (int64_t)b * stride;
-  for (int e = tid; e < n * n; e += 256) {
-    const int i = e / n, j = e - i * n;
-    Ls[i * ld + j] = a[e];
-  }
-  if (tid == 0) fail = 0;
-  __syncthreads();
-  // right-looking Cholesky, one column per step
-  for (int j = 0; j < n; ++j) {
-    const double d = Ls[j * ld + j];
-    if (!(d > 0.0) || !isfinite(d)) {
-      if (tid == 0 && fail == 0) fail = j + 1;
-    }
-    const double piv = sqrt(d);
-    __syncthreads();
-    for (int i = j + 1 + tid; i < n; i += 256) Ls[i * ld + j] /= piv;
-    if (tid == 0) Ls[j * ld + j] = piv;
-    __syncthreads();
-    const int R = n - j - 1;
-    for (int e = tid; e < R * R; e += 256) {
-      const int ii = e / R, jj = e - ii * R;
-      if (jj <= ii) {
-        const int i = j + 1 + ii, c = j + 1 + jj;
-        Ls[i * ld + c] -= Ls[i * ld + j] * Ls[c * ld + j];
-      }
-    }
-    __syncthreads();
-  }
-  // log|A|
-  double ls = 0.0;
-  for (int j = tid; j < n; j += 256) ls += log(Ls[j * ld + j]);
-  ls = block_sum<256>(ls, red);
-  if (tid == 0) {
-    logdet[b] = 2.0 * ls;
-    info[b] = fail;
-  }
-  // in-place inverse of the lower factor (LAPACK trti2 order: last column first)
-  for (int j = n - 1; j >= 0; --j) {
-    __syncthreads();
-    const double wjj = 1.0 / Ls[j * ld + j];
-    // x = L[j+1:, j];  W[j+1:, j] = -wjj * W[j+1:, j+1:] x  (W[j+1:, j+1:] already inverted)
-    double y[1];
-    const int R = n - j - 1;
-    double acc = 0.0;
-    const int i = j + 1 + tid;
-    if (tid < R) {
-      for (int k = j + 1; k <= i; ++k) acc += Ls[i * ld + k] * Ls[k * ld + j];
-    }
-    y[0] = acc;
-    __syncthreads();
-    if (tid < R) Ls[i * ld + j] = -wjj * y[0];
-    if (tid == 0) Ls[j * ld + j] = wjj;
-  }
-  __syncthreads();
-  // A^-1 = W^T W : (i, j) = sum_{k >= max(i,j)} W[k][i] W[k][j]
-  double* o = Ainv + (int64_t)b * stride_out;
-  for (int e = tid; e < n * n; e += 256) {
-    const int i = e / n, j = e - i * n;
-    const int k0 = i > j ? i : j;
-    double acc = 0.0;
-    for (int k = k0; k < n; ++k) acc += Ls[k * ld + i] * Ls[k * ld + j];
-    o[e] = acc;
-  }
+template <int TS, int TPW>
+__global__ __launch_bounds__(64 * TS * TS / TPW) void spd_inv_small_kernel(int n, const double* __restrict__ A,
+                                                                           int64_t stride, double* __restrict__ Ainv,
+                                                                           int64_t stride_out,
+                                                                           double* __restrict__ logdet,
+                                                                           int32_t* __restrict__ info) {
+  const int b = blockIdx.x;
+  chol_inverse<double, TS, TPW>(n, A + (int64_t)b * stride, n, Ainv + (int64_t)b * stride_out, n, logdet + b, 0,
+                                 info + b, 0);
 }
 
 constexpr int kGS = 32;
@@ -146,14 +83,14 @@ int spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double*
   if (n < 1 || n > kSmallMax) return -1;
   if (batch < 0) return -2;
   if (batch == 0) return 0;
-  const size_t lds = (size_t)n * (n + 1) * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)spd_inv_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(kSmallMax * (kSmallMax + 1) * sizeof(double)));
-    attr = true;
-  }
-  spd_inv_small_kernel<<<batch, 256, lds, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+  if (n <= 16)
+    spd_inv_small_kernel<1, 1><<<batch, 64, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+  else if (n <= 32)
+    spd_inv_small_kernel<2, 2><<<batch, 128, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+  else if (n <= 64)
+    spd_inv_small_kernel<4, 4><<<batch, 256, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+  else
+    spd_inv_small_kernel<8, 4><<<batch, 1024, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

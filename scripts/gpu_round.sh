@@ -34,3 +34,12 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
 rc=$?; stage "rocprof rc=$rc"
 find "$OUT/prof" -name "*stats*" | head
 fi
+
+if [ "${PROF_HENSMAN:-0}" = "1" ]; then
+stage rocprof-hensman
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_h" -o run --output-format csv -- \
+  python3 "$ROOT/bench.py" --regime hensman --steps 50 --warmup 5 --no-cpu-baseline --no-phase-timing > "$OUT/prof_h_bench.json" 2> "$OUT/prof_h.err"
+rc=$?; stage "rocprof-hensman rc=$rc"
+cat "$OUT/prof_h_bench.json"
+fi

@@ -101,28 +101,37 @@ def test_kl_closed_vs_oracle(hip, P, L):
 
 
 def test_potrf_potri(hip):
-    """Blocked MFMA Cholesky + inverse on random SPD matrices vs fp64 torch on the host."""
+    """Blocked MFMA block-LDL^T + inverse on random SPD matrices vs fp64 torch on the host:
+    Lt Dt Lt^T reconstructs A, log|A| and A^-1 match (np = 384: three 128-blocks)."""
     import lvae_amd as la
     lib = hip
-    L, n = 2, 384
+    L, n, nb = 2, 384, 128
     gen = torch.Generator().manual_seed(1)
     Xm = torch.randn(L, n, n, generator=gen, dtype=torch.float64) / n ** 0.5
     A = Xm @ Xm.transpose(1, 2) + torch.eye(n, dtype=torch.float64)
-    Ad = A.float().to(DEV).contiguous()
+    Ad = torch.tril(A).float().to(DEV).contiguous()  # only the lower triangle is read
     W = torch.zeros_like(Ad)
     Ai = torch.zeros_like(Ad)
     logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
     info = torch.zeros(L, dtype=torch.int32, device=DEV)
     P = la._lib
     P.check(lib.lvae_potrf_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(logdet), P.ptr(info), P.stream_ptr()), "potrf")
+    torch.cuda.synchronize()
+    Wc = W.cpu().double()
+    Lt = torch.eye(n, dtype=torch.float64).repeat(L, 1, 1)
+    Dt = torch.zeros(L, n, n, dtype=torch.float64)
+    for I in range(n // nb):
+        sl = slice(I * nb, (I + 1) * nb)
+        Dt[:, sl, sl] = torch.linalg.inv(Wc[:, sl, sl])
+        for J in range(I):
+            sj = slice(J * nb, (J + 1) * nb)
+            Lt[:, sl, sj] = Wc[:, sl, sj]
+    assert int(info.abs().sum()) == 0
+    assert rel(Lt @ Dt @ Lt.transpose(1, 2), A) < 1e-5
+    assert rel(logdet.cpu(), torch.logdet(A)) < 1e-5
     P.check(lib.lvae_potri_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(Ai), P.stream_ptr()), "potri")
     torch.cuda.synchronize()
-    Lref = torch.linalg.cholesky(A)
-    assert int(info.abs().sum()) == 0
-    assert rel(torch.tril(Ad.cpu()), Lref) < 1e-5
-    assert rel(torch.tril(W.cpu()), torch.linalg.inv(Lref)) < 1e-4
     assert rel(Ai.cpu(), torch.linalg.inv(A)) < 1e-4
-    assert rel(logdet.cpu(), torch.logdet(A)) < 1e-5
 
 
 def test_not_positive_definite_raises(hip):
