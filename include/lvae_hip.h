@@ -155,6 +155,9 @@ typedef struct lvae_hensman_dims {
 } lvae_hensman_dims;
 
 size_t lvae_hensman_workspace_size(const lvae_hensman_dims* d);
+/* Byte offset inside the Hensman workspace of H^-1 [L, M, M] as left by lvae_hensman_fwd_f64
+ * (valid until the workspace is reused; lets the natural-gradient update skip re-inverting H). */
+size_t lvae_hensman_iH_offset(const lvae_hensman_dims* d);
 
 /* Forward of minibatch_KLD_upper_bound: kld (scalar, sum over L), grad_m [L,M], grad_H [L,M,M]
  * (natural_gradient only; may be NULL otherwise).  x [P_b*T, Q], z [L, M, Q], m [L, M], H [L, M, M],
@@ -177,10 +180,13 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
 
 /* Natural-gradient update of the inducing posterior (training.py:129-135), in place:
  *   iH' = H^-1 + lr (gH + gH^T);  H <- iH'^-1;  m <- H (H^-1 m - lr (gm - 2 gH m)).
+ * iH: H^-1 if the caller already has it (e.g. workspace + lvae_hensman_iH_offset after the
+ * forward on the same H), else NULL (H is inverted here, as training.py:130-131 does).
  * workspace: lvae_natgrad_workspace_size(L, M) bytes.                                        */
 size_t lvae_natgrad_workspace_size(int L, int M);
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m,
-                            const double* grad_H, double lr, int32_t* info, void* workspace, void* stream);
+                            const double* grad_H, double lr, const double* iH, int32_t* info,
+                            void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Phase timing (profiling aid; the only process-wide state of the library).  When enabled, */

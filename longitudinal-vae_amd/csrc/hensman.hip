@@ -28,6 +28,9 @@ int gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int
                  double* ddiag, hipStream_t st);
 int spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double* Ainv, int64_t stride_out,
                       double* logdet, int32_t* info, hipStream_t st);
+int spd_inv_small2_f64(int n, int nb0, const double* A0, int64_t stride0, double* Ainv0, int64_t stride_out0,
+                       double* logdet0, int32_t* info0, int nb1, const double* A1, int64_t stride1, double* Ainv1,
+                       int64_t stride_out1, double* logdet1, int32_t* info1, hipStream_t st);
 int gemm_small_f64(int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda, int64_t sa1,
                    int64_t sa2, const double* B, int ldb, int64_t sb1, int64_t sb2, double beta, double* C, int ldc,
                    int64_t sc1, int64_t sc2, int nb1, int nb2, hipStream_t st);
@@ -284,6 +287,11 @@ extern "C" {
 
 size_t lvae_hensman_workspace_size(const lvae_hensman_dims* d) { return HWs(nullptr, *d).bytes; }
 
+size_t lvae_hensman_iH_offset(const lvae_hensman_dims* d) {
+  char* const base = reinterpret_cast<char*>(uintptr_t(4096));  // any non-null base: offsets only
+  return (size_t)((char*)HWs(base, *d).iH - base);
+}
+
 int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, const lvae_hensman_dims* dp,
                          const double* x, const double* z, const double* m, const double* H, const double* mu,
                          const double* logv, const double* params0, const double* params1, const double* noise,
@@ -304,9 +312,9 @@ int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   LVAE_TRY(lvae_gram_f64(spec0, xs, xs, P_b, L, T, T, params0, nullptr, w.K0st, TT, P_b * TT, T, stream));
   LVAE_TRY(lvae_gram_f64(spec1, xs, xs, P_b, L, T, T, params1, noise, w.Bst, TT, P_b * TT, T, stream));
   // factor + inverse (177-186)
-  LVAE_TRY(spd_inv_small_f64(M, L, w.K0zz, MM, w.iK, MM, w.ldK, w.info, st));
+  LVAE_TRY(spd_inv_small2_f64(M, L, w.K0zz, MM, w.iK, MM, w.ldK, w.info, L, H, MM, w.iH, MM, w.ldH,
+                              w.info + L + L * P_b, st));
   LVAE_TRY(spd_inv_small_f64(T, L * P_b, w.Bst, TT, w.iB, TT, w.ldB, w.info + L, st));
-  LVAE_TRY(spd_inv_small_f64(M, L, H, MM, w.iH, MM, w.ldH, w.info + L + L * P_b, st));
   // t = iK m ; r = K0xz t - mu ; s = iB r ; iBK = iB K0xz ; Q = K0xz^T iBK ; Y = iK H iK
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, m, 1, M, 0, 0.0, w.t, 1, M, 0, L, 1, st));
   LVAE_TRY(gemm_small_f64(0, 0, B, 1, M, 1.0, w.K0xz, M, BM, 0, w.t, 1, M, 0, 0.0, w.y, 1, B, 0, L, 1, st));
@@ -417,7 +425,7 @@ size_t lvae_natgrad_workspace_size(int L, int M) {
 }
 
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m, const double* grad_H, double lr,
-                            int32_t* info, void* workspace, void* stream) {
+                            const double* iH_in, int32_t* info, void* workspace, void* stream) {
   if (L < 1) return -1;
   if (M < 1 || M > 128) return -2;
   if (!workspace || ((uintptr_t)workspace & 255)) return -9;
@@ -427,6 +435,7 @@ int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* gr
   const size_t mmb = align256((size_t)L * MM * sizeof(double)), vb = align256((size_t)L * M * sizeof(double));
   char* base = (char*)workspace;
   double* iH = (double*)base;
+  const double* iHc = iH_in ? iH_in : iH;
   double* iHn = (double*)(base + mmb);
   double* Hn = (double*)(base + 2 * mmb);
   double* v = (double*)(base + 3 * mmb);
@@ -434,14 +443,18 @@ int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* gr
   double* y = (double*)(base + 3 * mmb + 2 * vb);
   double* ld = (double*)(base + 3 * mmb + 3 * vb);
   int32_t* inf = (int32_t*)(base + 3 * mmb + 3 * vb + align256((size_t)L * sizeof(double)));
-  LVAE_TRY(spd_inv_small_f64(M, L, H, MM, iH, MM, ld, inf, st));
+  if (iH_in) {
+    (void)hipMemsetAsync(inf, 0, sizeof(int32_t) * L, st);
+  } else {
+    LVAE_TRY(spd_inv_small_f64(M, L, H, MM, iH, MM, ld, inf, st));
+  }
   // iH' = iH + lr (gH + gH^T)
-  axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 1.0, iH, 0.0, iHn, nullptr, nullptr);
+  axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 1.0, iHc, 0.0, iHn, nullptr, nullptr);
   lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, lr, grad_H, 1.0, iHn, iHn, nullptr, 0, 0);
   add_transpose_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, grad_H, iHn);
   LVAE_TRY(spd_inv_small_f64(M, L, iHn, MM, Hn, MM, ld, inf + L, st));
   // v = iH m ; gw = gH m ; y = v - lr gm + 2 lr gw ; m = Hn y ; H = Hn
-  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, iH, M, MM, 0, m, 1, M, 0, 0.0, v, 1, M, 0, L, 1, st));
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, iHc, M, MM, 0, m, 1, M, 0, 0.0, v, 1, M, 0, L, 1, st));
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, grad_H, M, MM, 0, m, 1, M, 0, 0.0, gw, 1, M, 0, L, 1, st));
   lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 1.0, v, -lr, grad_m, y, nullptr, 0, 0);
   lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 2.0 * lr, gw, 1.0, y, y, nullptr, 0, 0);

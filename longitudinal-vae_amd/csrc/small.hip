@@ -14,15 +14,24 @@ namespace lvae {
 
 constexpr int kSmallMax = 128;
 
+// Two independent batches in one launch (blocks [0, nb0) take set 0, the rest set 1): the
+// Hensman forward inverts K0zz and H together, halving the serial inverse launches per step.
+struct InvSet {
+  const double* A;
+  int64_t stride;
+  double* Ainv;
+  int64_t stride_out;
+  double* logdet;
+  int32_t* info;
+};
+
 template <int TS, int TPW>
-__global__ __launch_bounds__(64 * TS * TS / TPW) void spd_inv_small_kernel(int n, const double* __restrict__ A,
-                                                                           int64_t stride, double* __restrict__ Ainv,
-                                                                           int64_t stride_out,
-                                                                           double* __restrict__ logdet,
-                                                                           int32_t* __restrict__ info) {
-  const int b = blockIdx.x;
-  chol_inverse<double, TS, TPW>(n, A + (int64_t)b * stride, n, Ainv + (int64_t)b * stride_out, n, logdet + b, 0,
-                                 info + b, 0);
+__global__ __launch_bounds__(64 * TS * TS / TPW) void spd_inv_small_kernel(int n, int nb0, InvSet s0, InvSet s1) {
+  const bool first = (int)blockIdx.x < nb0;
+  const InvSet& s = first ? s0 : s1;
+  const int b = first ? blockIdx.x : blockIdx.x - nb0;
+  chol_inverse<double, TS, TPW>(n, s.A + (int64_t)b * s.stride, n, s.Ainv + (int64_t)b * s.stride_out, n,
+                                 s.logdet + b, 0, s.info + b, 0);
 }
 
 constexpr int kGS = 32;
@@ -78,21 +87,31 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(int ta, int tb, int m, 
   }
 }
 
-int spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double* Ainv, int64_t stride_out,
-                      double* logdet, int32_t* info, hipStream_t st) {
+int spd_inv_small2_f64(int n, int nb0, const double* A0, int64_t stride0, double* Ainv0, int64_t stride_out0,
+                       double* logdet0, int32_t* info0, int nb1, const double* A1, int64_t stride1, double* Ainv1,
+                       int64_t stride_out1, double* logdet1, int32_t* info1, hipStream_t st) {
   if (n < 1 || n > kSmallMax) return -1;
-  if (batch < 0) return -2;
+  if (nb0 < 0 || nb1 < 0) return -2;
+  const int batch = nb0 + nb1;
   if (batch == 0) return 0;
+  const InvSet s0{A0, stride0, Ainv0, stride_out0, logdet0, info0};
+  const InvSet s1{A1, stride1, Ainv1, stride_out1, logdet1, info1};
   if (n <= 16)
-    spd_inv_small_kernel<1, 1><<<batch, 64, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+    spd_inv_small_kernel<1, 1><<<batch, 64, 0, st>>>(n, nb0, s0, s1);
   else if (n <= 32)
-    spd_inv_small_kernel<2, 2><<<batch, 128, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+    spd_inv_small_kernel<2, 2><<<batch, 128, 0, st>>>(n, nb0, s0, s1);
   else if (n <= 64)
-    spd_inv_small_kernel<4, 4><<<batch, 256, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+    spd_inv_small_kernel<4, 4><<<batch, 256, 0, st>>>(n, nb0, s0, s1);
   else
-    spd_inv_small_kernel<8, 4><<<batch, 1024, 0, st>>>(n, A, stride, Ainv, stride_out, logdet, info);
+    spd_inv_small_kernel<8, 4><<<batch, 1024, 0, st>>>(n, nb0, s0, s1);
   LVAE_CHECK_LAUNCH();
   return 0;
+}
+
+int spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double* Ainv, int64_t stride_out,
+                      double* logdet, int32_t* info, hipStream_t st) {
+  return spd_inv_small2_f64(n, batch, A, stride, Ainv, stride_out, logdet, info, 0, A, stride, Ainv, stride_out,
+                            logdet, info, st);
 }
 
 int gemm_small_f64(int ta, int tb, int m, int n, int k, double alpha, const double* A, int lda, int64_t sa1,

@@ -96,7 +96,8 @@ SIGNATURES = {
     "lvae_hensman_bwd_f64": (_I32, [_SPEC, _SPEC, _DIMS, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                     _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_natgrad_workspace_size": (_SZ, [_I32, _I32]),
-    "lvae_natgrad_update_f64": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _D, _VP, _VP, _VP]),
+    "lvae_natgrad_update_f64": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _D, _VP, _VP, _VP, _VP]),
+    "lvae_hensman_iH_offset": (_SZ, [_DIMS]),
     "lvae_prof_enable": (_I32, [_I32]),
     "lvae_prof_collect": (_I32, [_VP, _VP, _I32]),
     "lvae_version": (ctypes.c_char_p, []),

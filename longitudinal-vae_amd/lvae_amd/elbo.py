@@ -145,6 +145,9 @@ class _HensmanFn(torch.autograd.Function):
         ctx.spec0, ctx.spec1, ctx.dims = spec0, spec1, dims
         ctx.dtypes = (params0.dtype, params1.dtype, noise.dtype, noise.shape, mu.dtype, logv.dtype, m.dtype, H.dtype)
         if want_ng:
+            # H^-1 stays in the workspace: the natural-gradient update reuses it while H is unchanged
+            off = int(lib.lvae_hensman_iH_offset(dims))
+            gH._lvae_iH = (ws[off:off + L * M * M * 8].view(torch.float64).view(L, M, M), H, H._version)
             ctx.mark_non_differentiable(gm, gH)
             return kld, gm, gH
         return kld, None, None
@@ -211,8 +214,14 @@ def natural_gradient_update(m, H, grad_m, grad_H, natural_gradient_lr):
     gH = grad_H.detach().to(torch.float64).contiguous()
     ws = torch.empty(int(lib.lvae_natgrad_workspace_size(L, M)), dtype=torch.uint8, device=H.device)
     info = torch.empty(L, dtype=torch.int32, device=H.device)
+    # H^-1 from the forward that produced grad_H, if H is still the very tensor (same version) it saw
+    iH = None
+    cached = getattr(grad_H, "_lvae_iH", None)
+    if cached is not None and cached[1] is H and cached[1]._version == cached[2]:
+        iH = cached[0]
     rc = lib.lvae_natgrad_update_f64(L, M, _lib.ptr(m2), _lib.ptr(H2), _lib.ptr(gm), _lib.ptr(gH),
-                                     float(natural_gradient_lr), _lib.ptr(info), _lib.ptr(ws), _lib.stream_ptr())
+                                     float(natural_gradient_lr), _lib.ptr(iH), _lib.ptr(info), _lib.ptr(ws),
+                                     _lib.stream_ptr())
     _lib.check(rc, "natgrad_update")
     _check_info(info, "natural-gradient update cholesky")
     return m2.reshape(m.shape), H2

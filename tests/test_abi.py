@@ -45,7 +45,9 @@ def test_host_queries_need_no_gpu():
     assert lib.lvae_kl_closed_padded_n(200) == 256
     assert lib.lvae_kl_closed_workspace_size(4096, 16) > 3 * 16 * 4096 * 4096 * 4
     d = _lib.HensmanDims(16, 120, 5, 16, 6, 256.0, 1e-6, 1, 1.0)
-    assert lib.lvae_hensman_workspace_size(ctypes.byref(d)) > 0
+    ws = lib.lvae_hensman_workspace_size(ctypes.byref(d))
+    off = lib.lvae_hensman_iH_offset(ctypes.byref(d))
+    assert ws > 0 and off % 256 == 0 and off + 16 * 120 * 120 * 8 <= ws
 
 
 def test_compute_without_gpu_fails_loudly():

@@ -119,6 +119,30 @@ def test_natural_gradient_update(hip):
     assert rel(m2, m_ref) < 1e-7
 
 
+def test_natural_gradient_update_reuses_forward_inverse(hip):
+    """After the forward on H, the update reuses the workspace's H^-1 (no second inversion); the
+    result equals the fresh-inversion path and the oracle.  A changed H disables the reuse."""
+    from lvae_amd.elbo import minibatch_KLD_upper_bound, natural_gradient_update
+    g = golden("hensman_ng.npz")
+    k0, k1, lik = build(g)
+    X = torch.tensor(g["X_all"][g["idx"]], device=DEV)
+    m = torch.tensor(g["m"], device=DEV)
+    H = torch.tensor(g["H"], device=DEV)
+    with torch.no_grad():
+        _, gm, gH = minibatch_KLD_upper_bound(k0, k1, lik, int(g["L"]), m, H, X, torch.tensor(g["mu"], device=DEV),
+                                              torch.tensor(g["logv"], device=DEV), torch.tensor(g["Z"], device=DEV),
+                                              int(g["P_tot"]), int(g["P_b"]), int(g["T"]), True, float(g["eps"]))
+    assert getattr(gH, "_lvae_iH", None) is not None
+    m_a, H_a = natural_gradient_update(m, H, gm, gH, 0.01)          # reuse path
+    m_b, H_b = natural_gradient_update(m, H, gm, gH.clone(), 0.01)  # fresh inversion
+    m_ref, H_ref = O.natural_gradient_update(m.cpu(), H.cpu(), gm.cpu(), gH.cpu(), 0.01)
+    assert rel(H_a, H_b) < 1e-9 and rel(m_a, m_b) < 1e-7
+    assert rel(H_a, H_ref) < 1e-7 and rel(m_a, m_ref) < 1e-6
+    H.mul_(1.0)  # bumps H's version: the cached inverse must not be used any more
+    m_c, H_c = natural_gradient_update(m, H, gm, gH, 0.01)
+    assert rel(H_c, H_b) < 1e-12
+
+
 def test_spd_inv_small_and_gemm(hip):
     import lvae_amd as la
     P = la._lib
