@@ -4,7 +4,7 @@
 // Right-looking block LDL^T with 128-wide pivot blocks (K = Lt Dt Lt^T, Lt unit block-lower,
 // Dt = diag(D_k) the Schur-complement pivot blocks; the Cholesky factor is Lt chol(Dt)):
 //   per pivot block k:
-//     diag   : D_k^-1 and log|D_k| by the in-accumulator MFMA Cholesky inverse (sweep.hpp), one workgroup per matrix
+//     diag   : D_k^-1 and log|D_k| by the in-accumulator 16-block MFMA Cholesky inverse (blkinv.hpp), one WG per matrix
 //     panel  : Lt_ik = A_ik D_k^-1                      (the trsm, as an MFMA GEMM)
 //     update : A_ij -= Lt_ik A_jk^T, k < j <= i          (MFMA, lower tiles only)
 //   log|K| = sum_k log|D_k|
@@ -15,7 +15,7 @@
 // Buffers [L][np][np] row-major, np % 128 == 0: A (covariance, later Z), W (D_k^-1 on the diagonal
 // tiles, Lt -> Y below), Ainv.  Grids are (tiles, L): all latent dims share every launch.
 #include "mfma_tile.hpp"
-#include "sweep.hpp"
+#include "blkinv.hpp"
 
 namespace lvae {
 
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(1024) void ldl_diag_kernel(const float* __restrict_
                                                         int32_t* __restrict__ info) {
   const int l = blockIdx.x;
   const int64_t off = (int64_t)l * np_ * np_ + (int64_t)kb * kNB * np_ + kb * kNB;
-  chol_inverse<float, 8, 4>(kNB, Aall + off, np_, Wall + off, np_, logdet + l, 1, info + l, kb * kNB);
+  blk_inverse<float, 8, 4>(kNB, Aall + off, np_, Wall + off, np_, logdet + l, 1, info + l, kb * kNB);
 }
 
 // panel: W_ik = A_ik D_k^-1 for tile rows i > kb

@@ -1,14 +1,14 @@
 // small.hip -- batched small fp64 linear algebra for the Hensman SVI path (Regime A, fp64 required:
 // K0zz has a 1e-6 jitter and cond ~1e8, fp32 Cholesky fails -- SURVEY.md §0).
 //
-//   spd_inv_small : one workgroup per matrix (n <= 128): Cholesky + solves in MFMA f64 accumulators
-//                   (sweep.hpp, chol_inverse) -> A^-1, log|A| (= sum of the block-LDL^T pivots) and LAPACK-style info.
+//   spd_inv_small : one workgroup per matrix (n <= 128): 16-block Cholesky + block triangular solves in
+//                   MFMA f64 accumulators (blkinv.hpp) -> A^-1, log|A| and LAPACK-style info.
 //                   Replaces torch.cholesky + cholesky_solve(I) at elbo_functions.py:176-186 and
-//                   training.py:130-134 (M = 120 -> 128: 16 waves x 4 tiles, 32 rank-4 MFMA steps).
+//                   training.py:130-134 (M = 120 -> 128: 8 waves x 8 tiles, 8 + 8 + 8 block steps).
 //   gemm_small    : C = alpha op(A) op(B) + beta C over a two-level batch; 32x32 output tile per
 //                   workgroup, K staged through LDS in chunks of 32.
 #include "common.hpp"
-#include "sweep.hpp"
+#include "blkinv.hpp"
 
 namespace lvae {
 
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(64 * TS * TS / TPW) void spd_inv_small_kernel(int n
   const bool first = (int)blockIdx.x < nb0;
   const InvSet& s = first ? s0 : s1;
   const int b = first ? blockIdx.x : blockIdx.x - nb0;
-  chol_inverse<double, TS, TPW>(n, s.A + (int64_t)b * s.stride, n, s.Ainv + (int64_t)b * s.stride_out, n,
+  blk_inverse<double, TS, TPW>(n, s.A + (int64_t)b * s.stride, n, s.Ainv + (int64_t)b * s.stride_out, n,
                                  s.logdet + b, 0, s.info + b, 0);
 }
 
@@ -101,9 +101,9 @@ int spd_inv_small2_f64(int n, int nb0, const double* A0, int64_t stride0, double
   else if (n <= 32)
     spd_inv_small_kernel<2, 2><<<batch, 128, 0, st>>>(n, nb0, s0, s1);
   else if (n <= 64)
-    spd_inv_small_kernel<4, 4><<<batch, 256, 0, st>>>(n, nb0, s0, s1);
+    spd_inv_small_kernel<4, 2><<<batch, 512, 0, st>>>(n, nb0, s0, s1);
   else
-    spd_inv_small_kernel<8, 4><<<batch, 1024, 0, st>>>(n, nb0, s0, s1);
+    spd_inv_small_kernel<8, 8><<<batch, 512, 0, st>>>(n, nb0, s0, s1);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

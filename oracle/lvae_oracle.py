@@ -200,6 +200,97 @@ def hensman_kld(spec0, params0, spec1, params1, noise, m, H, x, mu, logv, z, P_t
     return kld, gm, gH
 
 
+def hensman_kld_iter(spec0, params0, spec1, params1, noise, m, H, x, mu, logv, z, P, P_in_batch, N,
+                     natural_gradient, id_col, eps):
+    """minibatch_KLD_upper_bound_iter (elbo_functions.py:219-307): the same bound for subjects of
+    varying length, a loop over the batch's subjects (torch.unique order, elbo_functions.py:249)."""
+    Lh, M = H.shape[0], H.shape[-1]
+    dt = x.dtype
+    K0xz = gram(spec0, params0, x, z)
+    K0zz = gram(spec0, params0, z, z) + eps * torch.eye(M, dtype=dt)
+    LK = torch.linalg.cholesky(K0zz)
+    iK = torch.cholesky_solve(torch.eye(M, dtype=dt), LK)
+    LH = torch.linalg.cholesky(H)
+    iH = torch.cholesky_solve(torch.eye(M, dtype=dt), LH)
+    Apart = ((K0xz @ (iK @ m)).squeeze(-1) - mu.T).unsqueeze(2)          # [L, B, 1]
+    Epart = iK @ H @ iK
+    A = Bt = C = D = E = torch.zeros((), dtype=dt)
+    P1 = torch.zeros(Lh, M, 1, dtype=dt)
+    P2 = torch.zeros(Lh, M, M, dtype=dt)
+    for s in torch.unique(x[:, id_col]).tolist():
+        sel = x[:, id_col] == s
+        tx = x[sel]
+        T = tx.shape[0]
+        st = tx.unsqueeze(0).expand(Lh, T, tx.shape[-1])
+        K0 = gram(spec0, params0, st, st)
+        Bm = gram(spec1, params1, st, st) + torch.eye(T, dtype=dt) * noise.reshape(Lh, 1, 1)
+        LB = torch.linalg.cholesky(Bm)
+        iB = torch.cholesky_solve(torch.eye(T, dtype=dt), LB)
+        Ks = K0xz[:, sel]
+        Qs = Ks.transpose(1, 2) @ iB @ Ks
+        ap = Apart[:, sel]
+        A = A + (ap.transpose(1, 2) @ iB @ ap).sum()
+        Bt = Bt + (torch.diagonal(iB, dim1=-1, dim2=-2) * torch.exp(logv[sel].T)).sum()
+        C = C + 2 * torch.log(torch.diagonal(LB, dim1=-2, dim2=-1)).sum()
+        D = D + (iB * K0).sum() - (Qs * iK).sum()
+        E = E + (Epart * Qs).sum()
+        if natural_gradient:
+            P1 = P1 + Ks.transpose(1, 2) @ (iB @ mu[sel].T.unsqueeze(2))
+            P2 = P2 + Qs
+    Fs = logv.sum()
+    kl_u = 0.5 * ((iK * H.transpose(-1, -2)).sum() + (m * (iK @ m)).sum() - Lh * M
+                  + 2 * torch.log(torch.diagonal(LK, dim1=-2, dim2=-1)).sum()
+                  - 2 * torch.log(torch.diagonal(LH, dim1=-2, dim2=-1)).sum())
+    kld = P / P_in_batch * 0.5 * (A + Bt + C + D + E - Fs) + kl_u - Lh * N / 2
+    gm = gH = None
+    if natural_gradient:
+        Bn = iK @ P2 @ iK + iK
+        gm = -(iK @ P1) + Bn @ m
+        gH = 0.5 * (-iH + Bn)
+    return kld, gm, gH
+
+
+def batch_predict_varying_T(spec0, params0, spec1, params1, noise, pred_x, test_x, mu, z, id_col, eps):
+    """GP posterior mean of the latents at test_x (utils.py:115-211): Z_pred [N_test, L]."""
+    Lh, M = z.shape[0], z.shape[1]
+    dt = pred_x.dtype
+    K0xz = gram(spec0, params0, pred_x, z)
+    K0zz = gram(spec0, params0, z, z) + eps * torch.eye(M, dtype=dt)
+    K0Xz = gram(spec0, params0, test_x, z)
+    K0zx = K0xz.transpose(-1, -2)
+    H = K0zz
+    iB_mu = torch.zeros(Lh, pred_x.shape[0], 1, dtype=dt)
+    iBs = []
+    subjects = torch.unique(pred_x[:, id_col]).tolist()
+    for s in subjects:
+        sel = pred_x[:, id_col] == s
+        xs = pred_x[sel]
+        T = xs.shape[0]
+        st = xs.unsqueeze(0).expand(Lh, T, xs.shape[-1])
+        Bm = gram(spec1, params1, st, st) + torch.eye(T, dtype=dt) * noise.reshape(Lh, 1, 1)
+        iB = torch.cholesky_solve(torch.eye(T, dtype=dt), torch.linalg.cholesky(Bm))
+        Ks = K0xz[:, sel]
+        H = H + Ks.transpose(-1, -2) @ iB @ Ks
+        iB_mu[:, sel] = iB @ mu[sel].T.unsqueeze(2)
+        iBs.append(iB)
+    t = K0xz @ torch.linalg.solve(H, K0zx @ iB_mu)
+    corr = torch.zeros_like(iB_mu)
+    for i, s in enumerate(subjects):
+        sel = pred_x[:, id_col] == s
+        corr[:, sel] = iBs[i] @ t[:, sel]
+    mu_tilde = iB_mu - corr
+    out = K0Xz @ torch.linalg.solve(K0zz, K0zx @ mu_tilde)
+    test_subjects = torch.unique(test_x[:, id_col]).tolist()
+    mask = torch.isin(pred_x[:, id_col], torch.tensor(test_subjects, dtype=dt))
+    pm = pred_x[mask]
+    for s in test_subjects:
+        sel = test_x[:, id_col] == s
+        a = test_x[sel].unsqueeze(0).expand(Lh, int(sel.sum()), test_x.shape[-1])
+        b = pm.unsqueeze(0).expand(Lh, pm.shape[0], pm.shape[-1])
+        out[:, sel] = out[:, sel] + gram(spec1, params1, a, b) @ mu_tilde[:, mask]
+    return out.squeeze(2).T
+
+
 def natural_gradient_update(m, H, grad_m, grad_H, lr):
     """training.py:129-135."""
     M = H.shape[-1]

@@ -82,6 +82,12 @@ class LikStub:
         self.noise = noise
         self.noise_covar = types.SimpleNamespace(noise=noise)
 
+    def eval(self):
+        return self
+
+    def train(self, mode=True):
+        return self
+
 
 # ----------------------------------------------------------------------------------------------
 # synthetic Health-MNIST covariates (Health_MNIST_generate.py:89-154)
@@ -272,6 +278,86 @@ def gen_hensman(P_tot, T, L, M, P_b, seed, natural_gradient, benign=False, noise
     return out
 
 
+def varying_batch(X, T, subjects, lengths, rng):
+    """Rows of the given subjects, each keeping a sorted random subset of its T time points;
+    subjects appear in the given (unsorted) order, rows subject-contiguous."""
+    rows = []
+    for s, n in zip(subjects, lengths):
+        keep = np.sort(rng.choice(T, size=n, replace=False))
+        rows.append(T * s + keep)
+    return np.concatenate(rows)
+
+
+def gen_hensman_iter(P_tot, T, L, M, seed, lengths, natural_gradient):
+    """minibatch_KLD_upper_bound_iter (elbo_functions.py:219-307) on subjects of varying length."""
+    rng = np.random.default_rng(seed)
+    X = covariates(P_tot, T, seed)
+    k0, k1 = batched_kernels(L)
+    randomise(k0, rng)
+    randomise(k1, rng)
+    subjects = rng.permutation(P_tot)[:len(lengths)]
+    idx = varying_batch(X, T, subjects, lengths, rng)
+    xb = X[idx]
+    N_tot = int(sum(lengths)) * P_tot // len(lengths) + 3  # any N: enters as -L N / 2
+    half = M // 2
+    zrows = np.concatenate([np.arange(0, half), np.arange(P_tot * T // 2, P_tot * T // 2 + half)])
+    Z = np.stack([X[zrows]] * L)
+    B = len(idx)
+    mu = rng.standard_normal((B, L))
+    logv = 0.1 * rng.standard_normal((B, L))
+    m = rng.standard_normal((L, M, 1))
+    Hr = rng.standard_normal((L, M, M)) / 10
+    H = Hr @ np.transpose(Hr, (0, 2, 1)) + 0.05 * np.eye(M)
+    noise_v = np.full((L, 1), 0.9)
+    out = dict(X_all=X, idx=idx, Z=Z, mu=mu, logv=logv, m=m, H=H, noise=noise_v, P_tot=P_tot,
+               P_in_batch=len(lengths), N=N_tot, T=T, L=L, M=M, natural_gradient=int(natural_gradient),
+               eps=1e-6, id_covariate=2, lengths=np.array(lengths))
+    n0, v0 = raw_params(k0)
+    n1, v1 = raw_params(k1)
+    out.update(raw0=np.stack(v0, 0), raw1=np.stack(v1, 0))
+    mu_t = torch.tensor(mu, requires_grad=True)
+    lv_t = torch.tensor(logv, requires_grad=True)
+    m_t = torch.tensor(m, requires_grad=not natural_gradient)
+    H_t = torch.tensor(H, requires_grad=not natural_gradient)
+    kld, gm, gH = EF.minibatch_KLD_upper_bound_iter(
+        KernelAdapter(k0), KernelAdapter(k1), LikStub(torch.tensor(noise_v)), L, m_t, H_t, torch.tensor(xb),
+        mu_t, lv_t, torch.tensor(Z), P_tot, len(lengths), N_tot, natural_gradient, 2, 1e-6)
+    kld.sum().backward()
+    out.update(kld=kld.detach().numpy().reshape(-1)[0], dmu=mu_t.grad.numpy().copy(),
+               dlogv=lv_t.grad.numpy().copy(), draw0=np.stack(raw_grads(k0)), draw1=np.stack(raw_grads(k1)))
+    if natural_gradient:
+        out.update(grad_m=gm.detach().numpy().copy(), grad_H=gH.detach().numpy().copy())
+    else:
+        out.update(dm=m_t.grad.numpy().copy(), dH=H_t.grad.numpy().copy())
+    return out
+
+
+def gen_predict(P, T, L, M, seed, pred_lengths, test_subjects, test_lengths):
+    """utils.batch_predict_varying_T (utils.py:115-211): GP posterior mean of the latents at the
+    test covariates given the (varying-length) prediction set and its encoder means."""
+    import utils as RU  # noqa: E402  (reference)
+    rng = np.random.default_rng(seed)
+    X = covariates(P, T, seed)
+    k0, k1 = batched_kernels(L)
+    randomise(k0, rng)
+    randomise(k1, rng)
+    pidx = varying_batch(X, T, np.arange(P), pred_lengths, rng)
+    tidx = varying_batch(X, T, np.asarray(test_subjects), test_lengths, rng)
+    half = M // 2
+    zrows = np.concatenate([np.arange(0, half), np.arange(P * T // 2, P * T // 2 + half)])
+    Z = np.stack([X[zrows]] * L)
+    mu = rng.standard_normal((len(pidx), L))
+    noise_v = np.full((L, 1), 1.1)
+    with torch.no_grad():
+        zp = RU.batch_predict_varying_T(L, KernelAdapter(k0), KernelAdapter(k1), LikStub(torch.tensor(noise_v)),
+                                        torch.tensor(X[pidx]), torch.tensor(X[tidx]), torch.tensor(mu),
+                                        torch.tensor(Z), 2, 1e-6)
+    n0, v0 = raw_params(k0)
+    n1, v1 = raw_params(k1)
+    return dict(X_all=X, pidx=pidx, tidx=tidx, Z=Z, mu=mu, noise=noise_v, L=L, M=M, eps=1e-6, id_covariate=2,
+                raw0=np.stack(v0, 0), raw1=np.stack(v1, 0), Z_pred=zp.numpy().copy())
+
+
 # ----------------------------------------------------------------------------------------------
 # 3. per-dim GPapprox: elbo (36-84) and deviance_upper_bound (86-142)
 # ----------------------------------------------------------------------------------------------
@@ -369,6 +455,13 @@ def main():
                                            natural_gradient=False, noise=0.8))
     save("gpapprox.npz", **gen_gpapprox(P=16, T=16, M=40, seed=6))
     save("convvae.npz", **gen_vae(L=4, B=6, seed=7))
+    save("hensman_iter_ng.npz", **gen_hensman_iter(P_tot=24, T=16, L=3, M=40, seed=8,
+                                                   lengths=[16, 11, 7, 14, 9], natural_gradient=True))
+    save("hensman_iter_adam.npz", **gen_hensman_iter(P_tot=24, T=16, L=2, M=40, seed=9,
+                                                     lengths=[5, 16, 12], natural_gradient=False))
+    save("predict_varying.npz", **gen_predict(P=12, T=16, L=3, M=40, seed=10,
+                                              pred_lengths=[16, 9, 12, 16, 5, 14, 16, 8, 11, 16, 13, 7],
+                                              test_subjects=[3, 0, 7, 10], test_lengths=[6, 4, 10, 3]))
 
 
 if __name__ == "__main__":

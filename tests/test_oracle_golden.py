@@ -128,3 +128,46 @@ def test_convvae():
     for k in g.files:
         if k.startswith("g_"):
             assert rel(named[k[2:]].grad, g[k]) < 1e-10, k
+
+
+@pytest.mark.parametrize("name", ["hensman_iter_ng.npz", "hensman_iter_adam.npz"])
+def test_hensman_iter_varying_T(name):
+    """minibatch_KLD_upper_bound_iter (elbo_functions.py:219-307) on subjects of varying length."""
+    g = golden(name)
+    s0, s1 = spec_split()
+    ng = bool(g["natural_gradient"])
+    raw0 = torch.tensor(g["raw0"].T.copy(), requires_grad=True)
+    raw1 = torch.tensor(g["raw1"].T.copy(), requires_grad=True)
+    X = torch.tensor(g["X_all"][g["idx"]])
+    mu = torch.tensor(g["mu"], requires_grad=True)
+    lv = torch.tensor(g["logv"], requires_grad=True)
+    m = torch.tensor(g["m"], requires_grad=not ng)
+    H = torch.tensor(g["H"], requires_grad=not ng)
+    kld, gm, gH = O.hensman_kld_iter(s0, O.constrain(raw0), s1, O.constrain(raw1), torch.tensor(g["noise"]), m, H,
+                                     X, mu, lv, torch.tensor(g["Z"]), int(g["P_tot"]), int(g["P_in_batch"]),
+                                     int(g["N"]), ng, int(g["id_covariate"]), float(g["eps"]))
+    kld.backward()
+    assert rel(kld.item(), g["kld"]) < 1e-10
+    assert rel(mu.grad, g["dmu"]) < 1e-8
+    assert rel(lv.grad, g["dlogv"]) < 1e-8
+    assert rel(raw0.grad.T, g["draw0"]) < 1e-6
+    assert rel(raw1.grad.T, g["draw1"]) < 1e-6
+    if ng:
+        assert rel(gm, g["grad_m"]) < 1e-6
+        assert rel(gH, g["grad_H"]) < 1e-6
+    else:
+        assert rel(m.grad, g["dm"]) < 1e-8
+        assert rel(H.grad, g["dH"]) < 1e-8
+
+
+def test_batch_predict_varying_T():
+    """utils.batch_predict_varying_T (utils.py:115-211)."""
+    g = golden("predict_varying.npz")
+    s0, s1 = spec_split()
+    X = g["X_all"]
+    zp = O.batch_predict_varying_T(s0, O.constrain(torch.tensor(g["raw0"].T.copy())), s1,
+                                   O.constrain(torch.tensor(g["raw1"].T.copy())), torch.tensor(g["noise"]),
+                                   torch.tensor(X[g["pidx"]]), torch.tensor(X[g["tidx"]]), torch.tensor(g["mu"]),
+                                   torch.tensor(g["Z"]), int(g["id_covariate"]), float(g["eps"]))
+    assert zp.shape == g["Z_pred"].shape
+    assert rel(zp, g["Z_pred"]) < 1e-9
