@@ -152,6 +152,10 @@ typedef struct lvae_hensman_dims {
   double ng_prior_share;   /* weight of the data-independent part (iK m, iK, iH) in grad_m /   */
                            /* grad_H: 1 for one process; 1/world under data parallelism, so a  */
                            /* SUM all-reduce of the per-rank directions equals the union batch */
+  const int32_t* seg_len;  /* varying T (minibatch_KLD_upper_bound_iter, elbo_functions.py:219-307): */
+                           /* device [P_b] valid rows per subject, rows T_p..T-1 of subject p are  */
+                           /* padding (masked out of every term); NULL = all T rows valid          */
+  double n_total;          /* N of the constant -L N / 2; 0 -> P_tot * T                          */
 } lvae_hensman_dims;
 
 size_t lvae_hensman_workspace_size(const lvae_hensman_dims* d);
@@ -187,6 +191,19 @@ size_t lvae_natgrad_workspace_size(int L, int M);
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m,
                             const double* grad_H, double lr, const double* iH, int32_t* info,
                             void* workspace, void* stream);
+
+/* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
+ * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject
+ * (seg_len [P] valid rows each; padding rows of x are any finite covariates, of mu must be 0),
+ * x [P*T, Q], mu [P*T, L]; include [P] = 1 for subjects that also appear in test_x (the k1 term);
+ * z [L, M, Q]; test_x [Nt, Q]; out [Nt, L].  info[l]: 10000/20000/30000 + col for a failed
+ * K0zz / B_p / H factorisation.  workspace: lvae_predict_workspace_size(L, M, P, T, Nt) bytes. */
+size_t lvae_predict_workspace_size(int L, int M, int P, int T, int Nt);
+int lvae_predict_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, int L, int M, int Q, int P,
+                     int T, const int32_t* seg_len, const int32_t* include, const double* x,
+                     const double* mu, const double* z, int Nt, const double* test_x,
+                     const double* params0, const double* params1, const double* noise, double eps,
+                     double* out, int32_t* info, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Phase timing (profiling aid; the only process-wide state of the library).  When enabled, */

@@ -77,18 +77,40 @@ struct HWs {
   }
 };
 
+// varying T: row q of subject p is valid iff q < seg[p] (seg == NULL: all rows)
+__device__ inline bool seg_valid(const int32_t* __restrict__ seg, int p, int q) { return !seg || q < seg[p]; }
+
+// padding rows of a varying-T batch: K0xz rows -> 0, K0_p rows/cols -> 0, B_p rows/cols -> I
+__global__ void hn_seg_mask_kernel(int L, int P_b, int T, int M, const int32_t* __restrict__ seg,
+                                   double* __restrict__ K0xz, double* __restrict__ K0st, double* __restrict__ Bst) {
+  const int64_t B = (int64_t)P_b * T, nxz = (int64_t)L * B * M, TT = (int64_t)T * T, nst = (int64_t)L * P_b * TT;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nxz) {
+    const int64_t row = (e / M) % B;
+    const int p = (int)(row / T), q = (int)(row % T);
+    if (!seg_valid(seg, p, q)) K0xz[e] = 0.0;
+  } else if (e < nxz + nst) {
+    const int64_t f = e - nxz;
+    const int p = (int)((f / TT) % P_b), i = (int)((f % TT) / T), j = (int)(f % T);
+    if (!seg_valid(seg, p, i) || !seg_valid(seg, p, j)) {
+      K0st[f] = 0.0;
+      Bst[f] = (i == j) ? 1.0 : 0.0;
+    }
+  }
+}
+
 __global__ void fill_kernel(double* p, int n, double v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
 }
 
 // r[l][i] = y[l][i] - mu[i][l]
-__global__ void resid_kernel(const double* __restrict__ y, const double* __restrict__ mu, int B, int L,
-                             double* __restrict__ r) {
+__global__ void resid_kernel(const double* __restrict__ y, const double* __restrict__ mu, int B, int L, int T,
+                             const int32_t* __restrict__ seg, double* __restrict__ r) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * L) return;
   const int l = e / B, i = e % B;
-  r[e] = y[e] - mu[(int64_t)i * L + l];
+  r[e] = seg_valid(seg, i / T, i % T) ? y[e] - mu[(int64_t)i * L + l] : 0.0;
 }
 
 // per-dim partial sums: part[l][0..] = A, Bt, C, D1, D2, E, F, tr1, qf1, ldK, ldH
@@ -101,7 +123,8 @@ __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, i
                                                         const double* __restrict__ Y, const double* __restrict__ H,
                                                         const double* __restrict__ m, const double* __restrict__ t,
                                                         const double* __restrict__ ldK,
-                                                        const double* __restrict__ ldH, double* __restrict__ part) {
+                                                        const double* __restrict__ ldH,
+                                                        const int32_t* __restrict__ seg, double* __restrict__ part) {
   __shared__ double red[4];
   const int l = blockIdx.x, tid = threadIdx.x;
   const int B = P_b * T;
@@ -110,6 +133,7 @@ __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, i
   for (int i = tid; i < B; i += 256) {
     A += r[(int64_t)l * B + i] * s[(int64_t)l * B + i];
     const int p = i / T, q = i % T;
+    if (!seg_valid(seg, p, q)) continue;
     const double lv = logv[(int64_t)i * L + l];
     Bt += iB[l * TT + (int64_t)p * T * T + q * T + q] * exp(lv);
     F += lv;
@@ -137,7 +161,7 @@ __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, i
   }
 }
 
-__global__ void hn_final_kernel(int L, int M, double P_tot, int P_b, int T, const double* __restrict__ part,
+__global__ void hn_final_kernel(int L, int M, double P_tot, int P_b, double n_total, const double* __restrict__ part,
                                 double* __restrict__ kld) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double tot = 0.0;
@@ -148,7 +172,7 @@ __global__ void hn_final_kernel(int L, int M, double P_tot, int P_b, int T, cons
     const double klu = 0.5 * (p[7] + p[8] - (double)M + p[9] - p[10]);
     tot += c0 * 0.5 * inner + klu;
   }
-  kld[0] = tot - (double)L * P_tot * (double)T / 2.0;
+  kld[0] = tot - (double)L * n_total / 2.0;
 }
 
 // y = alpha * x + beta * y  (n elements), optional scale from device scalar: alpha *= *g, beta *= *g
@@ -175,8 +199,8 @@ __global__ void lincomb_kernel(int64_t n, double ax, const double* x, double ay,
 // dmu[i][l] = -2c s[l][i];  dlogv[i][l] = c (iB_ii v_i - 1)
 __global__ void hn_bwd_vec_kernel(int P_b, int T, int L, double k, const double* __restrict__ g,
                                   const double* __restrict__ s, const double* __restrict__ iB,
-                                  const double* __restrict__ logv, double* __restrict__ dmu,
-                                  double* __restrict__ dlogv) {
+                                  const double* __restrict__ logv, const int32_t* __restrict__ seg,
+                                  double* __restrict__ dmu, double* __restrict__ dlogv) {
   const int B = P_b * T;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * L) return;
@@ -184,7 +208,7 @@ __global__ void hn_bwd_vec_kernel(int P_b, int T, int L, double k, const double*
   const double c = k * g[0];
   dmu[(int64_t)i * L + l] = -2.0 * c * s[e];
   const double d = iB[((int64_t)l * P_b + p) * T * T + q * T + q];
-  dlogv[(int64_t)i * L + l] = c * (d * exp(logv[(int64_t)i * L + l]) - 1.0);
+  dlogv[(int64_t)i * L + l] = seg_valid(seg, p, q) ? c * (d * exp(logv[(int64_t)i * L + l]) - 1.0) : 0.0;
 }
 
 // X[l][i][j] += a * u[l][i] * v[l][j]  (a scaled by device g)
@@ -218,20 +242,22 @@ __global__ void giK_kernel(int L, int M, double kc, double kh, const double* __r
 
 // VB[l,p][i][j] = v_{l,p,i} iB[l,p][i][j]
 __global__ void rowscale_v_kernel(int P_b, int T, int L, const double* __restrict__ logv,
-                                  const double* __restrict__ iB, double* __restrict__ VB) {
+                                  const double* __restrict__ iB, const int32_t* __restrict__ seg,
+                                  double* __restrict__ VB) {
   const int64_t TT = (int64_t)T * T;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)L * P_b * TT) return;
   const int lp = (int)(e / TT), l = lp / P_b, p = lp % P_b;
   const int i = (int)((e % TT) / T);
-  VB[e] = exp(logv[((int64_t)p * T + i) * L + l]) * iB[e];
+  VB[e] = seg_valid(seg, p, i) ? exp(logv[((int64_t)p * T + i) * L + l]) * iB[e] : 0.0;
 }
 
 // GB = c (iB - s s^T - iBVB - iBK0iB) - QB ;  GK0 = c iB
 __global__ void gb_kernel(int P_b, int T, int L, double kc, const double* __restrict__ g,
                           const double* __restrict__ iB, const double* __restrict__ s,
                           const double* __restrict__ iBVB, const double* __restrict__ iBK0iB,
-                          const double* __restrict__ QB, double* __restrict__ GB, double* __restrict__ GK0) {
+                          const double* __restrict__ QB, const int32_t* __restrict__ seg,
+                          double* __restrict__ GB, double* __restrict__ GK0) {
   const int64_t TT = (int64_t)T * T;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)L * P_b * TT) return;
@@ -240,8 +266,9 @@ __global__ void gb_kernel(int P_b, int T, int L, double kc, const double* __rest
   const double c = kc * g[0];
   const int B = P_b * T;
   const double si = s[(int64_t)l * B + p * T + i], sj = s[(int64_t)l * B + p * T + j];
-  GB[e] = c * (iB[e] - si * sj - iBVB[e] - iBK0iB[e]) - QB[e];
-  GK0[e] = c * iB[e];
+  const bool ok = seg_valid(seg, p, i) && seg_valid(seg, p, j);
+  GB[e] = ok ? c * (iB[e] - si * sj - iBVB[e] - iBK0iB[e]) - QB[e] : 0.0;
+  GK0[e] = ok ? c * iB[e] : 0.0;
 }
 
 // Y[l][i][j] += a * X[l][j][i]
@@ -311,6 +338,9 @@ int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   LVAE_TRY(lvae_gram_f64(spec0, zv, zv, 1, L, M, M, params0, w.epsv, w.K0zz, 0, MM, M, stream));
   LVAE_TRY(lvae_gram_f64(spec0, xs, xs, P_b, L, T, T, params0, nullptr, w.K0st, TT, P_b * TT, T, stream));
   LVAE_TRY(lvae_gram_f64(spec1, xs, xs, P_b, L, T, T, params1, noise, w.Bst, TT, P_b * TT, T, stream));
+  if (d.seg_len)
+    hn_seg_mask_kernel<<<blocks((int64_t)L * B * M + (int64_t)L * P_b * TT), 256, 0, st>>>(L, P_b, T, M, d.seg_len,
+                                                                                           w.K0xz, w.K0st, w.Bst);
   // factor + inverse (177-186)
   LVAE_TRY(spd_inv_small2_f64(M, L, w.K0zz, MM, w.iK, MM, w.ldK, w.info, L, H, MM, w.iH, MM, w.ldH,
                               w.info + L + L * P_b, st));
@@ -318,7 +348,7 @@ int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   // t = iK m ; r = K0xz t - mu ; s = iB r ; iBK = iB K0xz ; Q = K0xz^T iBK ; Y = iK H iK
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, m, 1, M, 0, 0.0, w.t, 1, M, 0, L, 1, st));
   LVAE_TRY(gemm_small_f64(0, 0, B, 1, M, 1.0, w.K0xz, M, BM, 0, w.t, 1, M, 0, 0.0, w.y, 1, B, 0, L, 1, st));
-  resid_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(w.y, mu, B, L, w.r);
+  resid_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(w.y, mu, B, L, T, d.seg_len, w.r);
   LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, w.r, 1, B, T, 0.0, w.s, 1, B, T, L, P_b, st));
   LVAE_TRY(gemm_small_f64(0, 0, T, M, T, 1.0, w.iB, T, P_b * TT, TT, w.K0xz, M, BM, (int64_t)T * M, 0.0, w.iBK, M,
                           BM, (int64_t)T * M, L, P_b, st));
@@ -327,8 +357,8 @@ int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKH, M, MM, 0, w.iK, M, MM, 0, 0.0, w.Y, M, MM, 0, L, 1, st));
   // partial sums + total (189-204)
   hn_reduce_kernel<<<L, 256, 0, st>>>(M, P_b, T, L, w.r, w.s, w.iB, logv, w.ldB, w.K0st, w.Q, w.iK, w.Y, H, m, w.t,
-                                      w.ldK, w.ldH, w.part);
-  hn_final_kernel<<<1, 64, 0, st>>>(L, M, d.P_tot, P_b, T, w.part, kld);
+                                      w.ldK, w.ldH, d.seg_len, w.part);
+  hn_final_kernel<<<1, 64, 0, st>>>(L, M, d.P_tot, P_b, d.n_total > 0.0 ? d.n_total : d.P_tot * T, w.part, kld);
   // natural-gradient directions (208-214)
   if (d.natural_gradient && grad_m && grad_H) {
     LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, mu, L, 1, (int64_t)T * L, 0.0, w.u, 1, B, T,
@@ -368,7 +398,8 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   const double kc = d.P_tot / (2.0 * P_b), kh = 0.5;
   HWs w((char*)workspace, d);
   // mu / logv
-  hn_bwd_vec_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(P_b, T, L, kc, gkld, w.s, w.iB, logv, dmu, dlogv);
+  hn_bwd_vec_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(P_b, T, L, kc, gkld, w.s, w.iB, logv, d.seg_len, dmu,
+                                                            dlogv);
   // Xq = c (Y - iK)
   lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, kc, w.Y, -kc, w.iK, w.Xq, gkld, 1, 1);
   // dK0xz = 2 iBK Xq + 2c s t^T
@@ -382,7 +413,7 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, kh, w.iK, 0.0, nullptr, w.dK0zz, gkld, 1, 0);
   LVAE_TRY(gemm_small_f64(0, 0, M, M, M, -1.0, w.T1, M, MM, 0, w.iK, M, MM, 0, 1.0, w.dK0zz, M, MM, 0, L, 1, st));
   // dB_p and dK0_p
-  rowscale_v_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, logv, w.iB, w.VB);
+  rowscale_v_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, logv, w.iB, d.seg_len, w.VB);
   LVAE_TRY(gemm_small_f64(0, 0, T, T, T, 1.0, w.iB, T, P_b * TT, TT, w.VB, T, P_b * TT, TT, 0.0, w.iBVB, T,
                           P_b * TT, TT, L, P_b, st));
   LVAE_TRY(gemm_small_f64(0, 0, T, T, T, 1.0, w.K0st, T, P_b * TT, TT, w.iB, T, P_b * TT, TT, 0.0, w.K0iB, T,
@@ -393,7 +424,8 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
                           (int64_t)T * M, L, P_b, st));
   LVAE_TRY(gemm_small_f64(0, 1, T, T, M, 1.0, w.tBM, M, BM, (int64_t)T * M, w.iBK, M, BM, (int64_t)T * M, 0.0, w.QB,
                           T, P_b * TT, TT, L, P_b, st));
-  gb_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, kc, gkld, w.iB, w.s, w.iBVB, w.iBK0iB, w.QB, w.GB, w.GK0);
+  gb_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, kc, gkld, w.iB, w.s, w.iBVB, w.iBK0iB, w.QB, d.seg_len, w.GB,
+                                          w.GK0);
   // hyper-parameter gradients through the four Grams
   (void)hipMemsetAsync(dparams0, 0, sizeof(double) * L * spec0->n_params, st);
   (void)hipMemsetAsync(dparams1, 0, sizeof(double) * L * spec1->n_params, st);

@@ -40,7 +40,8 @@ class XView(ctypes.Structure):
 class HensmanDims(ctypes.Structure):
     _fields_ = [("L", ctypes.c_int32), ("M", ctypes.c_int32), ("P_b", ctypes.c_int32), ("T", ctypes.c_int32),
                 ("Q", ctypes.c_int32), ("P_tot", ctypes.c_double), ("eps", ctypes.c_double),
-                ("natural_gradient", ctypes.c_int32), ("ng_prior_share", ctypes.c_double)]
+                ("natural_gradient", ctypes.c_int32), ("ng_prior_share", ctypes.c_double),
+                ("seg_len", ctypes.c_void_p), ("n_total", ctypes.c_double)]
 
 
 def make_spec(components):
@@ -98,6 +99,9 @@ SIGNATURES = {
     "lvae_natgrad_workspace_size": (_SZ, [_I32, _I32]),
     "lvae_natgrad_update_f64": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _D, _VP, _VP, _VP, _VP]),
     "lvae_hensman_iH_offset": (_SZ, [_DIMS]),
+    "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),
+    "lvae_predict_f64": (_I32, [_SPEC, _SPEC, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP, _VP,
+                                _VP, _VP, _D, _VP, _VP, _VP, _VP]),
     "lvae_prof_enable": (_I32, [_I32]),
     "lvae_prof_collect": (_I32, [_VP, _VP, _I32]),
     "lvae_version": (ctypes.c_char_p, []),

@@ -204,6 +204,63 @@ def minibatch_KLD_upper_bound(covar_module0, covar_module1, likelihood, latent_d
     return kld, gm, gH
 
 
+def _subject_layout(ids):
+    """Host-side layout of a varying-length batch: subjects in torch.unique (sorted) order, each
+    padded to the longest subject.  Returns (gather [P_b*T_max] row indices, valid mask, seg_len
+    [P_b], T_max).  Padding slots point at the subject's first row and are masked out."""
+    ids_c = ids.detach().to("cpu", torch.float64)
+    subjects = torch.unique(ids_c)
+    rows = [torch.nonzero(ids_c == s_, as_tuple=False).reshape(-1) for s_ in subjects]
+    T_max = max(int(r.numel()) for r in rows)
+    gather = torch.empty(len(rows), T_max, dtype=torch.int64)
+    valid = torch.zeros(len(rows), T_max, dtype=torch.bool)
+    for p, r in enumerate(rows):
+        gather[p, :r.numel()] = r
+        gather[p, r.numel():] = r[0]
+        valid[p, :r.numel()] = True
+    seg = torch.tensor([int(r.numel()) for r in rows], dtype=torch.int32)
+    return gather.reshape(-1), valid.reshape(-1), seg, T_max
+
+
+def minibatch_KLD_upper_bound_iter(covar_module0, covar_module1, likelihood, latent_dim, m, H, train_xt, mu, log_v,
+                                   z, P, P_in_current_batch, N, natural_gradient, id_covariate, eps,
+                                   ng_prior_share=1.0):
+    """The Hensman bound for subjects of varying length (elbo_functions.py:219-307), same signature.
+
+    The reference loops over the batch's subjects in Python; here the batch is laid out once as
+    [P_b, T_max] (subject-sorted, as torch.unique orders them) and the whole bound runs in the
+    same HIP kernels as minibatch_KLD_upper_bound with the padding rows masked out
+    (lvae_hensman_dims.seg_len).  Gradients flow back to the caller's mu / log_v rows."""
+    spec0, params0 = kernel_spec_and_params(covar_module0)
+    spec1, params1 = kernel_spec_and_params(covar_module1)
+    L, M = latent_dim, H.shape[-1]
+    if params0.shape[0] == 1 and L > 1:
+        params0 = params0.expand(L, -1)
+    if params1.shape[0] == 1 and L > 1:
+        params1 = params1.expand(L, -1)
+    noise = likelihood.noise_covar.noise.reshape(-1)
+    if noise.numel() == 1 and L > 1:
+        noise = noise.expand(L)
+    dev = mu.device
+    gather, valid, seg, T_max = _subject_layout(train_xt[:, id_covariate])
+    P_b = int(seg.numel())
+    gather_d = gather.to(dev)
+    keep = valid.to(dev, mu.dtype).unsqueeze(1)
+    x_pad = train_xt.detach()[gather_d]
+    mu_pad = mu[gather_d] * keep
+    lv_pad = log_v[gather_d] * keep.to(log_v.dtype)
+    seg_d = seg.to(dev)
+    zz = z if z.dim() == 3 else z.unsqueeze(0).expand(L, -1, -1)
+    # scale P / P_in_current_batch (elbo_functions.py:298) with P_b padded subjects: P_tot' = P P_b / P_in
+    p_tot = float(P) * P_b / float(P_in_current_batch)
+    dims = _lib.HensmanDims(L, M, P_b, int(T_max), int(train_xt.shape[-1]), p_tot, float(eps),
+                            int(bool(natural_gradient)), float(ng_prior_share), seg_d.data_ptr(), float(N))
+    dims.keepalive = seg_d  # the device seg_len array lives as long as the dims (saved for backward)
+    kld, gm, gH = _HensmanFn.apply(params0, params1, noise, mu_pad, lv_pad, m, H, x_pad, zz, spec0, spec1, dims,
+                                   bool(natural_gradient))
+    return kld, gm, gH
+
+
 def natural_gradient_update(m, H, grad_m, grad_H, natural_gradient_lr):
     """training.py:129-135 on the device: returns the updated (m, H) (new tensors, detached)."""
     lib = _lib.lib()

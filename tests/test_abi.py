@@ -35,7 +35,7 @@ def test_spec_struct_layout():
     """ctypes mirror of lvae_kernel_spec matches the C layout (2 + 16*2 + 16*4*3 int32)."""
     from lvae_amd import _lib
     assert ctypes.sizeof(_lib.KernelSpec) == 4 * (2 + 16 * 2 + 16 * 4 * 3)
-    assert ctypes.sizeof(_lib.HensmanDims) == 56  # 5 int32 + pad, 2 double, int32 + pad, double
+    assert ctypes.sizeof(_lib.HensmanDims) == 72  # 5 int32 + pad, 2 double, int32 + pad, double, ptr, double
 
 
 def test_host_queries_need_no_gpu():

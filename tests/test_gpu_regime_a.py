@@ -80,6 +80,55 @@ def test_hensman_golden(hip, name):
         assert rel(H.grad, g["dH"]) < 1e-6
 
 
+@pytest.mark.parametrize("name", ["hensman_iter_ng.npz", "hensman_iter_adam.npz"])
+def test_hensman_iter_varying_T_golden(hip, name):
+    """minibatch_KLD_upper_bound_iter (elbo_functions.py:219-307) on subjects of 5..16 time points,
+    rows in unsorted subject order: padded [P_b, T_max] layout + masked HIP bound vs the reference."""
+    from lvae_amd.elbo import minibatch_KLD_upper_bound_iter
+    g = golden(name)
+    k0, k1, lik = build(g)
+    ng = bool(g["natural_gradient"])
+    X = torch.tensor(g["X_all"][g["idx"]], device=DEV)
+    mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+    lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+    m = torch.tensor(g["m"], device=DEV, requires_grad=not ng)
+    H = torch.tensor(g["H"], device=DEV, requires_grad=not ng)
+    kld, gm, gH = minibatch_KLD_upper_bound_iter(k0, k1, lik, int(g["L"]), m, H, X, mu, lv,
+                                                 torch.tensor(g["Z"], device=DEV), int(g["P_tot"]),
+                                                 int(g["P_in_batch"]), int(g["N"]), ng, int(g["id_covariate"]),
+                                                 float(g["eps"]))
+    kld.backward()
+    assert rel(kld, g["kld"]) < 1e-8
+    assert rel(mu.grad, g["dmu"]) < 1e-6
+    assert rel(lv.grad, g["dlogv"]) < 1e-6
+    d0 = torch.stack([p.grad for _, p in k0.named_parameters()])
+    d1 = torch.stack([p.grad for _, p in k1.named_parameters()])
+    assert rel(d0, g["draw0"]) < 1e-6
+    assert rel(d1, g["draw1"]) < 1e-4
+    if ng:
+        assert rel(gm, g["grad_m"]) < 1e-6
+        assert rel(gH, g["grad_H"]) < 1e-6
+    else:
+        assert rel(m.grad, g["dm"]) < 1e-6
+        assert rel(H.grad, g["dH"]) < 1e-6
+
+
+def test_hensman_iter_uniform_T_matches_fixed(hip):
+    """With every subject at T rows the _iter variant equals the reference's _iter output (and the
+    fixed-T bound) on the same batch."""
+    from lvae_amd.elbo import minibatch_KLD_upper_bound_iter
+    g = golden("hensman_ng.npz")
+    k0, k1, lik = build(g)
+    X = torch.tensor(g["X_all"][g["idx"]], device=DEV)
+    kld, gm, gH = minibatch_KLD_upper_bound_iter(k0, k1, lik, int(g["L"]), torch.tensor(g["m"], device=DEV),
+                                                 torch.tensor(g["H"], device=DEV), X,
+                                                 torch.tensor(g["mu"], device=DEV), torch.tensor(g["logv"], device=DEV),
+                                                 torch.tensor(g["Z"], device=DEV), int(g["P_tot"]), int(g["P_b"]),
+                                                 int(g["P_tot"]) * int(g["T"]), True, 2, float(g["eps"]))
+    assert rel(kld, g["kld_iter"]) < 1e-8
+    assert rel(gm, g["grad_m_iter"]) < 1e-6
+
+
 def test_hensman_noise_gradient(hip):
     """A trainable noise (constrain_scales=False) gets d kld / d noise = sum_p tr(dB_p) (vs oracle)."""
     import lvae_amd as la
@@ -261,3 +310,59 @@ def test_hensman_step_vs_oracle(hip):
     assert rel(step.H, H_ref) < 1e-4
     d0 = torch.stack([p.grad for _, p in k0.named_parameters()], 1)
     assert rel(d0, raw0.grad) < 1e-4
+
+
+def test_batch_predict_varying_T_golden(hip):
+    """utils.batch_predict_varying_T (utils.py:115-211) through lvae_predict_f64: 12 prediction
+    subjects of 5..16 points, 4 test subjects (rows in unsorted subject order)."""
+    from lvae_amd.predict import batch_predict_varying_T
+    g = golden("predict_varying.npz")
+    k0, k1, lik = build(g)
+    X = g["X_all"]
+    zp = batch_predict_varying_T(int(g["L"]), k0, k1, lik, torch.tensor(X[g["pidx"]], device=DEV),
+                                 torch.tensor(X[g["tidx"]], device=DEV), torch.tensor(g["mu"], device=DEV),
+                                 torch.tensor(g["Z"], device=DEV), int(g["id_covariate"]), float(g["eps"]))
+    assert tuple(zp.shape) == g["Z_pred"].shape
+    # Z_pred applies K0zz^-1 (cond ~1e8 with the 1e-6 jitter) and H^-1: the reference LU-solves
+    # (torch.solve), the HIP path multiplies by the Cholesky-based inverse -> cond * eps ~ 1e-7
+    assert rel(zp, g["Z_pred"]) < 1e-6
+
+
+def test_gpapprox_elbo_and_dubo_golden(hip):
+    """Full-batch GPapprox ELBO (elbo_functions.py:36-84) and DUBO (86-142) of one latent dim:
+    values and autograd gradients (y / mu / log_v and raw kernel parameters) vs the reference."""
+    import lvae_amd as la
+    g = golden("gpapprox.npz")
+    P, T = int(g["P"]), int(g["T"])
+    X, Z = torch.tensor(g["X"], device=DEV), torch.tensor(g["Z"], device=DEV)
+
+    def kernels():
+        k0, k1 = la.generate_kernel_batched(1, **CFG, id_covariate=2)
+        set_raw(k0, g["raw0"].T)
+        set_raw(k1, g["raw1"].T)
+        lik = la.GaussianLikelihood(1, noise=float(g["noise"])).to(DEV)
+        return k0.to(DEV), k1.to(DEV), lik
+
+    k0, k1, lik = kernels()
+    y = torch.tensor(g["y"], device=DEV, requires_grad=True)
+    el = la.elbo(k0, k1, lik, X, y, Z, P, T, float(g["eps"]))
+    el.backward()
+    assert rel(el, g["elbo"]) < 1e-9
+    assert rel(y.grad, g["elbo_dy"]) < 1e-7
+    assert rel(torch.cat([p.grad for _, p in k0.named_parameters()]), g["elbo_draw0"][:, 0]) < 1e-6
+    assert rel(torch.cat([p.grad for _, p in k1.named_parameters()]), g["elbo_draw1"][:, 0]) < 1e-6
+    k0, k1, lik = kernels()
+    mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+    lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+    du = la.deviance_upper_bound(k0, k1, lik, X, mu, lv, Z, P, T, float(g["eps"]))
+    du.backward()
+    assert rel(du, g["dubo"]) < 1e-9
+    assert rel(mu.grad, g["dubo_dmu"]) < 1e-7
+    assert rel(lv.grad, g["dubo_dlogv"]) < 1e-7
+    assert rel(torch.cat([p.grad for _, p in k0.named_parameters()]), g["dubo_draw0"][:, 0]) < 1e-6
+    assert rel(torch.cat([p.grad for _, p in k1.named_parameters()]), g["dubo_draw1"][:, 0]) < 1e-6
+    # validation_dubo with batched kernels == sum of per-dim DUBOs (here one dim)
+    k0, k1, lik = kernels()
+    vd = la.validation_dubo(1, k0, k1, lik, X, torch.tensor(g["mu"], device=DEV)[:, None],
+                            torch.tensor(g["logv"], device=DEV)[:, None], Z[None], P, T, float(g["eps"]))
+    assert rel(vd, g["dubo"]) < 1e-9
