@@ -444,6 +444,34 @@ def gen_vae(L, B, seed):
                 mse=mse.detach().numpy(), nll=nll.detach().numpy(), loss=loss.item(), **grads)
 
 
+# ----------------------------------------------------------------------------------------------
+# 5. data ingest: HealthMNISTDatasetConv (dataset_def.py:172-219) on a tiny CSV trio written in
+#    Health_MNIST_generate.py's format (fixture files committed under tests/golden/hmnist_tiny/)
+# ----------------------------------------------------------------------------------------------
+def gen_hmnist_tiny(seed):
+    sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "longitudinal-vae_amd"))
+    from lvae_amd.data import write_health_mnist_csv  # our writer (format under test)
+    import dataset_def as RD  # noqa: E402  (reference)
+    rng = np.random.default_rng(seed)
+    P, T = 3, 4
+    N = P * T
+    pixels = rng.integers(0, 256, size=(N, 1296))
+    mask = rng.binomial(1, 0.75, size=(N, 1296))
+    labels = np.zeros((N, 8))
+    for r in range(N):
+        p, t = divmod(r, T)
+        sick = p % 2
+        labels[r] = [p, 5, 0.0, sick, (t - 2) if sick else np.nan, p >= 1, t, (p + 1) % 2]
+    d = os.path.join(OUT, "hmnist_tiny")
+    os.makedirs(d, exist_ok=True)
+    fd, fl, fm = write_health_mnist_csv(d, pixels, mask, labels, prefix="tiny")
+    ds = RD.HealthMNISTDatasetConv(csv_file_data=fd, csv_file_label=fl, mask_file=fm, root_dir=d, transform=None)
+    items = [ds[i] for i in range(len(ds))]
+    return dict(files=np.array([fd, fl, fm]), digit=np.stack([it["digit"] for it in items]),
+                label=np.stack([it["label"].numpy() for it in items]), mask=np.stack([it["mask"] for it in items]),
+                n=len(ds))
+
+
 def main():
     save("kl_closed_n64.npz", **gen_kl_closed(P=4, T=16, L=2, seed=0, noise=1.0, store_gram=True))
     save("kl_closed_n256.npz", **gen_kl_closed(P=16, T=16, L=2, seed=1, noise=1.0, store_gram=False))
@@ -459,6 +487,7 @@ def main():
                                                    lengths=[16, 11, 7, 14, 9], natural_gradient=True))
     save("hensman_iter_adam.npz", **gen_hensman_iter(P_tot=24, T=16, L=2, M=40, seed=9,
                                                      lengths=[5, 16, 12], natural_gradient=False))
+    save("hmnist_tiny.npz", **gen_hmnist_tiny(seed=11))
     save("predict_varying.npz", **gen_predict(P=12, T=16, L=3, M=40, seed=10,
                                               pred_lengths=[16, 9, 12, 16, 5, 14, 16, 8, 11, 16, 13, 7],
                                               test_subjects=[3, 0, 7, 10], test_lengths=[6, 4, 10, 3]))
