@@ -16,10 +16,42 @@
 // tiles, Lt -> Y below), Ainv.  Grids are (tiles, L): all latent dims share every launch.
 #include "mfma_tile.hpp"
 #include "blkinv.hpp"
+#include "mfma_x3.hpp"
+
+#include <cstdlib>
 
 namespace lvae {
 
 constexpr int kNB = 128;
+
+// GEMM engine per kernel: fp32-input MFMA (exact fp32 products) or the 3-product f16 split
+// (mfma_x3.hpp, ~2^-22 per product, 3/16 of the cost).  Bit i of the mask selects X3 for
+// kernel class i (GemmClass); LVAE_X3 in the environment overrides the default.
+enum GemmClass { GC_PANEL = 0, GC_UPDATE = 1, GC_TRTRI = 2, GC_Z = 3, GC_LAUUM = 4, GC_SYRK = 5 };
+constexpr int kX3DefaultMask = 0x3f;  // all classes: KL/grad parity within 1e-4 (tests), 1.36x step
+inline int x3_mask() {
+  static const int m = [] {
+    const char* e = getenv("LVAE_X3");
+    return e ? (int)strtol(e, nullptr, 0) : kX3DefaultMask;
+  }();
+  return m;
+}
+inline bool use_x3(GemmClass c) { return (x3_mask() >> c) & 1; }
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+template <bool AK, bool BK_>
+constexpr int gemm_lds_bytes() {
+  return cmax(tile_lds_floats<AK, BK_>() * (int)sizeof(float), x3_lds_bytes());
+}
+
+template <bool X3, bool AK, bool BKc, bool NEG = false>
+__device__ inline void tile_gemm_any(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                     int kbeg, int kend, Frag& f, void* lds, const float* __restrict__ ascale = nullptr) {
+  if constexpr (X3)
+    tile_gemm_x3<AK, BKc, NEG>(A, lda, B, ldb, kbeg, kend, f, (_Float16*)lds, ascale);
+  else
+    tile_gemm<AK, BKc, NEG>(A, lda, B, ldb, kbeg, kend, f, (float*)lds, ascale);
+}
 
 __device__ inline void tri_index2(int t, int& I, int& J) {
   int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -39,25 +71,27 @@ __global__ __launch_bounds__(1024) void ldl_diag_kernel(const float* __restrict_
 }
 
 // panel: W_ik = A_ik D_k^-1 for tile rows i > kb
+template <bool X3>
 __global__ __launch_bounds__(256) void ldl_panel_kernel(const float* __restrict__ Aall, float* __restrict__ Wall,
                                                         int np_, int kb) {
-  __shared__ __attribute__((aligned(16))) float lds[tile_lds_floats<true, true>()];
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<true, true>()];
   const int l = blockIdx.y, i = kb + 1 + blockIdx.x;
   const float* A = Aall + (int64_t)l * np_ * np_;
   float* W = Wall + (int64_t)l * np_ * np_;
   Frag f;
   f.zero();
   // op(B)(k, n) = Dinv[k][n] = Dinv[n][k]: k-contiguous rows of the symmetric W_kk
-  tile_gemm<true, true>(A + (int64_t)i * kNB * np_ + kb * kNB, np_, W + (int64_t)kb * kNB * np_ + kb * kNB, np_, 0,
+  tile_gemm_any<X3, true, true>(A + (int64_t)i * kNB * np_ + kb * kNB, np_, W + (int64_t)kb * kNB * np_ + kb * kNB, np_, 0,
                         kNB, f, lds);
   float* C = W + (int64_t)i * kNB * np_ + kb * kNB;
   frag_foreach(f, [&](int r, int c, float v) { C[(int64_t)r * np_ + c] = v; });
 }
 
 // update: A_ij -= W_ik A_jk^T, kb < j <= i
+template <bool X3>
 __global__ __launch_bounds__(256) void ldl_update_kernel(float* __restrict__ Aall, const float* __restrict__ Wall,
                                                          int np_, int kb) {
-  __shared__ __attribute__((aligned(16))) float lds[tile_lds_floats<true, true>()];
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<true, true>()];
   int I, J;
   tri_index2(blockIdx.x, I, J);
   const int l = blockIdx.y, i = kb + 1 + I, j = kb + 1 + J;
@@ -66,28 +100,30 @@ __global__ __launch_bounds__(256) void ldl_update_kernel(float* __restrict__ Aal
   float* C = A + (int64_t)i * kNB * np_ + j * kNB;
   Frag f;
   frag_load(f, C, np_);
-  tile_gemm<true, true, true>(W + (int64_t)i * kNB * np_ + kb * kNB, np_, A + (int64_t)j * kNB * np_ + kb * kNB, np_,
+  tile_gemm_any<X3, true, true, true>(W + (int64_t)i * kNB * np_ + kb * kNB, np_, A + (int64_t)j * kNB * np_ + kb * kNB, np_,
                               0, kNB, f, lds);
   frag_foreach(f, [&](int r, int c, float v) { C[(int64_t)r * np_ + c] = v; });
 }
 
 // trtri step jb: W_rc -= W_r,jb W_jb,c   (r > jb > c)
+template <bool X3>
 __global__ __launch_bounds__(256) void ldl_trtri_kernel(float* __restrict__ Wall, int np_, int jb) {
-  __shared__ __attribute__((aligned(16))) float lds[tile_lds_floats<true, false>()];
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<true, false>()];
   const int l = blockIdx.y, r = jb + 1 + blockIdx.x / jb, c = blockIdx.x % jb;
   float* W = Wall + (int64_t)l * np_ * np_;
   float* C = W + (int64_t)r * kNB * np_ + c * kNB;
   Frag f;
   frag_load(f, C, np_);
-  tile_gemm<true, false, true>(W + (int64_t)r * kNB * np_ + jb * kNB, np_, W + (int64_t)jb * kNB * np_ + c * kNB, np_,
+  tile_gemm_any<X3, true, false, true>(W + (int64_t)r * kNB * np_ + jb * kNB, np_, W + (int64_t)jb * kNB * np_ + c * kNB, np_,
                                0, kNB, f, lds);
   frag_foreach(f, [&](int rr, int cc, float v) { C[(int64_t)rr * np_ + cc] = v; });
 }
 
 // Z_KJ = -D_K^-1 Y_KJ (K > J), into A's tile (K, J)
+template <bool X3>
 __global__ __launch_bounds__(256) void ldl_z_kernel(float* __restrict__ Aall, const float* __restrict__ Wall,
                                                     int np_) {
-  __shared__ __attribute__((aligned(16))) float lds[tile_lds_floats<true, false>()];
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<true, false>()];
   int I, J;
   tri_index2(blockIdx.x, I, J);  // strictly lower: (I + 1, J)
   const int K = I + 1, l = blockIdx.y;
@@ -95,16 +131,17 @@ __global__ __launch_bounds__(256) void ldl_z_kernel(float* __restrict__ Aall, co
   const float* W = Wall + (int64_t)l * np_ * np_;
   Frag f;
   f.zero();
-  tile_gemm<true, false, true>(W + (int64_t)K * kNB * np_ + K * kNB, np_, W + (int64_t)K * kNB * np_ + J * kNB, np_,
+  tile_gemm_any<X3, true, false, true>(W + (int64_t)K * kNB * np_ + K * kNB, np_, W + (int64_t)K * kNB * np_ + J * kNB, np_,
                                0, kNB, f, lds);
   float* C = A + (int64_t)K * kNB * np_ + J * kNB;
   frag_foreach(f, [&](int r, int c, float v) { C[(int64_t)r * np_ + c] = v; });
 }
 
 // lauum: Ainv_IJ = Z_IJ - sum_{K > I} Y_KI^T Z_KJ  (I >= J), mirrored into the upper triangle
+template <bool X3>
 __global__ __launch_bounds__(256) void ldl_lauum_kernel(const float* __restrict__ Zall, const float* __restrict__ Wall,
                                                         float* __restrict__ Ball, int np_) {
-  __shared__ __attribute__((aligned(16))) float lds[tile_lds_floats<false, false>()];
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<false, false>()];
   int I, J;
   tri_index2(blockIdx.x, I, J);
   const int l = blockIdx.y;
@@ -114,7 +151,7 @@ __global__ __launch_bounds__(256) void ldl_lauum_kernel(const float* __restrict_
   Frag f;
   if (I == J) frag_load(f, W + (int64_t)I * kNB * np_ + I * kNB, np_);
   else frag_load(f, Z + (int64_t)I * kNB * np_ + J * kNB, np_);
-  tile_gemm<false, false, true>(W + I * kNB, np_, Z + J * kNB, np_, (I + 1) * kNB, np_, f, lds);
+  tile_gemm_any<X3, false, false, true>(W + I * kNB, np_, Z + J * kNB, np_, (I + 1) * kNB, np_, f, lds);
   float* C = B + (int64_t)I * kNB * np_ + J * kNB;
   float* Ct = B + (int64_t)J * kNB * np_ + I * kNB;
   const bool mirror = I != J;
@@ -125,9 +162,10 @@ __global__ __launch_bounds__(256) void ldl_lauum_kernel(const float* __restrict_
 }
 
 // S = B diag(v) B (lower tiles), B symmetric: S_IJ = sum_k B[I m][k] v_k B[J n][k]
+template <bool X3>
 __global__ __launch_bounds__(256) void syrk_scaled_kernel(const float* __restrict__ Ball, const float* __restrict__ vall,
                                                           float* __restrict__ Sall, int np_) {
-  __shared__ __attribute__((aligned(16))) float lds[tile_lds_floats<true, true>()];
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<true, true>()];
   int I, J;
   tri_index2(blockIdx.x, I, J);
   const int l = blockIdx.y;
@@ -135,7 +173,7 @@ __global__ __launch_bounds__(256) void syrk_scaled_kernel(const float* __restric
   const float* v = vall + (int64_t)l * np_;
   Frag f;
   f.zero();
-  tile_gemm<true, true>(B + (int64_t)I * kNB * np_, np_, B + (int64_t)J * kNB * np_, np_, 0, np_, f, lds, v);
+  tile_gemm_any<X3, true, true>(B + (int64_t)I * kNB * np_, np_, B + (int64_t)J * kNB * np_, np_, 0, np_, f, lds, v);
   float* C = Sall + (int64_t)l * np_ * np_ + (int64_t)I * kNB * np_ + J * kNB;
   frag_foreach(f, [&](int r, int c, float val) { C[(int64_t)r * np_ + c] = val; });
 }
@@ -153,8 +191,8 @@ int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info,
     ldl_diag_kernel<<<L, 1024, 0, st>>>(A, W, np_, kb, logdet, info);
     const int T = nt - kb - 1;
     if (T > 0) {
-      ldl_panel_kernel<<<dim3(T, L), 256, 0, st>>>(A, W, np_, kb);
-      ldl_update_kernel<<<dim3(T * (T + 1) / 2, L), 256, 0, st>>>(A, W, np_, kb);
+      (use_x3(GC_PANEL) ? ldl_panel_kernel<true> : ldl_panel_kernel<false>)<<<dim3(T, L), 256, 0, st>>>(A, W, np_, kb);
+      (use_x3(GC_UPDATE) ? ldl_update_kernel<true> : ldl_update_kernel<false>)<<<dim3(T * (T + 1) / 2, L), 256, 0, st>>>(A, W, np_, kb);
     }
   }
   LVAE_CHECK_LAUNCH();
@@ -164,16 +202,16 @@ int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info,
 int potri_f32(int np_, int L, float* A, float* W, float* Ainv, hipStream_t st) {
   if (np_ <= 0 || np_ % kNB) return -1;
   const int nt = np_ / kNB;
-  for (int jb = 1; jb + 1 < nt; ++jb) ldl_trtri_kernel<<<dim3((nt - jb - 1) * jb, L), 256, 0, st>>>(W, np_, jb);
-  if (nt > 1) ldl_z_kernel<<<dim3(nt * (nt - 1) / 2, L), 256, 0, st>>>(A, W, np_);
-  ldl_lauum_kernel<<<dim3(nt * (nt + 1) / 2, L), 256, 0, st>>>(A, W, Ainv, np_);
+  for (int jb = 1; jb + 1 < nt; ++jb) (use_x3(GC_TRTRI) ? ldl_trtri_kernel<true> : ldl_trtri_kernel<false>)<<<dim3((nt - jb - 1) * jb, L), 256, 0, st>>>(W, np_, jb);
+  if (nt > 1) (use_x3(GC_Z) ? ldl_z_kernel<true> : ldl_z_kernel<false>)<<<dim3(nt * (nt - 1) / 2, L), 256, 0, st>>>(A, W, np_);
+  (use_x3(GC_LAUUM) ? ldl_lauum_kernel<true> : ldl_lauum_kernel<false>)<<<dim3(nt * (nt + 1) / 2, L), 256, 0, st>>>(A, W, Ainv, np_);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
 
 int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st) {
   const int nt = np_ / kNB;
-  syrk_scaled_kernel<<<dim3(nt * (nt + 1) / 2, L), 256, 0, st>>>(B, v, S, np_);
+  (use_x3(GC_SYRK) ? syrk_scaled_kernel<true> : syrk_scaled_kernel<false>)<<<dim3(nt * (nt + 1) / 2, L), 256, 0, st>>>(B, v, S, np_);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,52 @@
+"""Print the relative errors of the exact-KL path vs the fp64 oracle (values and gradients) for
+the current LVAE_X3 engine mask -- how much of the 1e-4 budget each GEMM engine uses."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "longitudinal-vae_amd"))
+sys.path.insert(0, ROOT)
+import lvae_amd as la  # noqa: E402
+from lvae_amd.data import health_mnist_covariates  # noqa: E402
+from oracle import lvae_oracle as O  # noqa: E402
+
+CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+           cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2}, {'cont_covariate': 0, 'cat_covariate': 3},
+                           {'cont_covariate': 1, 'cat_covariate': 4}], bin_int_kernel=[], covariate_missing_val=[])
+
+
+def rel(a, b):
+    a, b = a.detach().cpu().double().numpy(), b.detach().cpu().double().numpy()
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def main():
+    for P in (64, 128):
+        T, L = 16, 2
+        X = torch.tensor(health_mnist_covariates(P, T, seed=P))
+        gen = torch.Generator().manual_seed(P)
+        mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+        lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+        k = la.generate_kernel(**CFG, latent_dim=L).double()
+        raw = torch.stack([p.detach() for _, p in k.named_parameters()], 1)
+        kd = k.cuda()
+        lik = la.GaussianLikelihood(L, noise=1.0).cuda()
+        mu_d, lv_d = mu.cuda().requires_grad_(), lv.cuda().requires_grad_()
+        kl = la.KL_closed_batched(kd, X.cuda(), lik, mu_d, lv_d)
+        kl.sum().backward()
+        spec = O.spec_full(**CFG)
+        for l in range(L):
+            r = raw[l].clone().requires_grad_()
+            m_, v_ = mu[:, l].clone().requires_grad_(), lv[:, l].clone().requires_grad_()
+            ref = O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_)
+            ref.backward()
+            draw = torch.stack([p.grad[l] for _, p in kd.named_parameters()])
+            print(f"N={P * T} l={l} kl {rel(kl[l], ref):.2e} dmu {rel(mu_d.grad[:, l], m_.grad):.2e} "
+                  f"dlogv {rel(lv_d.grad[:, l], v_.grad):.2e} draw {rel(draw, r.grad):.2e}")
+
+
+if __name__ == "__main__":
+    main()
