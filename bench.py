@@ -31,6 +31,23 @@ CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
                            {'cont_covariate': 1, 'cat_covariate': 4}],
            bin_int_kernel=[], covariate_missing_val=[])
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA peak
+F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense f16/bf16 MFMA peak (~2.5 PF, no sparsity)
+X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product (mfma_x3.hpp)
+# Memory-side bytes per syrk launch from the committed rocprofv3 PMC passes (scripts/pmc.sh ->
+# profiles/r1_v5_pmc_summary.json: FETCH_SIZE / WRITE_SIZE in KiB per dispatch; FETCH_SIZE x 2 for
+# 16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM").  Counts L2 misses incl.
+# Infinity-Cache hits, so it bounds HBM traffic from above.
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_v5_pmc_summary.json")
+
+
+def pmc_traffic(kernel_prefix):
+    try:
+        d = json.load(open(PMC_SUMMARY))
+        f = [v["mean"] for k, v in d["FETCH_SIZE"].items() if kernel_prefix in k]
+        w = [v["mean"] for k, v in d["WRITE_SIZE"].items() if kernel_prefix in k]
+        return (2 * f[0] + w[0]) * 1024 if f and w else None
+    except (OSError, KeyError, ValueError):
+        return None
 HBM_PEAK_GBS = 8000.0
 
 
@@ -178,12 +195,18 @@ def main():
             res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
             # dominant kernel: S = K^-1 V K^-1 (syrk_scaled_kernel, one launch per step):
             # algorithmic flops per launch = L * N^2 (N+1)  (lower triangle incl. diagonal, 2 flop/FMA)
-            flops = L * N * N * (N + 1)
+            # (np = N here).  Engine: fp32-input MFMA -> peak 157.3; 3-product f16 split -> the f16
+            # dense peak / 3 (each algorithmic fp32 FMA costs three f16 MFMA FMAs).
+            flops = L * np_ * np_ * (np_ + 1)
             achieved = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
+            x3 = bool((_lib.load().lvae_gemm_engine_mask() >> 5) & 1)
+            peak = F16_MFMA_PEAK_TFLOPS / X3_PRODUCTS if x3 else FP32_MFMA_PEAK_TFLOPS
             res["roofline"] = {"kernel": "syrk_scaled_kernel (K^-1 V K^-1)", "bound": "mfma",
-                               "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
-                               "traffic": None, "padded_n": int(np_)}
+                               "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                               "frac": (achieved / peak) if achieved else None,
+                               "traffic": pmc_traffic("syrk_scaled_kernel<true>" if x3 else "syrk_scaled_kernel<false>"), "padded_n": int(np_),
+                               "engine": ("f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)" if x3
+                                          else "fp32-input MFMA")}
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(P, T, L)
             res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]

@@ -219,6 +219,11 @@ enum lvae_phase {
 int lvae_prof_enable(int on);
 int lvae_prof_collect(double* ms, int32_t* count, int n_phases);
 
+/* GEMM engine of the Regime B tile GEMMs: bit c set = the fp32-accurate 3-product f16 split
+ * (mfma_x3.hpp) for kernel class c (0 panel, 1 update, 2 trtri, 3 z, 4 lauum, 5 syrk), clear =
+ * fp32-input MFMA.  Default 0x3f; the LVAE_X3 environment variable overrides it.            */
+int lvae_gemm_engine_mask(void);
+
 /* library identification: "lvae_hip <version> gfx950" */
 const char* lvae_version(void);
 

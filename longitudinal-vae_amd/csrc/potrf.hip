@@ -219,6 +219,7 @@ int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hi
 }  // namespace lvae
 
 extern "C" {
+int lvae_gemm_engine_mask(void) { return lvae::x3_mask(); }
 int lvae_potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, void* stream) {
   return lvae::potrf_f32(np_, L, A, W, logdet, info, (hipStream_t)stream);
 }

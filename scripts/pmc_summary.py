@@ -1,0 +1,34 @@
+"""Summarise rocprofv3 --pmc counter_collection.csv files into per-kernel mean counter values
+(one row per dispatch in the raw file; the raw files are too big to keep)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main(out_dir):
+    res = {}
+    for path in glob.glob(os.path.join(out_dir, "*", "*counter_collection.csv")):
+        acc = defaultdict(lambda: [0.0, 0])
+        counter = None
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Kernel_Name", "")
+                counter = row.get("Counter_Name", counter)
+                v = float(row.get("Counter_Value", 0.0))
+                a = acc[(name, counter)]
+                a[0] += v
+                a[1] += 1
+        for (name, c), (s, n) in acc.items():
+            res.setdefault(c, {})[name] = {"mean": s / n, "dispatches": n}
+    with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    for c, d in res.items():
+        for name, v in sorted(d.items(), key=lambda kv: -kv[1]["mean"] * kv[1]["dispatches"])[:12]:
+            print(f"{c:12s} {v['mean']:14.1f} x{v['dispatches']:4d}  {name[:100]}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
