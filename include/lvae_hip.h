@@ -117,6 +117,15 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
                            const double* gkl, double* dmu, double* dlogv, double* dparams, double* dnoise,
                            void* workspace, void* stream);
 
+/* A^-1 and log|A| of L padded SPD matrices by recursive Schur complements (the Regime B path):
+ * A = [[A11, A21^T], [A21, A22]]: A11^-1, X = A21 A11^-1, S = A22 - X A21^T, S^-1, Y = S^-1 X,
+ * A^-1 = [[A11^-1 + X^T Y, -Y^T], [-Y, S^-1]], log|A| = log|A11| + log|S|; leaves 128 x 128.
+ * A [L, np, np] (lower 128-tiles read; A's lower tiles are overwritten by Schur complements),
+ * W [L, np, np] scratch, Ainv [L, np, np] full symmetric out; logdet [L]; info [L] LAPACK-style.
+ * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
+int lvae_spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info,
+                         void* stream);
+
 /* Blocked factorisation of L padded SPD matrices (in place, fp32 MFMA): right-looking block LDL^T
  * with 128-wide pivot blocks, K = Lt Dt Lt^T (the Cholesky factor is Lt chol(Dt)).  On return W's
  * diagonal tiles hold D_k^-1, its strictly-lower tiles Lt; logdet[l] = log|A_l|, info[l] LAPACK-style.
@@ -220,8 +229,9 @@ int lvae_prof_enable(int on);
 int lvae_prof_collect(double* ms, int32_t* count, int n_phases);
 
 /* GEMM engine of the Regime B tile GEMMs: bit c set = the fp32-accurate 3-product f16 split
- * (mfma_x3.hpp) for kernel class c (0 panel, 1 update, 2 trtri, 3 z, 4 lauum, 5 syrk), clear =
- * fp32-input MFMA.  Default 0x3f; the LVAE_X3 environment variable overrides it.            */
+ * (mfma_x3.hpp) for kernel class c (0 panel, 1 update, 2 trtri, 3 z, 4 lauum, 5 syrk,
+ * 6 recursive inverse), clear = fp32-input MFMA.  Default 0x7f; LVAE_X3 in the environment
+ * overrides it.                                                                              */
 int lvae_gemm_engine_mask(void);
 
 /* library identification: "lvae_hip <version> gfx950" */

@@ -13,6 +13,8 @@
 #include "common.hpp"
 #include "prof.hpp"
 
+#include <cstdlib>
+
 namespace lvae {
 
 int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
@@ -23,6 +25,7 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
                 double* part, double* dparams, double* dnoise, hipStream_t st);
 int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, hipStream_t st);
 int potri_f32(int np_, int L, float* A, float* W, float* Ainv, hipStream_t st);
+int spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info, hipStream_t st);
 int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st);
 
 struct KLWorkspace {
@@ -147,12 +150,22 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
     kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v);
   }
   {
-    ProfScope ps(LVAE_PH_POTRF, st);
-    LVAE_TRY(potrf_f32(np_, L, ws.A, ws.W, ws.logdet, info, st));
-  }
-  {
-    ProfScope ps(LVAE_PH_POTRI, st);
-    LVAE_TRY(potri_f32(np_, L, ws.A, ws.W, ws.Kinv, st));
+    // K^-1 and log|K|: block LDL^T (128-wide pivots) + inverse.  The recursive Schur-complement
+    // inverse (LVAE_KL_REC=1) is ~1.2 ms/step faster at C3 but multiplies by explicit inverses of
+    // blocks up to N/2 wide: at N = 4096 its dmu / dlogv errors reach 9e-5 of the 1e-4 budget
+    // (LDL^T: 2e-5), so it is not the default.
+    static const bool rec = getenv("LVAE_KL_REC") && atoi(getenv("LVAE_KL_REC"));
+    if (rec) {
+      ProfScope ps(LVAE_PH_POTRF, st);
+      LVAE_TRY(spd_inverse_f32(np_, L, ws.A, ws.W, ws.Kinv, ws.logdet, info, st));
+    } else {
+      {
+        ProfScope ps(LVAE_PH_POTRF, st);
+        LVAE_TRY(potrf_f32(np_, L, ws.A, ws.W, ws.logdet, info, st));
+      }
+      ProfScope ps(LVAE_PH_POTRI, st);
+      LVAE_TRY(potri_f32(np_, L, ws.A, ws.W, ws.Kinv, st));
+    }
   }
   {
     ProfScope ps(LVAE_PH_KL_REDUCE, st);

@@ -10,12 +10,11 @@
 // Same interface as tile_gemm (mfma_tile.hpp): 256 threads = 2x2 waves of 64x64, the fp32 Frag
 // accumulators (the 32x32 C/D layout is dtype-independent on gfx950), fp32 operands in global
 // memory with k contiguous (KCONT) or rows contiguous (!KCONT), optional per-k scale of op(A),
-// NEG for acc -= op(A) op(B).  K chunks of 32, register prefetch of the next chunk.
+// NEG for acc -= op(A) op(B).  K chunks of kX3BK, register prefetch of the next chunk.
 //
 // f16 operand maps (cdna_hip_programming.md §3): lane l holds A[row l&31][k = 8(l>>5) + j] and
 // B[k = 8(l>>5) + j][col l&31], j = 0..7 -- both read as 8 contiguous halves of one LDS row
-// [row][k] (pitch 40 halves = 80 B: the 16 lanes of a ds_read_b128 phase hit 16 distinct
-// 4-bank groups).
+// [row][k] (pitch kX3BK + 8 halves: 16 lanes of a ds_read_b128 phase start 16 B-groups apart).
 #pragma once
 #include "mfma_tile.hpp"
 
@@ -24,10 +23,14 @@ namespace lvae {
 typedef _Float16 x3_half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 x3_half4 __attribute__((ext_vector_type(4)));
 
-constexpr int kX3Ld = kBK + 8;                  // LDS row pitch in halves
-constexpr int kX3Op = kTM * kX3Ld;              // halves per operand part (hi or lo)
-constexpr float kX3Scale = 256.0f;              // per-operand scale (exact power of two)
-constexpr float kX3Unscale = 1.0f / 65536.0f;   // 1 / scale^2
+#ifndef LVAE_X3_BK
+#define LVAE_X3_BK 32
+#endif
+constexpr int kX3BK = LVAE_X3_BK;              // K chunk per LDS stage
+constexpr int kX3Ld = kX3BK + 8;               // LDS row pitch in halves (16-B aligned rows)
+constexpr int kX3Op = kTM * kX3Ld;             // halves per operand part (hi or lo)
+constexpr float kX3Scale = 256.0f;             // per-operand scale (exact power of two)
+constexpr float kX3Unscale = 1.0f / 65536.0f;  // 1 / scale^2
 
 constexpr int x3_lds_bytes() { return 4 * kX3Op * (int)sizeof(_Float16); }
 
@@ -37,30 +40,49 @@ __device__ inline void x3_split(float x, _Float16& hi, _Float16& lo) {
   lo = (_Float16)(s - (float)hi);
 }
 
-// Register prefetch of one 128 x 32 fp32 chunk.  KCONT: OpChunk<true>'s mapping (4 float4 along k
-// per row).  !KCONT (ptr[k * ld + row]): thread t loads the 4 x 4 block rows 4(t&31) .. +3 x
-// k 4(t>>5) .. +3 (four coalesced float4 row loads), so after a register transpose each row's 4
-// k-values are contiguous and go to LDS as one 8-byte store per part.
+// Register prefetch of one 128 x kX3BK fp32 chunk (NV = kX3BK / 8 float4 per thread).
+//  KCONT (ptr[row * ld + k]): thread t holds rows (t >> 3) + 32 i (i < NV/2... see below), k-quads.
+//  !KCONT (ptr[k * ld + row]): thread t loads 4 x 4 blocks rows 4(t&31)..+3 x k 4((t>>5) + 8 q)..+3
+//  (coalesced float4 row loads); after a register transpose each row's 4 k are contiguous.
 template <bool KCONT>
-struct X3Chunk;
-template <>
-struct X3Chunk<true> : OpChunk<true> {};
-template <>
-struct X3Chunk<false> {
-  f32x4 v[4];  // v[kk] = rows 4 (t&31) .. +3 at k = k0 + 4 (t>>5) + kk
+struct X3Chunk {
+  static constexpr int NV = kX3BK / 8;
+  f32x4 v[NV];
   __device__ inline void load(const float* __restrict__ base, int64_t ld, int k0) {
-    const int t = threadIdx.x, c4 = t & 31, kq = t >> 5;
+    const int t = threadIdx.x;
+    if constexpr (KCONT) {
+      // kX3BK/4 float4 per row; 256 threads cover 256 * 4 / kX3BK rows per pass
+      constexpr int QPR = kX3BK / 4, RPP = 256 / QPR;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) v[kk] = *reinterpret_cast<const f32x4*>(base + (int64_t)(k0 + 4 * kq + kk) * ld + c4 * 4);
+      for (int i = 0; i < NV; ++i) {
+        const int row = t / QPR + RPP * i, q = t % QPR;
+        v[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)row * ld + k0 + q * 4);
+      }
+    } else {
+      const int c4 = t & 31, kq = t >> 5;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int kb = 4 * (kq + 8 * (i >> 2)) + (i & 3);
+        v[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)(k0 + kb) * ld + c4 * 4);
+      }
+    }
   }
   __device__ inline void scale_k(const float* __restrict__ s, int k0) {
-    const int kq = threadIdx.x >> 5;
+    const int t = threadIdx.x;
+    if constexpr (KCONT) {
+      constexpr int QPR = kX3BK / 4;
+      const f32x4 sv = *reinterpret_cast<const f32x4*>(s + k0 + (t % QPR) * 4);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) v[kk] *= s[k0 + 4 * kq + kk];
+      for (int i = 0; i < NV; ++i) v[i] *= sv;
+    } else {
+      const int kq = t >> 5;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) v[i] *= s[k0 + 4 * (kq + 8 * (i >> 2)) + (i & 3)];
+    }
   }
   __device__ inline void negate() {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) v[kk] = -v[kk];
+    for (int i = 0; i < NV; ++i) v[i] = -v[i];
   }
 };
 
@@ -69,9 +91,10 @@ template <bool KCONT>
 __device__ inline void x3_store(const X3Chunk<KCONT>& c, _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
   const int t = threadIdx.x;
   if constexpr (KCONT) {
+    constexpr int QPR = kX3BK / 4, RPP = 256 / QPR;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (t >> 3) + 32 * i, k = (t & 7) * 4;
+    for (int i = 0; i < X3Chunk<true>::NV; ++i) {
+      const int row = t / QPR + RPP * i, k = (t % QPR) * 4;
       x3_half4 h, l;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -84,19 +107,23 @@ __device__ inline void x3_store(const X3Chunk<KCONT>& c, _Float16* __restrict__ 
       *reinterpret_cast<x3_half4*>(lo + row * kX3Ld + k) = l;
     }
   } else {
-    const int row0 = (t & 31) * 4, k = (t >> 5) * 4;
+    const int row0 = (t & 31) * 4, kq = t >> 5;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      x3_half4 h, l;
+    for (int g = 0; g < X3Chunk<false>::NV / 4; ++g) {
+      const int k = 4 * (kq + 8 * g);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        _Float16 a, b;
-        x3_split(c.v[kk][e], a, b);
-        h[kk] = a;
-        l[kk] = b;
+      for (int e = 0; e < 4; ++e) {
+        x3_half4 h, l;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          _Float16 a, b;
+          x3_split(c.v[4 * g + kk][e], a, b);
+          h[kk] = a;
+          l[kk] = b;
+        }
+        *reinterpret_cast<x3_half4*>(hi + (row0 + e) * kX3Ld + k) = h;
+        *reinterpret_cast<x3_half4*>(lo + (row0 + e) * kX3Ld + k) = l;
       }
-      *reinterpret_cast<x3_half4*>(hi + (row0 + e) * kX3Ld + k) = h;
-      *reinterpret_cast<x3_half4*>(lo + (row0 + e) * kX3Ld + k) = l;
     }
   }
 }
@@ -107,7 +134,7 @@ __device__ inline void x3_mma_chunk(const _Float16* __restrict__ ah, const _Floa
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
   const int r = lane & 31, kh = (lane >> 5) * 8;
 #pragma unroll
-  for (int kk = 0; kk < kBK; kk += 16) {
+  for (int kk = 0; kk < kX3BK; kk += 16) {
     x3_half8 aH[2], aL[2], bH[2], bL[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -137,8 +164,8 @@ __device__ inline void frag_scale(Frag& f, float s) {
       for (int r = 0; r < 16; ++r) f.acc[a][b][r] *= s;
 }
 
-// acc (+/-)= op(A)[128 x K] op(B)[K x 128] over k in [kbeg, kend) (multiples of 32), fp32-accurate
-// on the f16 matrix cores.  lds: x3_lds_bytes() bytes, 16-B aligned.
+// acc (+/-)= op(A)[128 x K] op(B)[K x 128] over k in [kbeg, kend) (multiples of kX3BK),
+// fp32-accurate on the f16 matrix cores.  lds: x3_lds_bytes() bytes, 16-B aligned.
 template <bool AK, bool BKc, bool NEG = false>
 __device__ inline void tile_gemm_x3(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                                     int kbeg, int kend, Frag& f, _Float16* __restrict__ lds,
@@ -153,16 +180,16 @@ __device__ inline void tile_gemm_x3(const float* __restrict__ A, int64_t lda, co
   X3Chunk<BKc> cb;
   ca.load(A, lda, kbeg);
   cb.load(B, ldb, kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+  for (int k0 = kbeg; k0 < kend; k0 += kX3BK) {
     if (ascale) ca.scale_k(ascale, k0);
     if constexpr (NEG) ca.negate();
     __syncthreads();  // previous chunk fully consumed
     x3_store<AK>(ca, ah, al);
     x3_store<BKc>(cb, bh, bl);
     __syncthreads();
-    if (k0 + kBK < kend) {
-      ca.load(A, lda, k0 + kBK);
-      cb.load(B, ldb, k0 + kBK);
+    if (k0 + kX3BK < kend) {
+      ca.load(A, lda, k0 + kX3BK);
+      cb.load(B, ldb, k0 + kX3BK);
     }
     x3_mma_chunk(ah, al, bh, bl, f);
   }

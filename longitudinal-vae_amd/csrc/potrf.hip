@@ -27,8 +27,8 @@ constexpr int kNB = 128;
 // GEMM engine per kernel: fp32-input MFMA (exact fp32 products) or the 3-product f16 split
 // (mfma_x3.hpp, ~2^-22 per product, 3/16 of the cost).  Bit i of the mask selects X3 for
 // kernel class i (GemmClass); LVAE_X3 in the environment overrides the default.
-enum GemmClass { GC_PANEL = 0, GC_UPDATE = 1, GC_TRTRI = 2, GC_Z = 3, GC_LAUUM = 4, GC_SYRK = 5 };
-constexpr int kX3DefaultMask = 0x3f;  // all classes: KL/grad parity within 1e-4 (tests), 1.36x step
+enum GemmClass { GC_PANEL = 0, GC_UPDATE = 1, GC_TRTRI = 2, GC_Z = 3, GC_LAUUM = 4, GC_SYRK = 5, GC_REC = 6 };
+constexpr int kX3DefaultMask = 0x7f;  // all classes: KL/grad parity within 1e-4 (tests), 1.36x step
 inline int x3_mask() {
   static const int m = [] {
     const char* e = getenv("LVAE_X3");
@@ -179,6 +179,111 @@ __global__ __launch_bounds__(256) void syrk_scaled_kernel(const float* __restric
 }
 
 // ------------------------------------------------------------------------------------------
+// Recursive Schur-complement inverse (the Regime B path): for K = [[A, B^T], [B, C]],
+//   A^-1 (recursion), X = B A^-1, S = C - X B^T, S^-1 (recursion), Y = S^-1 X,
+//   K^-1 = [[A^-1 + X^T Y, -Y^T], [-Y, S^-1]],   log|K| = log|A| + log|S|.
+// Same n^3 flops as Cholesky + inverse, but the GEMMs of the top levels have K = n/2, n/4, ...
+// (compute-bound) where the right-looking block LDL^T spends its time in rank-128 updates
+// (memory-bound, one launch per block column).  Leaves are the 128x128 in-register inverse.
+// ------------------------------------------------------------------------------------------
+struct RecGemm {
+  const float* A;
+  int64_t lda, sA;
+  const float* B;
+  int64_t ldb, sB;
+  float* C;
+  int64_t ldc, sC;
+  float* Ct;  // mirror base (nullable): element (r, c) of tile (I, J) also to Ct[(J*128 + c) * ldc + I*128 + r]
+  int K, tm, tn;
+};
+
+template <bool X3, bool AK, bool BKc, bool NEG, bool LOWER, bool CIN>
+__global__ __launch_bounds__(256) void rec_gemm_kernel(RecGemm g) {
+  __shared__ __attribute__((aligned(16))) char lds[gemm_lds_bytes<AK, BKc>()];
+  int I, J;
+  if constexpr (LOWER) {
+    tri_index2(blockIdx.x, I, J);
+  } else {
+    I = blockIdx.x / g.tn;
+    J = blockIdx.x % g.tn;
+  }
+  const int64_t l = blockIdx.y;
+  const float* A = g.A + l * g.sA + (AK ? (int64_t)I * kNB * g.lda : (int64_t)I * kNB);
+  const float* B = g.B + l * g.sB + (BKc ? (int64_t)J * kNB * g.ldb : (int64_t)J * kNB);
+  float* C = g.C + l * g.sC + (int64_t)I * kNB * g.ldc + J * kNB;
+  Frag f;
+  if constexpr (CIN) frag_load(f, C, g.ldc);
+  else f.zero();
+  tile_gemm_any<X3, AK, BKc, NEG>(A, g.lda, B, g.ldb, 0, g.K, f, lds);
+  float* Ct = g.Ct ? g.Ct + l * g.sC + (int64_t)J * kNB * g.ldc + I * kNB : nullptr;
+  const bool mir = Ct != nullptr && !(LOWER && I == J);
+  const int64_t ldc = g.ldc;
+  frag_foreach(f, [&](int r, int c, float v) {
+    C[(int64_t)r * ldc + c] = v;
+    if (mir) Ct[(int64_t)c * ldc + r] = v;
+  });
+}
+
+__global__ __launch_bounds__(1024) void rec_leaf_kernel(const float* __restrict__ Kall, float* __restrict__ Kinv,
+                                                        int np_, int off, double* __restrict__ logdet,
+                                                        int32_t* __restrict__ info) {
+  const int l = blockIdx.x;
+  const int64_t o = (int64_t)l * np_ * np_ + (int64_t)off * np_ + off;
+  blk_inverse<float, 8, 4>(kNB, Kall + o, np_, Kinv + o, np_, logdet + l, 1, info + l, off);
+}
+
+template <bool AK, bool BKc, bool NEG, bool LOWER, bool CIN>
+static void rec_launch(const RecGemm& g, int L, hipStream_t st) {
+  const int nt = LOWER ? g.tm * (g.tm + 1) / 2 : g.tm * g.tn;
+  if (nt <= 0 || g.K <= 0) return;
+  if (use_x3(GC_REC))
+    rec_gemm_kernel<true, AK, BKc, NEG, LOWER, CIN><<<dim3(nt, L), 256, 0, st>>>(g);
+  else
+    rec_gemm_kernel<false, AK, BKc, NEG, LOWER, CIN><<<dim3(nt, L), 256, 0, st>>>(g);
+}
+
+// Kinv[off:off+n, off:off+n] <- K[off:off+n, off:off+n]^-1 (K: lower 128-tiles valid; the C block's
+// lower tiles are overwritten by the Schur complement); W: scratch of K's shape.
+static void rec_inv(float* K, float* Kinv, float* W, int np_, int L, int off, int n, double* logdet, int32_t* info,
+                    hipStream_t st) {
+  if (n == kNB) {
+    rec_leaf_kernel<<<L, 1024, 0, st>>>(K, Kinv, np_, off, logdet, info);
+    return;
+  }
+  const int64_t np2 = (int64_t)np_ * np_;
+  const int t = n / kNB, h1 = (t / 2) * kNB, h2 = n - h1, o2 = off + h1;
+  auto at = [&](float* base, int r, int c) { return base + (int64_t)r * np_ + c; };
+  rec_inv(K, Kinv, W, np_, L, off, h1, logdet, info, st);  // A^-1
+  // X = B A^-1   [h2 x h1] -> W
+  rec_launch<true, false, false, false, false>(
+      RecGemm{at(K, o2, off), np_, np2, at(Kinv, off, off), np_, np2, at(W, o2, off), np_, np2, nullptr, h1, h2 / kNB,
+              h1 / kNB}, L, st);
+  // S = C - X B^T   (lower tiles, in place)
+  rec_launch<true, true, true, true, true>(
+      RecGemm{at(W, o2, off), np_, np2, at(K, o2, off), np_, np2, at(K, o2, o2), np_, np2, nullptr, h1, h2 / kNB,
+              h2 / kNB}, L, st);
+  rec_inv(K, Kinv, W, np_, L, o2, h2, logdet, info, st);  // S^-1
+  // -Y = -S^-1 X  -> Kinv lower-left, mirrored to upper-right
+  rec_launch<true, false, true, false, false>(
+      RecGemm{at(Kinv, o2, o2), np_, np2, at(W, o2, off), np_, np2, at(Kinv, o2, off), np_, np2, at(Kinv, off, o2), h2,
+              h2 / kNB, h1 / kNB}, L, st);
+  // A^-1 += X^T Y = A^-1 - X^T (-Y)   (lower tiles, mirrored)
+  rec_launch<false, false, true, true, true>(
+      RecGemm{at(W, o2, off), np_, np2, at(Kinv, o2, off), np_, np2, at(Kinv, off, off), np_, np2, at(Kinv, off, off),
+              h2, h1 / kNB, h1 / kNB}, L, st);
+}
+
+int spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info, hipStream_t st) {
+  if (np_ <= 0 || np_ % kNB) return -1;
+  if (L <= 0) return -2;
+  (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
+  (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
+  rec_inv(A, Ainv, W, np_, L, 0, np_, logdet, info, st);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
 // host sequencing
 // ------------------------------------------------------------------------------------------
 int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, hipStream_t st) {
@@ -220,6 +325,10 @@ int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hi
 
 extern "C" {
 int lvae_gemm_engine_mask(void) { return lvae::x3_mask(); }
+int lvae_spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info,
+                         void* stream) {
+  return lvae::spd_inverse_f32(np_, L, A, W, Ainv, logdet, info, (hipStream_t)stream);
+}
 int lvae_potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, void* stream) {
   return lvae::potrf_f32(np_, L, A, W, logdet, info, (hipStream_t)stream);
 }

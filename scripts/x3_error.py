@@ -24,8 +24,8 @@ def rel(a, b):
 
 
 def main():
-    for P in (64, 128):
-        T, L = 16, 2
+    for P in [int(a) for a in (sys.argv[1:] or ["64", "128"])]:
+        T, L = 16, 1 if P >= 256 else 2
         X = torch.tensor(health_mnist_covariates(P, T, seed=P))
         gen = torch.Generator().manual_seed(P)
         mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
