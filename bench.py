@@ -34,18 +34,24 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA peak
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense f16/bf16 MFMA peak (~2.5 PF, no sparsity)
 X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product (mfma_x3.hpp)
 # Memory-side bytes per syrk launch from the committed rocprofv3 PMC passes (scripts/pmc.sh ->
-# profiles/r1_v5_pmc_summary.json: FETCH_SIZE / WRITE_SIZE in KiB per dispatch; FETCH_SIZE x 2 for
+# profiles/r1_v6_pmc_summary.json: FETCH_SIZE / WRITE_SIZE in KiB per dispatch; FETCH_SIZE x 2 for
 # 16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM").  Counts L2 misses incl.
 # Infinity-Cache hits, so it bounds HBM traffic from above.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_v5_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_v6_pmc_summary.json")
 
 
-def pmc_traffic(kernel_prefix):
+def pmc_traffic(kernels):
+    """Sum over the named kernels (one dispatch each per step) of FETCH_SIZE x 2 + WRITE_SIZE, bytes."""
     try:
         d = json.load(open(PMC_SUMMARY))
-        f = [v["mean"] for k, v in d["FETCH_SIZE"].items() if kernel_prefix in k]
-        w = [v["mean"] for k, v in d["WRITE_SIZE"].items() if kernel_prefix in k]
-        return (2 * f[0] + w[0]) * 1024 if f and w else None
+        tot = 0.0
+        for name in kernels:
+            f = [v["mean"] for k, v in d["FETCH_SIZE"].items() if name in k]
+            w = [v["mean"] for k, v in d["WRITE_SIZE"].items() if name in k]
+            if not (f and w):
+                return None
+            tot += (2 * f[0] + w[0]) * 1024
+        return tot
     except (OSError, KeyError, ValueError):
         return None
 HBM_PEAK_GBS = 8000.0
@@ -56,15 +62,24 @@ def log(*a):
 
 
 def setup_dist(ngpu):
+    """One process per GPU (torchrun env).  Returns (world, rank, device index).  RCCL ("nccl") by
+    default; LVAE_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on fewer GPUs
+    (device = LOCAL_RANK mod the visible GPU count)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(torch.cuda.device_count(), 1)
+    dev = local % ndev
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("LVAE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    return world, rank, local
+    return world, rank, dev
 
 
 def cpu_baseline(P, T, L, dims_timed=1):
@@ -199,12 +214,15 @@ def main():
             # dense peak / 3 (each algorithmic fp32 FMA costs three f16 MFMA FMAs).
             flops = L * np_ * np_ * (np_ + 1)
             achieved = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
-            x3 = bool((_lib.load().lvae_gemm_engine_mask() >> 5) & 1)
+            fast_syrk = np_ % 256 == 0 and not int(os.environ.get("LVAE_SYRK_GENERIC", "0"))
+            x3 = fast_syrk or bool((_lib.load().lvae_gemm_engine_mask() >> 5) & 1)
             peak = F16_MFMA_PEAK_TFLOPS / X3_PRODUCTS if x3 else FP32_MFMA_PEAK_TFLOPS
-            res["roofline"] = {"kernel": "syrk_scaled_kernel (K^-1 V K^-1)", "bound": "mfma",
+            res["roofline"] = {"kernel": "syrk_split_kernel + syrk_x3_kernel (S = K^-1 V K^-1)" if fast_syrk
+                               else "syrk_scaled_kernel (S = K^-1 V K^-1)", "bound": "mfma",
                                "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                                "frac": (achieved / peak) if achieved else None,
-                               "traffic": pmc_traffic("syrk_scaled_kernel<true>" if x3 else "syrk_scaled_kernel<false>"), "padded_n": int(np_),
+                               "traffic": pmc_traffic(("syrk_x3_kernel", "syrk_split_kernel") if fast_syrk else
+                                                      ("syrk_scaled_kernel<true>" if x3 else "syrk_scaled_kernel<false>",)), "padded_n": int(np_),
                                "engine": ("f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)" if x3
                                           else "fp32-input MFMA")}
         if not args.no_cpu_baseline:

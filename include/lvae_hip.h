@@ -201,6 +201,14 @@ int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* gr
                             const double* grad_H, double lr, const double* iH, int32_t* info,
                             void* workspace, void* stream);
 
+/* ConvVAE encoder (VAE.py:44-50): y = max_pool2d(relu(x), 2, 2) over planes = N*C planes of H x W
+ * (H, W even) fp32, idx = argmax byte (0..3, row-major in the window, first strict maximum);
+ * backward gx = the pooled gradient routed to the argmax where y > 0, 0 elsewhere.            */
+int lvae_relu_maxpool2_fwd_f32(const float* x, int64_t planes, int H, int W, float* y, uint8_t* idx,
+                               void* stream);
+int lvae_relu_maxpool2_bwd_f32(const float* gy, const float* y, const uint8_t* idx, int64_t planes, int H,
+                               int W, float* gx, void* stream);
+
 /* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
  * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject
  * (seg_len [P] valid rows each; padding rows of x are any finite covariates, of mu must be 0),

@@ -27,6 +27,7 @@ int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info,
 int potri_f32(int np_, int L, float* A, float* W, float* Ainv, hipStream_t st);
 int spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info, hipStream_t st);
 int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st);
+int syrk_x3_f32(int np_, int L, const float* Kinv, const float* v, _Float16* planes, float* S, hipStream_t st);
 
 struct KLWorkspace {
   float *A, *W, *Kinv, *v;
@@ -185,10 +186,16 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
-  // S = K^-1 V K^-1 into the (no longer needed) factor buffer
+  // S = K^-1 V K^-1 into the (no longer needed) Gram buffer; the fp16 hi / lo planes of the
+  // split operand go to the (no longer needed) factor buffer W (2 x 2 B per element = its size).
+  // np a multiple of 256: the pre-split 256-tile kernel (syrk_x3.hip); else the generic tile GEMM.
   {
+    static const bool generic = getenv("LVAE_SYRK_GENERIC") && atoi(getenv("LVAE_SYRK_GENERIC"));
     ProfScope ps(LVAE_PH_SYRK, st);
-    LVAE_TRY(syrk_scaled_f32(np_, L, ws.Kinv, ws.v, ws.A, st));
+    if (!generic && np_ % 256 == 0)
+      LVAE_TRY(syrk_x3_f32(np_, L, ws.Kinv, ws.v, (_Float16*)ws.W, ws.A, st));
+    else
+      LVAE_TRY(syrk_scaled_f32(np_, L, ws.Kinv, ws.v, ws.A, st));
   }
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);

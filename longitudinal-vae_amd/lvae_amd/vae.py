@@ -11,6 +11,45 @@ import torch.nn.functional as F
 from torch import nn
 
 
+class _ReluMaxPool2(torch.autograd.Function):
+    """max_pool2d(relu(x), 2, 2) in one HIP pass (lvae_relu_maxpool2_fwd/bwd_f32, vae_ops.hip):
+    one byte of argmax per output instead of torch's int64 indices, one write per input in the
+    backward.  Same values and gradient routing as relu + max_pool2d (first strict maximum)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from . import _lib
+        lib = _lib.lib()
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty(N, C, H // 2, W // 2, dtype=x.dtype, device=x.device)
+        idx = torch.empty(N, C, H // 2, W // 2, dtype=torch.uint8, device=x.device)
+        _lib.check(lib.lvae_relu_maxpool2_fwd_f32(_lib.ptr(x), N * C, H, W, _lib.ptr(y), _lib.ptr(idx),
+                                                   _lib.stream_ptr()), "relu_maxpool2_fwd")
+        ctx.save_for_backward(y, idx)
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import _lib
+        lib = _lib.lib()
+        y, idx = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        gy = gy.contiguous()
+        gx = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
+        _lib.check(lib.lvae_relu_maxpool2_bwd_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), N * C, H, W, _lib.ptr(gx),
+                                                   _lib.stream_ptr()), "relu_maxpool2_bwd")
+        return gx
+
+
+def relu_maxpool2(x):
+    """pool(relu(x)) of the encoder (VAE.py:44-50): fused HIP kernel for CUDA fp32 activations."""
+    if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0:
+        return _ReluMaxPool2.apply(x)
+    return F.max_pool2d(F.relu(x), kernel_size=2, stride=2)
+
+
 class ConvVAE(nn.Module):
     def __init__(self, latent_dim, num_dim=1296, vy_init=1.0, vy_fixed=False, p_input=0.2, p=0.5):
         super().__init__()
@@ -52,8 +91,8 @@ class ConvVAE(nn.Module):
         return torch.exp(self.min_log_vy + F.softplus(self._log_vy - self.min_log_vy))
 
     def encode(self, x):
-        z = self.dropout2d_1(self.pool1(F.relu(self.conv1(x))))
-        z = self.dropout2d_2(self.pool2(F.relu(self.conv2(z))))
+        z = self.dropout2d_1(relu_maxpool2(self.conv1(x)))   # pool1(relu(conv1))
+        z = self.dropout2d_2(relu_maxpool2(self.conv2(z)))   # pool2(relu(conv2))
         h1 = self.dropout1(F.relu(self.fc1(z.reshape(-1, 32 * 9 * 9))))
         h2 = self.dropout2(F.relu(self.fc21(h1)))
         return self.fc211(h2), self.fc221(h2)

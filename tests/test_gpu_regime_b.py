@@ -229,3 +229,22 @@ def test_kl_closed_vs_oracle_full_size(hip):
     assert rel(mu_d.grad[:, 0], m_.grad) < 1e-4
     assert rel(lv_d.grad[:, 0], v_.grad) < 1e-4
     assert rel(torch.stack([p.grad[0] for _, p in kd.named_parameters()]), r.grad) < 1e-4
+
+
+def test_relu_maxpool2_matches_torch(hip):
+    """Fused encoder relu + 2x2 max pool vs torch (values bit-exact, gradient routing identical)."""
+    from lvae_amd.vae import relu_maxpool2
+    import torch.nn.functional as F
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(7, 16, 36, 36, device=DEV, generator=gen)
+    x[0, 0, :4, :4] = -1.0       # all-negative windows
+    x[1, 1, 2:4, 2:4] = 0.5      # ties: the first maximum in scan order takes the gradient
+    xa = x.clone().requires_grad_()
+    xb = x.clone().requires_grad_()
+    ya = relu_maxpool2(xa)
+    yb = F.max_pool2d(F.relu(xb), 2, 2)
+    assert torch.equal(ya, yb)
+    g = torch.randn(ya.shape, device=DEV, generator=gen)
+    ya.backward(g)
+    yb.backward(g)
+    assert torch.equal(xa.grad, xb.grad)
