@@ -126,6 +126,18 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
 int lvae_spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info,
                          void* stream);
 
+/* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
+ * 256-wide pivot blocks -- the default Regime B inverse of lvae_kl_closed_fwd_f32: per pivot block k,
+ * A_kk <- -P^-1, A_ik <- A_ik P^-1, A_ij <- A_ij - A_ik P^-1 A_kj (P = A_kk); after the last block
+ * A = -K^-1.  np % 256 == 0.  A [L, np, np] (lower 256-block tiles read, overwritten);
+ * scratch: lvae_spd_sweep_scratch_size(np, L) bytes, 256-B aligned; Ainv [L, np, np] full
+ * symmetric out; logdet [L]; info [L] LAPACK-style (first bad column + 1).  The pivot inverses run
+ * on a second (internal) stream joined back to `stream`.
+ * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
+size_t lvae_spd_sweep_scratch_size(int np_, int L);
+int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
+                       void* stream);
+
 /* Blocked factorisation of L padded SPD matrices (in place, fp32 MFMA): right-looking block LDL^T
  * with 128-wide pivot blocks, K = Lt Dt Lt^T (the Cholesky factor is Lt chol(Dt)).  On return W's
  * diagonal tiles hold D_k^-1, its strictly-lower tiles Lt; logdet[l] = log|A_l|, info[l] LAPACK-style.

@@ -14,6 +14,7 @@
 #include "prof.hpp"
 
 #include <cstdlib>
+#include <string>
 
 namespace lvae {
 
@@ -28,9 +29,13 @@ int potri_f32(int np_, int L, float* A, float* W, float* Ainv, hipStream_t st);
 int spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info, hipStream_t st);
 int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st);
 int syrk_x3_f32(int np_, int L, const float* Kinv, const float* v, _Float16* planes, float* S, hipStream_t st);
+int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
+                  hipStream_t st);
+size_t spd_sweep_scratch_bytes(int np_, int L);
 
 struct KLWorkspace {
   float *A, *W, *Kinv, *v;
+  char* sweep;
   double *mu, *alpha, *kdiag, *logdet, *part;
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
@@ -49,6 +54,7 @@ struct KLWorkspace {
     alpha = (double*)take((size_t)L * np_ * sizeof(double));
     kdiag = (double*)take((size_t)L * np_ * sizeof(double));
     logdet = (double*)take((size_t)L * sizeof(double));
+    sweep = take(spd_sweep_scratch_bytes(np_, L));
     part = (double*)take(kl_gram_bwd_partials_bytes(np_, L));
     bytes = off;
   }
@@ -123,7 +129,7 @@ using namespace lvae;
 
 extern "C" {
 
-int lvae_kl_closed_padded_n(int n) { return ((n + 127) / 128) * 128; }
+int lvae_kl_closed_padded_n(int n) { return ((n + 255) / 256) * 256; }
 
 size_t lvae_kl_closed_workspace_size(int n, int L) {
   const int np_ = lvae_kl_closed_padded_n(n);
@@ -151,12 +157,21 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
     kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v);
   }
   {
-    // K^-1 and log|K|: block LDL^T (128-wide pivots) + inverse.  The recursive Schur-complement
-    // inverse (LVAE_KL_REC=1) is ~1.2 ms/step faster at C3 but multiplies by explicit inverses of
-    // blocks up to N/2 wide: at N = 4096 its dmu / dlogv errors reach 9e-5 of the 1e-4 budget
-    // (LDL^T: 2e-5), so it is not the default.
-    static const bool rec = getenv("LVAE_KL_REC") && atoi(getenv("LVAE_KL_REC"));
-    if (rec) {
+    // K^-1 and log|K|.  Default: the block symmetric sweep (spd_sweep.hip: 16 rank-256 passes at
+    // np = 4096, pivot inverses overlapped on a second stream).  LVAE_KL_INV=ldl: block LDL^T
+    // (128-wide pivots) + triangular inverse + product; LVAE_KL_INV=rec: recursive Schur
+    // complements (multiplies by explicit inverses of blocks up to N/2 wide: at N = 4096 its
+    // dmu / dlogv errors reach 9e-5 of the 1e-4 budget).
+    static const int inv = [] {
+      const char* e = getenv("LVAE_KL_INV");
+      if (!e) return 0;
+      const std::string s(e);
+      return s == "ldl" ? 1 : (s == "rec" ? 2 : 0);
+    }();
+    if (inv == 0) {
+      ProfScope ps(LVAE_PH_POTRF, st);
+      LVAE_TRY(spd_sweep_f32(np_, L, ws.A, ws.sweep, ws.Kinv, ws.logdet, info, st));
+    } else if (inv == 2) {
       ProfScope ps(LVAE_PH_POTRF, st);
       LVAE_TRY(spd_inverse_f32(np_, L, ws.A, ws.W, ws.Kinv, ws.logdet, info, st));
     } else {

@@ -1,0 +1,488 @@
+// spd_sweep.hip -- K^-1 and log|K| of L batched SPD np x np fp32 covariances by a block symmetric
+// sweep (Gauss-Jordan on SPD), the Regime B inverse of the exact KL (replaces torch.cholesky +
+// cholesky_solve(I) + the log-det, elbo_functions.py:26-29).
+//
+// Sweep on pivot block k (256 wide), P = A_kk the current Schur complement of the unswept part:
+//   A_kk <- -P^-1,   A_ik <- W_i = A_ik P^-1 (i != k),   A_ij <- A_ij - W_i A_kj (i, j != k)
+// After every block is swept, A = -K^-1; log|K| = sum_k log|P_k|.  The same n^3 flops as
+// Cholesky + trtri + lauum, but in nt = np / 256 uniform passes: every pass is ONE rank-256 update
+// of the whole lower triangle (K = 256: twice the reuse of a 128-wide blocked factorisation's
+// updates), so factor, triangular inverse and product collapse into one HBM-streaming kernel per pass.
+//
+// Per pass k (all L latent dims in every launch):
+//   prep(k)   (one launch, three workgroup roles)
+//             W_i = A_ik P^-1 for i != k (x3 tile GEMM) -> fp32 Wbuf[k & 1][i] ([rows of i][cols of k])
+//                 and the fp16 planes of -256 W_i;
+//             C_j = A_jk for j != k (the unswept column, transposed from row k where j < k) -> the
+//                 fp16 planes of 256 C_j;
+//             the previous pass's swept column Wbuf[(k-1) & 1] copied into its in-place tiles
+//   U1(k)     A_{k+1,k+1} += (-W_{k+1}) C_{k+1}^T               (one 256-tile per dim)
+//   pivot(k+1) on a second stream, overlapped with U2(k): -P^-1 by an in-register Gauss-Jordan
+//             sweep of the 256 x 256 block (one 1024-thread workgroup per dim), log|P|, info
+//   U2(k)     A_ij += (-W_i) C_j^T for every other lower 256-tile (x3_dma.hpp: pre-split planes,
+//             DMA-staged); the last pass writes -A to Kinv (both triangles)
+//   finish    the last swept column and pivot block to Kinv
+//
+// Scratch (spd_sweep_scratch_bytes): Wbuf 2 x [L, np, 256] fp32, planes Wh Wl Ch Cl [L, np, 256]
+// fp16, Pinv [L, 256, 256] fp32.  A [L, np, np]: lower 256-block tiles read, overwritten.
+// Kinv [L, np, np]: out, full symmetric.  np % 256 == 0.
+#include "mfma_x3.hpp"
+#include "x3_dma.hpp"
+
+#include <climits>
+
+namespace lvae {
+
+constexpr int kSwB = 256;  // pivot block
+constexpr int kSwT = 128;  // output tile of tile_gemm_x3 (prep)
+constexpr int kSwBB = kSwB * kSwB;
+
+struct SwScratch {
+  float* W[2];                  // [L][np][256]
+  _Float16 *Wh, *Wl, *Ch, *Cl;  // [L][np][256]
+  float* Pinv;                  // [L][256][256]
+  size_t bytes;
+  SwScratch(char* base, int np_, int L) {
+    size_t off = 0;
+    auto take = [&](size_t b) {
+      char* p = base ? base + off : nullptr;
+      off += align256(b);
+      return p;
+    };
+    const size_t col = (size_t)L * np_ * kSwB;
+    W[0] = (float*)take(col * 4);
+    W[1] = (float*)take(col * 4);
+    Wh = (_Float16*)take(col * 2);
+    Wl = (_Float16*)take(col * 2);
+    Ch = (_Float16*)take(col * 2);
+    Cl = (_Float16*)take(col * 2);
+    Pinv = (float*)take((size_t)L * kSwBB * 4);
+    bytes = off;
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// pivot: T = A_kk (lower triangle read, symmetrised) -> T = -P^-1 (full), Pinv = P^-1.
+// 1024 threads; thread (tr, tc) = (tid >> 5, tid & 31) holds rows 8 tr + r (r < 8) of columns
+// tc + 32 b (b < 8) in a[b][r] (row pairs adjacent: v_pk_fma_f32 with the column value
+// broadcast).  The block is first scaled to unit diagonal (P' = S P S, s_i = P_ii^-1/2), so every
+// sweep pivot d lies in (0, 1] and the whole step is ONE rank-1 update
+//   a_ij -= u_i v_j,  u = c (u_p = d - 1),  v = c / d (v_p = 1 - 1/d),  c = column p,
+// which leaves row / column p at c / d and a_pp at 2 - 1/d (the constant 2 is removed from the
+// diagonal at the end; no later pivot reads a_pp).  With d <= 1 none of these cancels.  Column p + 1
+// is published in a double-buffered LDS vector by its 32 owner threads: one barrier per pivot.
+// ------------------------------------------------------------------------------------------
+template <int B0>
+__device__ __attribute__((always_inline)) inline void sw_pivot_cols(float (&a)[8][8], float (*colbuf)[kSwB],
+                                                                    float* dpiv, int tid, int tr, int tc) {
+  for (int q = 0; q < 32; ++q) {
+    const int p = 32 * B0 + q;
+    const float* cb = colbuf[p & 1];
+    const float d = cb[p];
+    if (tid == 0) dpiv[p] = d;
+    const float id = __builtin_amdgcn_rcpf(d);
+    float u[8];
+    {
+      const float4 u0 = *reinterpret_cast<const float4*>(cb + 8 * tr);
+      const float4 u1 = *reinterpret_cast<const float4*>(cb + 8 * tr + 4);
+      u[0] = u0.x, u[1] = u0.y, u[2] = u0.z, u[3] = u0.w;
+      u[4] = u1.x, u[5] = u1.y, u[6] = u1.z, u[7] = u1.w;
+    }
+    const int rp = p - 8 * tr;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) u[r] = (r == rp) ? d - 1.0f : u[r];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      float v = cb[tc + 32 * b] * id;
+      if (b == B0) v = (tc == q) ? 1.0f - id : v;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) a[b][r] = fmaf(-u[r], v, a[b][r]);
+    }
+    // publish column p + 1 (owner: tc == (p + 1) & 31, register column (p + 1) >> 5)
+    float* nb = colbuf[(p + 1) & 1] + 8 * tr;
+    if (q < 31) {
+      if (tc == q + 1) {
+        *reinterpret_cast<float4*>(nb) = make_float4(a[B0][0], a[B0][1], a[B0][2], a[B0][3]);
+        *reinterpret_cast<float4*>(nb + 4) = make_float4(a[B0][4], a[B0][5], a[B0][6], a[B0][7]);
+      }
+    } else if constexpr (B0 < 7) {
+      if (tc == 0) {
+        *reinterpret_cast<float4*>(nb) = make_float4(a[B0 + 1][0], a[B0 + 1][1], a[B0 + 1][2], a[B0 + 1][3]);
+        *reinterpret_cast<float4*>(nb + 4) = make_float4(a[B0 + 1][4], a[B0 + 1][5], a[B0 + 1][6], a[B0 + 1][7]);
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (B0 < 7) sw_pivot_cols<B0 + 1>(a, colbuf, dpiv, tid, tr, tc);
+}
+
+__global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall, int np_, int kb,
+                                                        float* __restrict__ Pinv, double* __restrict__ logdet,
+                                                        int32_t* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) float colbuf[2][kSwB];
+  __shared__ float dg[kSwB];
+  __shared__ float dpiv[kSwB];
+  __shared__ double red[16];
+  __shared__ int bad_s;
+  const int l = blockIdx.x, tid = threadIdx.x, tr = tid >> 5, tc = tid & 31;
+  float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
+  float a[8][8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int row = 8 * tr + r, col = tc + 32 * b;
+      const int hi = row >= col ? row : col, lo = row >= col ? col : row;
+      a[b][r] = T[hi * np_ + lo];
+      if (row == col) dg[row] = a[b][r];
+    }
+  if (tid == 0) bad_s = INT_MAX;
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[b][r] *= rsqrtf(dg[8 * tr + r]) * rsqrtf(dg[tc + 32 * b]);
+  if (tc == 0) {
+    *reinterpret_cast<float4*>(&colbuf[0][8 * tr]) = make_float4(a[0][0], a[0][1], a[0][2], a[0][3]);
+    *reinterpret_cast<float4*>(&colbuf[0][8 * tr + 4]) = make_float4(a[0][4], a[0][5], a[0][6], a[0][7]);
+  }
+  __syncthreads();
+
+  sw_pivot_cols<0>(a, colbuf, dpiv, tid, tr, tc);
+
+  // a = -(S P S)^-1 + 2 I  ->  -P^-1 = S a' S
+  float* Pl = Pinv + (int64_t)l * kSwBB;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int row = 8 * tr + r, col = tc + 32 * b;
+      const float x = (a[b][r] - (row == col ? 2.0f : 0.0f)) * rsqrtf(dg[row]) * rsqrtf(dg[col]);
+      T[row * np_ + col] = x;
+      Pl[row * kSwB + col] = -x;
+    }
+  // log|P| = sum log d_p - 2 sum log s_i; first bad pivot
+  double lv = 0.0;
+  if (tid < kSwB) {
+    const float d = dpiv[tid];
+    if (!(d > 0.0f) || !isfinite(d)) atomicMin(&bad_s, tid);
+    lv = log((double)d) - 2.0 * log((double)rsqrtf(dg[tid]));
+  }
+  lv = block_sum<1024>(lv, red);
+  if (tid == 0) {
+    logdet[l] += lv;
+    if (bad_s != INT_MAX && info[l] == 0) info[l] = kb * kSwB + bad_s + 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// 128 x 128 block visitor: fn(r, c, f32x4 v) for dst element (r, c..c+3) = src[r][c..] (direct)
+// or src[c..][r] (transposed, through a 64 x 129 LDS stage per half).  256 threads; lanes of a
+// 16-group cover 64 consecutive dst columns of one dst row (coalesced reads and writes).
+// ------------------------------------------------------------------------------------------
+template <typename Fn>
+__device__ inline void blk128_visit(const float* __restrict__ src, int64_t ld, bool trans, float* __restrict__ lds,
+                                    Fn fn) {
+  const int t = threadIdx.x, c4 = t & 15, r0 = t >> 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (trans) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // src rows 64 h + (t >> 5) + 8 i, float4 at column 4 (t & 31)
+        const int sr = (t >> 5) + 8 * i, sc = 4 * (t & 31);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src + (int64_t)(64 * h + sr) * ld + sc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) lds[sr * 129 + sc + e] = v[e];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = r0 + 16 * i, c = 64 * h + 4 * c4;
+      f32x4 v;
+      if (trans) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = lds[(4 * c4 + e) * 129 + r];
+      } else {
+        v = *reinterpret_cast<const f32x4*>(src + (int64_t)r * ld + c);
+      }
+      fn(r, c, v);
+    }
+  }
+}
+
+__device__ inline void sw_split4(f32x4 v, float s, _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
+  x3_half4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float y = v[e] * s;
+    const _Float16 hh = (_Float16)y;
+    h[e] = hh;
+    l[e] = (_Float16)(y - (float)hh);
+  }
+  *reinterpret_cast<x3_half4*>(hi) = h;
+  *reinterpret_cast<x3_half4*>(lo) = l;
+}
+
+constexpr int cmaxi(int a, int b) { return a > b ? a : b; }
+
+// ------------------------------------------------------------------------------------------
+// prep(k): grid.x = 3 * 4 nt (role = blockIdx.x / 4 nt), grid.y = L; (block i, sub-tile sm, sn)
+//   role 0: W_i (i != k) = A_ik P^-1  (x3 tile GEMM; A_ik = tile (i, k) or tile (k, i)^T)
+//   role 1: C planes of block i (i != k) = split(256 A_ik)
+//   role 2: (k >= 1) copy of the previous pass's W_i into its in-place tile (i != k-1)
+// Tile (k, k-1) is still being copied in this launch: its readers take it from Wprev[k] instead.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, SwScratch S, int np_, int nt, int k) {
+  __shared__ __attribute__((aligned(16))) char lds[cmaxi(x3_lds_bytes(), 64 * 129 * 4)];
+  const int l = blockIdx.y, role = blockIdx.x / (4 * nt), w = blockIdx.x % (4 * nt);
+  const int i = w >> 2, sm = (w >> 1) & 1, sn = w & 1;
+  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
+  float* A = Aall + l * np2;
+  float* Wc = S.W[k & 1] + l * col;
+  const float* Wp = S.W[(k + 1) & 1] + l * col;
+  const int64_t sub = (int64_t)i * kSwBB + sm * kSwT * kSwB + sn * kSwT;  // sub-tile (sm, sn) of block row i
+  if (role == 0) {
+    if (i == k) return;
+    const float* P = S.Pinv + (int64_t)l * kSwBB;
+    Frag f;
+    f.zero();
+    if (i > k) {
+      tile_gemm_x3<true, true>(A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB, np_, P + sn * kSwT * kSwB, kSwB,
+                               0, kSwB, f, (_Float16*)lds);
+    } else {
+      // A_ik(m, t) = tile (k, i)[t][m]; tile (k, k-1) is Wprev[k] ([rows of k][cols of k-1])
+      const float* src = (i == k - 1) ? Wp + (int64_t)k * kSwBB : A + (int64_t)k * kSwB * np_ + i * kSwB;
+      const int64_t ls = (i == k - 1) ? kSwB : np_;
+      tile_gemm_x3<false, true>(src + sm * kSwT, ls, P + sn * kSwT * kSwB, kSwB, 0, kSwB, f, (_Float16*)lds);
+    }
+    float* C = Wc + sub;
+    _Float16* h = S.Wh + l * col + sub;
+    _Float16* lo = S.Wl + l * col + sub;
+    frag_foreach(f, [&](int r, int c, float v) {
+      C[r * kSwB + c] = v;
+      const float y = -v * kSxScale;
+      const _Float16 hh = (_Float16)y;
+      h[r * kSwB + c] = hh;
+      lo[r * kSwB + c] = (_Float16)(y - (float)hh);
+    });
+  } else if (role == 1) {
+    if (i == k) return;
+    // C_i(m, t) = A_ik: tile (i, k) for i > k; tile (k, i)^T for i < k (Wprev[k]^T for i = k-1)
+    const float* src;
+    int64_t ls;
+    if (i > k) {
+      src = A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB + sn * kSwT;
+      ls = np_;
+    } else if (i == k - 1) {
+      src = Wp + (int64_t)k * kSwBB + sn * kSwT * kSwB + sm * kSwT;
+      ls = kSwB;
+    } else {
+      src = A + ((int64_t)k * kSwB + sn * kSwT) * np_ + i * kSwB + sm * kSwT;
+      ls = np_;
+    }
+    _Float16* h = S.Ch + l * col + sub;
+    _Float16* lo = S.Cl + l * col + sub;
+    blk128_visit(src, ls, i < k, (float*)lds,
+                 [&](int r, int c, f32x4 v) { sw_split4(v, kSxScale, h + r * kSwB + c, lo + r * kSwB + c); });
+  } else {
+    const int c = k - 1;
+    if (k == 0 || i == c) return;
+    // tile (i, c) = W_i for i > c; tile (c, i) = W_i^T for i < c
+    float* dst;
+    const float* src;
+    if (i > c) {
+      dst = A + ((int64_t)i * kSwB + sm * kSwT) * np_ + c * kSwB + sn * kSwT;
+      src = Wp + sub;
+    } else {
+      dst = A + ((int64_t)c * kSwB + sm * kSwT) * np_ + i * kSwB + sn * kSwT;
+      src = Wp + (int64_t)i * kSwBB + sn * kSwT * kSwB + sm * kSwT;
+    }
+    blk128_visit(src, kSwB, i < c, (float*)lds,
+                 [&](int r, int cc, f32x4 v) { *reinterpret_cast<f32x4*>(dst + (int64_t)r * np_ + cc) = v; });
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// update(k): A_IJ += (-W_I) C_J^T on lower 256-tiles (I >= J, I, J != k), K = 256, pre-split
+// planes (x3_dma.hpp).  Tiles enumerate the lower triangle of the (nt-1)^2 block grid without row
+// and column k; workgroups are remapped so each XCD takes a contiguous tile range of one dim.
+//   only11: the single tile (k+1, k+1) (U1); else that tile is skipped (U2)
+//   LAST:   -result to Kinv (I, J) and its mirror instead of in place
+// ------------------------------------------------------------------------------------------
+template <bool LAST>
+__global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S, float* __restrict__ Kinv,
+                                                        int np_, int nt, int k, int only11, int ntl, int nwg) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int l = wgid / ntl;
+  int I, J;
+  if (only11) {
+    I = J = k + 1;
+  } else {
+    sx_tri(wgid % ntl, I, J);
+    I += I >= k;
+    J += J >= k;
+    if (!LAST && I == k + 1 && J == k + 1) return;
+  }
+  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
+  float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
+  // C tile through a buffer resource: one lane VGPR offset + uniform per-element row offsets (no
+  // 64-bit address per element for the compiler to keep alive across the GEMM)
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+  sx_f32x16 acc[4][2];
+  // acc = 65536 C (the planes carry 256 x each operand)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][b][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0)) *
+                       (kSxScale * kSxScale);
+  const int64_t oa = l * col + (int64_t)I * kSwBB, ob = l * col + (int64_t)J * kSwBB;
+  sx_gemm(S.Wh + oa, S.Wl + oa, S.Ch + ob, S.Cl + ob, kSwB, kSwB, lds, acc);
+  if constexpr (!LAST) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[a][b][e] * kSxUnscale), rc, vo,
+                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+  } else {
+    // -result to Kinv (I, J) and, transposed, to (J, I); diagonal tiles: lower elements only
+    float* O = Kinv + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
+    float* Ot = Kinv + l * np2 + (int64_t)J * kSwB * np_ + I * kSwB;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(O, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(Ot, (short)0, 0x7fffffff, 0x00020000);
+    const bool diag = I == J;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int c = sx_col(b);
+      const int vt = (c * np_ + (w >> 2) * 128 + 4 * (lane >> 5)) * 4;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = sx_row(a, e);
+          const uint32_t v = __builtin_bit_cast(uint32_t, -acc[a][b][e] * kSxUnscale);
+          if (!diag || r >= c) {
+            __builtin_amdgcn_raw_buffer_store_b32(v, ro, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(v, rt, vt, (32 * a + (e & 3) + 8 * (e >> 2)) * 4, 0);
+          }
+        }
+    }
+  }
+}
+
+// last pass: -(swept column nt-1) and -(last pivot block) to Kinv.  grid.x = 4 (2 (nt-1) + 1):
+// block w >> 2 < nt-1: Kinv (i, nt-1) = -W_i; < 2 (nt-1): Kinv (nt-1, i) = -W_i^T; else the pivot.
+__global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict__ Aall, SwScratch S,
+                                                        float* __restrict__ Kinv, int np_, int nt) {
+  __shared__ float lds[64 * 129];
+  const int l = blockIdx.y, w = blockIdx.x, blk = w >> 2, sm = (w >> 1) & 1, sn = w & 1, c = nt - 1;
+  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
+  const float* Wc = S.W[c & 1] + l * col;
+  const float* src;
+  int64_t ls, r0, c0;
+  bool tr = false;
+  if (blk < c) {
+    src = Wc + (int64_t)blk * kSwBB + sm * kSwT * kSwB + sn * kSwT;
+    ls = kSwB;
+    r0 = blk * kSwB + sm * kSwT;
+    c0 = c * kSwB + sn * kSwT;
+  } else if (blk < 2 * c) {
+    const int i = blk - c;
+    src = Wc + (int64_t)i * kSwBB + sn * kSwT * kSwB + sm * kSwT;
+    ls = kSwB;
+    tr = true;
+    r0 = c * kSwB + sm * kSwT;
+    c0 = i * kSwB + sn * kSwT;
+  } else {
+    src = Aall + l * np2 + (int64_t)(c * kSwB + sm * kSwT) * np_ + c * kSwB + sn * kSwT;
+    ls = np_;
+    r0 = c * kSwB + sm * kSwT;
+    c0 = c * kSwB + sn * kSwT;
+  }
+  float* dst = Kinv + l * np2 + r0 * np_ + c0;
+  blk128_visit(src, ls, tr, lds,
+               [&](int r, int cc, f32x4 v) { *reinterpret_cast<f32x4*>(dst + (int64_t)r * np_ + cc) = -v; });
+}
+
+// ------------------------------------------------------------------------------------------
+// host sequencing
+// ------------------------------------------------------------------------------------------
+struct SwSide {
+  hipStream_t s = nullptr;
+  hipEvent_t e1 = nullptr, e2 = nullptr;
+};
+
+// the pivot's second stream and its fork / join events, created once per device
+static int sw_side(SwSide*& out) {
+  static SwSide side[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return LVAE_ERR_LAUNCH;
+  SwSide& sd = side[dev];
+  if (!sd.s) {
+    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&sd.e1, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&sd.e2, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
+  }
+  out = &sd;
+  return 0;
+}
+
+size_t spd_sweep_scratch_bytes(int np_, int L) { return SwScratch(nullptr, np_, L).bytes; }
+
+int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
+                  hipStream_t st) {
+  if (np_ <= 0 || np_ % kSwB) return -1;
+  if (L <= 0) return -2;
+  SwSide* sd = nullptr;
+  LVAE_TRY(sw_side(sd));
+  SwScratch S((char*)scratch, np_, L);
+  (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
+  (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
+  const int nt = np_ / kSwB, ntl = (nt - 1) * nt / 2, nwg = ntl * L;
+  sw_pivot_kernel<<<L, 1024, 0, st>>>(A, np_, 0, S.Pinv, logdet, info);
+  for (int k = 0; k < nt; ++k) {
+    const bool last = k + 1 == nt;
+    if (nt > 1) sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, st>>>(A, S, np_, nt, k);
+    if (!last) {
+      sw_update_kernel<false><<<L, 512, 0, st>>>(A, S, Kinv, np_, nt, k, 1, 1, L);
+      if (hipEventRecord(sd->e1, st) != hipSuccess) return LVAE_ERR_LAUNCH;
+      if (hipStreamWaitEvent(sd->s, sd->e1, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
+      sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S.Pinv, logdet, info);
+      if (hipEventRecord(sd->e2, sd->s) != hipSuccess) return LVAE_ERR_LAUNCH;
+      if (ntl > 1) sw_update_kernel<false><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, nt, k, 0, ntl, nwg);
+      if (hipStreamWaitEvent(st, sd->e2, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
+    } else {
+      if (ntl > 0) sw_update_kernel<true><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, nt, k, 0, ntl, nwg);
+      sw_finish_kernel<<<dim3(4 * (2 * (nt - 1) + 1), L), 256, 0, st>>>(A, S, Kinv, np_, nt);
+    }
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace lvae
+
+extern "C" {
+size_t lvae_spd_sweep_scratch_size(int np_, int L) { return lvae::spd_sweep_scratch_bytes(np_, L); }
+int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
+                       void* stream) {
+  if (!A) return -3;
+  if (!scratch || ((uintptr_t)scratch & 255)) return -4;
+  if (!Kinv) return -5;
+  if (!logdet) return -6;
+  if (!info) return -7;
+  return lvae::spd_sweep_f32(np_, L, A, scratch, Kinv, logdet, info, (hipStream_t)stream);
+}
+}

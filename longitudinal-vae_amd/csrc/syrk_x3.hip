@@ -17,22 +17,10 @@
 //
 // Blocks are remapped so that each XCD (blockIdx % 8) works through a contiguous range of tiles
 // of one latent dim: neighbouring tiles share 256-row panels in that XCD's L2.
-#include "common.hpp"
+#include "x3_dma.hpp"
 
 namespace lvae {
 
-typedef _Float16 sx_half8 __attribute__((ext_vector_type(8)));
-typedef _Float16 sx_half4 __attribute__((ext_vector_type(4)));
-typedef float sx_f32x16 __attribute__((ext_vector_type(16)));
-typedef float sx_f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kSxT = 256;                // output tile edge
-constexpr int kSxBK = 32;                // K chunk (halves) per LDS stage
-constexpr int kSxPart = kSxT * kSxBK;    // halves per operand part per stage (16 KB)
-constexpr float kSxScale = 256.0f;
-constexpr float kSxUnscale = 1.0f / 65536.0f;
-
-// hi / lo planes of B = 256 K^-1 diag(sqrt v): 4 elements per thread
 __global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict__ Kinv, const float* __restrict__ v,
                                                          _Float16* __restrict__ Bh, _Float16* __restrict__ Bl,
                                                          int np_, int64_t n4) {
@@ -55,40 +43,6 @@ __global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict
   *reinterpret_cast<sx_half4*>(Bh + i0) = h;
   *reinterpret_cast<sx_half4*>(Bl + i0) = lo;
 }
-
-__device__ inline void sx_tri(int t, int& I, int& J) {
-  int r = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-  while ((r + 1) * (r + 2) / 2 <= t) ++r;
-  while (r * (r + 1) / 2 > t) --r;
-  I = r;
-  J = t - r * (r + 1) / 2;
-}
-
-// one stage: 4 parts (A hi, A lo, B hi, B lo) x 16 wave-instructions of 1 KB; wave w issues
-// instructions 2w, 2w+1 of every part -> 8 global_load_lds per thread.
-__device__ inline void sx_issue(const _Float16* __restrict__ ah, const _Float16* __restrict__ al,
-                                const _Float16* __restrict__ bh, const _Float16* __restrict__ bl, int64_t ld, int k0,
-                                _Float16* __restrict__ stage) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const _Float16* src[4] = {ah, al, bh, bl};
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int blk = 2 * w + q;                      // 16-row block of the 256-row part
-    const int row = 16 * blk + (lane >> 2);
-    const int c = (lane & 3) ^ ((row >> 2) & 3);    // logical chunk stored at physical chunk lane&3
-    const int64_t go = (int64_t)row * ld + k0 + 8 * c;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-      __builtin_amdgcn_global_load_lds((const void*)(src[p] + go), (void*)(stage + p * kSxPart + blk * 512), 16, 0,
-                                       0);
-  }
-}
-
-__device__ inline sx_half8 sx_frag(const _Float16* __restrict__ part, int row, int c) {
-  return *reinterpret_cast<const sx_half8*>(part + row * kSxBK + ((c ^ ((row >> 2) & 3)) << 3));
-}
-
-#define SX_WAIT_VM(N) __builtin_amdgcn_s_waitcnt(0xF70 | (N))  // vmcnt(N), expcnt / lgkmcnt untouched
 
 __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
                                                       float* __restrict__ S, int np_, int ntl, int nwg) {
@@ -116,45 +70,7 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-
-  const int nk = np_ / kSxBK;
-  sx_issue(ah, al, bh, bl, ld, 0, lds);
-  for (int s = 0; s < nk; ++s) {
-    // one barrier per K-chunk: it retires stage s (every wave waited for its own DMA of it) and
-    // every wave's reads of stage s-1, whose buffer then receives stage s+1 while s is multiplied
-    SX_WAIT_VM(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 1 < nk) sx_issue(ah, al, bh, bl, ld, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
-    const _Float16* cur = lds + (s & 1) * 4 * kSxPart;
-    const _Float16* pah = cur;
-    const _Float16* pal = cur + kSxPart;
-    const _Float16* pbh = cur + 2 * kSxPart;
-    const _Float16* pbl = cur + 3 * kSxPart;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < kSxBK / 16; ++ks) {
-      const int c = 2 * ks + kh;
-      sx_half8 bH[2], bL[2];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        bH[b] = sx_frag(pbh, wn + 32 * b + r32, c);
-        bL[b] = sx_frag(pbl, wn + 32 * b + r32, c);
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const sx_half8 aH = sx_frag(pah, wm + 32 * a + r32, c);
-        const sx_half8 aL = sx_frag(pal, wm + 32 * a + r32, c);
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH[b], acc[a][b], 0, 0, 0);
-        }
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
+  sx_gemm(ah, al, bh, bl, ld, np_, lds, acc);
   // epilogue: C layout of 32x32 blocks -- row (e&3) + 8(e>>2) + 4(lane>>5), col lane&31
   float* C = S + base + (int64_t)(I * kSxT + wm) * ld + J * kSxT + wn;
 #pragma unroll

@@ -103,6 +103,8 @@ SIGNATURES = {
     "lvae_relu_maxpool2_fwd_f32": (_I32, [_VP, _I64, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _I32, _I32, _VP, _VP]),
     "lvae_spd_inverse_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
+    "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),
     "lvae_predict_f64": (_I32, [_SPEC, _SPEC, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP, _VP,
                                 _VP, _VP, _D, _VP, _VP, _VP, _VP]),

@@ -204,6 +204,56 @@ def test_spd_inverse_recursive(hip, n):
     assert rel(logdet.cpu(), torch.logdet(A)) < 1e-6
 
 
+@pytest.mark.parametrize("n,L", [(256, 3), (512, 2), (768, 2), (1280, 2), (4096, 1)])
+def test_spd_sweep(hip, n, L):
+    """Block symmetric sweep (the default Regime B inverse) vs fp64 torch: A^-1 (both triangles
+    written) and log|A|.  nt = n / 256 = 1, 2, 3, 5, 16 pivot blocks; the upper triangle of A is
+    garbage (never read) and A's scale is uneven (diagonal 0.5 .. 50) as the unit-diagonal pivot
+    scaling must handle."""
+    import lvae_amd as la
+    gen = torch.Generator().manual_seed(n + L)
+    Xm = torch.randn(L, n, n, generator=gen, dtype=torch.float64) / n ** 0.5
+    A = Xm @ Xm.transpose(1, 2) + torch.eye(n, dtype=torch.float64)
+    s = torch.exp(torch.rand(L, n, 1, generator=gen, dtype=torch.float64) * 4.6 - 0.7) ** 0.5
+    A = s * A * s.transpose(1, 2)
+    Ad = (torch.tril(A) + 7.0 * torch.triu(torch.ones(n, n, dtype=torch.float64), 1)).float().to(DEV).contiguous()
+    scr = torch.full((hip.lvae_spd_sweep_scratch_size(n, L) // 4,), float("nan"), device=DEV)
+    Ai = torch.full_like(Ad, float("nan"))
+    logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
+    info = torch.zeros(L, dtype=torch.int32, device=DEV)
+    P = la._lib
+    P.check(hip.lvae_spd_sweep_f32(n, L, P.ptr(Ad), P.ptr(scr), P.ptr(Ai), P.ptr(logdet), P.ptr(info),
+                                   P.stream_ptr()), "spd_sweep")
+    torch.cuda.synchronize()
+    assert int(info.abs().sum()) == 0
+    ref = torch.linalg.inv(A)
+    got = Ai.cpu().double()
+    assert torch.isfinite(got).all()
+    err = rel(got, ref)
+    print(f"spd_sweep n={n} L={L}: rel err {err:.3e}")
+    assert err < 1e-4
+    assert rel(logdet.cpu(), torch.logdet(A)) < 1e-6
+
+
+def test_spd_sweep_not_pd(hip):
+    """A non-SPD pivot is reported LAPACK-style with the global column (block 1, local column 10)."""
+    import lvae_amd as la
+    n, L = 512, 2
+    A = torch.eye(n, dtype=torch.float64).repeat(L, 1, 1)
+    A[1, 256 + 10, 256 + 10] = -1.0
+    Ad = A.float().to(DEV).contiguous()
+    scr = torch.zeros(hip.lvae_spd_sweep_scratch_size(n, L) // 4, device=DEV)
+    Ai = torch.zeros_like(Ad)
+    logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
+    info = torch.zeros(L, dtype=torch.int32, device=DEV)
+    P = la._lib
+    P.check(hip.lvae_spd_sweep_f32(n, L, P.ptr(Ad), P.ptr(scr), P.ptr(Ai), P.ptr(logdet), P.ptr(info),
+                                   P.stream_ptr()), "spd_sweep")
+    torch.cuda.synchronize()
+    assert info.cpu().tolist() == [0, 256 + 10 + 1]
+    assert abs(float(logdet[0])) < 1e-6
+
+
 def test_kl_closed_vs_oracle_full_size(hip):
     """The headline size N = 4096 (P = 256 subjects x T = 16), one latent dim, vs the fp64 oracle
     (north-star tolerance 1e-4 on the KL and every gradient)."""
