@@ -16,11 +16,11 @@
 //             C_j = A_jk for j != k (the unswept column, transposed from row k where j < k) -> the
 //                 fp16 planes of 256 C_j;
 //             the previous pass's swept column Wbuf[(k-1) & 1] copied into its in-place tiles
-//   U1(k)     A_{k+1,k+1} += (-W_{k+1}) C_{k+1}^T               (one 256-tile per dim)
-//   pivot(k+1) on a second stream, overlapped with U2(k): -P^-1 by an in-register Gauss-Jordan
-//             sweep of the 256 x 256 block (one 1024-thread workgroup per dim), log|P|, info
-//   U2(k)     A_ij += (-W_i) C_j^T for every other lower 256-tile (x3_dma.hpp: pre-split planes,
-//             DMA-staged); the last pass writes -A to Kinv (both triangles)
+//   U1(k)     on a second, highest-priority stream: A_{k+1,k+1} += (-W_{k+1}) C_{k+1}^T, then
+//   pivot(k+1)  -P^-1 by an in-register Gauss-Jordan sweep of the 256 x 256 block (one 1024-thread
+//             workgroup per dim), log|P|, info -- overlapped with
+//   U2(k)     A_ij += (-W_i) C_j^T for every other lower 256-tile (pre-split planes, DMA-staged, C
+//             streamed non-temporally under the MFMAs); the last pass writes -A to Kinv (both triangles)
 //   finish    the last swept column and pivot block to Kinv
 //
 // Scratch (spd_sweep_scratch_bytes): Wbuf 2 x [L, np, 256] fp32, planes Wh Wl Ch Cl [L, np, 256]
@@ -304,16 +304,44 @@ __global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, 
   }
 }
 
+// tile t of the lower triangle of an m x m tile grid in blocked order: row blocks of 4, inside a
+// block by column, then row.  64 half-tile workgroups in flight on one XCD then touch ~4 W and ~8 C
+// panels (3 MB, inside its 4 MB L2) instead of a few rows x every C panel (row-major order).
+__device__ inline void u_tile(int t, int m, int& I, int& J) {
+  int r, c;
+  sx_tri(t, r, c);  // row r of t in row-major order: t lies in row block r / 4 either way
+  const int base = (r >> 2) << 2, h = min(4, m - base);
+  int u = t - base * (base + 1) / 2;
+  if (u < h * base) {
+    J = u / h;
+    I = base + u % h;
+  } else {
+    u -= h * base;
+    int jj = 0;
+    while (u >= h - jj) {
+      u -= h - jj;
+      ++jj;
+    }
+    J = base + jj;
+    I = J + u;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
-// update(k): A_IJ += (-W_I) C_J^T on lower 256-tiles (I >= J, I, J != k), K = 256, pre-split
-// planes (x3_dma.hpp).  Tiles enumerate the lower triangle of the (nt-1)^2 block grid without row
-// and column k; workgroups are remapped so each XCD takes a contiguous tile range of one dim.
-//   only11: the single tile (k+1, k+1) (U1); else that tile is skipped (U2)
+// update(k): A_IJ += (-W_I) C_J^T on lower 256-tiles (I >= J, I, J != k), K = 256: one 512-thread
+// workgroup per 256 x 256 tile on the pre-split fp16 planes (x3_dma.hpp layout and DMA staging,
+// double-buffered K chunks of 32).  C enters in 8 chunks of 16 accumulator elements INSIDE the K
+// loop (chunk j loaded in step j, added in step j + 1), read and written non-temporally (CAUX = slc:
+// the C stream does not evict the planes from L2).  Measured at np = 4096, L = 16: C streaming alone
+// ~200 us, the GEMM alone ~200 us, together 293 us per launch (a 256 x 128 half-tile form with two
+// workgroups per CU moved 1.5x the plane bytes and took 350-410 us).
+//   only11: the single tile (k+1, k+1) (U1, feeding the next pivot); else that tile is skipped (U2)
 //   LAST:   -result to Kinv (I, J) and its mirror instead of in place
 // ------------------------------------------------------------------------------------------
-template <bool LAST>
-__global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S, float* __restrict__ Kinv,
-                                                        int np_, int nt, int k, int only11, int ntl, int nwg) {
+template <bool LAST, int CAUX = LAST ? 0 : 2>
+__global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S,
+                                                           float* __restrict__ Kinv, int np_, int k, int only11,
+                                                           int ntl, int nwg) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
@@ -322,31 +350,59 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   if (only11) {
     I = J = k + 1;
   } else {
-    sx_tri(wgid % ntl, I, J);
+    u_tile(wgid % ntl, np_ / kSwB - 1, I, J);
     I += I >= k;
     J += J >= k;
     if (!LAST && I == k + 1 && J == k + 1) return;
   }
   const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
   float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
-  // C tile through a buffer resource: one lane VGPR offset + uniform per-element row offsets (no
-  // 64-bit address per element for the compiler to keep alive across the GEMM)
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+  const int64_t oa = l * col + (int64_t)I * kSwBB, ob = l * col + (int64_t)J * kSwBB;
+  const _Float16* ah = S.Wh + oa;
+  const _Float16* al = S.Wl + oa;
+  const _Float16* bh = S.Ch + ob;
+  const _Float16* bl = S.Cl + ob;
   sx_f32x16 acc[4][2];
-  // acc = 65536 C (the planes carry 256 x each operand)
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int e = 0; e < 16; ++e)
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  // chunk j = accumulator elements 16 j .. 16 j + 15 (a = i >> 5, e = (i >> 1) & 15, b = i & 1)
+  float cv[16];
+  constexpr int nk = kSwB / kSxBK;
+  static_assert(nk * 16 == 128, "one C chunk per K step");
+  sx_issue(ah, al, bh, bl, kSwB, 0, lds);
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-        acc[a][b][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0)) *
-                       (kSxScale * kSxScale);
-  const int64_t oa = l * col + (int64_t)I * kSwBB, ob = l * col + (int64_t)J * kSwBB;
-  sx_gemm(S.Wh + oa, S.Wl + oa, S.Ch + ob, S.Cl + ob, kSwB, kSwB, lds, acc);
+  for (int s = 0; s < nk; ++s) {
+    SX_WAIT_VM(0);  // chunk s staged, C chunk s - 1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nk) sx_issue(ah, al, bh, bl, kSwB, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
+    if (s >= 1) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 16 * (s - 1) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+        acc[a][b][e] += cv[q] * (kSxScale * kSxScale);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = 16 * s + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      cv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX));
+    }
+    __builtin_amdgcn_s_setprio(1);
+    sx_mma_stage(lds + (s & 1) * 4 * kSxPart, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = 16 * (nk - 1) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+    acc[a][b][e] += cv[q] * (kSxScale * kSxScale);
+  }
   if constexpr (!LAST) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -354,30 +410,56 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
       for (int e = 0; e < 16; ++e)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[a][b][e] * kSxUnscale), rc, vo,
-                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * kSxUnscale), rc, vo,
+                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
   } else {
-    // -result to Kinv (I, J) and, transposed, to (J, I); diagonal tiles: lower elements only
+    // -result to Kinv (I, J) (diagonal tiles: lower elements only) and, transposed through LDS, to
+    // (J, I): per 128-row half of the tile, U[c][r ^ 4 (c & 31)] = value (r, c), read back as float4
+    // runs of 4 rows of one column -> coalesced 512-B rows of (J, I)
     float* O = Kinv + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
     float* Ot = Kinv + l * np2 + (int64_t)J * kSwB * np_ + I * kSwB;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(O, (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(Ot, (short)0, 0x7fffffff, 0x00020000);
     const bool diag = I == J;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int c = sx_col(b);
-      const int vt = (c * np_ + (w >> 2) * 128 + 4 * (lane >> 5)) * 4;
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int e = 0; e < 16; ++e)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int r = sx_row(a, e);
-          const uint32_t v = __builtin_bit_cast(uint32_t, -acc[a][b][e] * kSxUnscale);
-          if (!diag || r >= c) {
-            __builtin_amdgcn_raw_buffer_store_b32(v, ro, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(v, rt, vt, (32 * a + (e & 3) + 8 * (e >> 2)) * 4, 0);
-          }
+        for (int b = 0; b < 2; ++b)
+          if (!diag || sx_row(a, e) >= sx_col(b))
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(-acc[a][b][e] * kSxUnscale), ro, vo,
+                                                  ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+    float* U = reinterpret_cast<float*>(lds);  // 128 x 256 fp32 = the 128 KB of the K stages
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      __syncthreads();  // (hh = 0: every wave's last LDS reads of the GEMM; hh = 1: the half-0 readers)
+      if ((w >> 2) == hh) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              const int rl = sx_row(a, e) - 128 * hh, c = sx_col(b);
+              U[c * 128 + (rl ^ ((c & 31) << 2))] = -acc[a][b][e] * kSxUnscale;
+            }
+      }
+      __syncthreads();
+      const int t4 = tid & 31;
+#pragma unroll 4
+      for (int cc = 0; cc < kSwB; cc += 16) {
+        const int c = cc + (tid >> 5), rl = 4 * t4;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(&U[c * 128 + (rl ^ ((c & 31) << 2))]);
+        float* dst = Ot + (int64_t)c * np_ + 128 * hh + rl;
+        if (!diag) {
+          *reinterpret_cast<f32x4*>(dst) = v;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (128 * hh + rl + q >= c) dst[q] = v[q];
         }
+      }
     }
   }
 }
@@ -419,21 +501,25 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------
 // host sequencing
 // ------------------------------------------------------------------------------------------
+// The pivot's stream (highest priority, so its workgroups are dispatched ahead of U2's as CUs free)
+// and its fork / join events, created once per device.  (Disjoint CU masks for the two streams
+// were measured 2.6 ms per step slower: every masked queue slowed the rest of the step.)
 struct SwSide {
   hipStream_t s = nullptr;
-  hipEvent_t e1 = nullptr, e2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
-// the pivot's second stream and its fork / join events, created once per device
 static int sw_side(SwSide*& out) {
   static SwSide side[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return LVAE_ERR_LAUNCH;
   SwSide& sd = side[dev];
   if (!sd.s) {
-    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess) return LVAE_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&sd.e1, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&sd.e2, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (hipStreamCreateWithPriority(&sd.s, hipStreamNonBlocking, greatest) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
   }
   out = &sd;
   return 0;
@@ -453,18 +539,17 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   const int nt = np_ / kSwB, ntl = (nt - 1) * nt / 2, nwg = ntl * L;
   sw_pivot_kernel<<<L, 1024, 0, st>>>(A, np_, 0, S.Pinv, logdet, info);
   for (int k = 0; k < nt; ++k) {
-    const bool last = k + 1 == nt;
     if (nt > 1) sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, st>>>(A, S, np_, nt, k);
-    if (!last) {
-      sw_update_kernel<false><<<L, 512, 0, st>>>(A, S, Kinv, np_, nt, k, 1, 1, L);
-      if (hipEventRecord(sd->e1, st) != hipSuccess) return LVAE_ERR_LAUNCH;
-      if (hipStreamWaitEvent(sd->s, sd->e1, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (k + 1 < nt) {
+      if (hipEventRecord(sd->fork, st) != hipSuccess) return LVAE_ERR_LAUNCH;
+      if (hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
+      sw_update_kernel<false><<<L, 512, 0, sd->s>>>(A, S, Kinv, np_, k, 1, 1, L);
       sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S.Pinv, logdet, info);
-      if (hipEventRecord(sd->e2, sd->s) != hipSuccess) return LVAE_ERR_LAUNCH;
-      if (ntl > 1) sw_update_kernel<false><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, nt, k, 0, ntl, nwg);
-      if (hipStreamWaitEvent(st, sd->e2, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
+      if (hipEventRecord(sd->join, sd->s) != hipSuccess) return LVAE_ERR_LAUNCH;
+      if (ntl > 1) sw_update_kernel<false><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, 0, ntl, nwg);
+      if (hipStreamWaitEvent(st, sd->join, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
     } else {
-      if (ntl > 0) sw_update_kernel<true><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, nt, k, 0, ntl, nwg);
+      if (ntl > 0) sw_update_kernel<true><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, 0, ntl, nwg);
       sw_finish_kernel<<<dim3(4 * (2 * (nt - 1) + 1), L), 256, 0, st>>>(A, S, Kinv, np_, nt);
     }
   }

@@ -25,7 +25,7 @@ constexpr int kSxPart = kSxT * kSxBK;    // halves per operand part per stage (1
 constexpr float kSxScale = 256.0f;
 constexpr float kSxUnscale = 1.0f / 65536.0f;
 
-// hi / lo planes of B = 256 K^-1 diag(sqrt v): 4 elements per thread
+// linear index t of a lower-triangular tile grid (row-major) -> (I, J), J <= I
 __device__ inline void sx_tri(int t, int& I, int& J) {
   int r = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
   while ((r + 1) * (r + 2) / 2 <= t) ++r;
