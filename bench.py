@@ -37,7 +37,7 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 # profiles/r1_v6_pmc_summary.json: FETCH_SIZE / WRITE_SIZE in KiB per dispatch; FETCH_SIZE x 2 for
 # 16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM").  Counts L2 misses incl.
 # Infinity-Cache hits, so it bounds HBM traffic from above.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_v6_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_v7_pmc_summary.json")
 
 
 def pmc_traffic(kernels):
@@ -208,23 +208,45 @@ def main():
             syrk_ms = phase["syrk"][0] / args.steps
             res["gp_cholesky_gflops"] = L * N ** 3 / 3 / (potrf_ms * 1e-3) / 1e9 if potrf_ms > 0 else None
             res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
-            # dominant kernel: S = K^-1 V K^-1 (syrk_scaled_kernel, one launch per step):
-            # algorithmic flops per launch = L * N^2 (N+1)  (lower triangle incl. diagonal, 2 flop/FMA)
-            # (np = N here).  Engine: fp32-input MFMA -> peak 157.3; 3-product f16 split -> the f16
-            # dense peak / 3 (each algorithmic fp32 FMA costs three f16 MFMA FMAs).
+            # dominant kernel: the sweep's rank-256 update U2 (sw_update_kernel<false, false>, nt - 1
+            # launches per step, 31% of the step's GPU time).  Algorithmic bytes per launch: every
+            # updated lower 256-tile is read and written once in fp32 -> 2 x 4 B x 256^2 per tile,
+            # (nt-1) nt / 2 - 1 tiles per dim (the grid without row / column k and tile (k+1, k+1)),
+            # x L.  The W / C operand planes are L2-resident re-reads, not algorithmic traffic.
+            nt = np_ // 256
+            upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
+            tiles = ((nt - 1) * nt // 2 - 1) * L
+            upd_bytes = 2 * 4 * 256 * 256 * tiles
+            if upd_n and np_ % 256 == 0:
+                avg_s = upd_ms / upd_n * 1e-3
+                ach = upd_bytes / avg_s / 1e9
+                res["roofline"] = {"kernel": "sw_update_kernel<false, false> (sweep rank-256 update U2, spd_sweep.hip)",
+                                   "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": ach / HBM_PEAK_GBS,
+                                   "traffic": pmc_traffic(("sw_update_kernel<false, false",)),
+                                   "algorithmic_bytes_per_launch": upd_bytes, "avg_launch_us": avg_s * 1e6,
+                                   "launches_per_step": upd_n / args.steps, "padded_n": int(np_)}
+            # secondary: S = K^-1 V K^-1, the largest single launch (one per step).  Algorithmic flops
+            # = L * N^2 (N+1) (lower triangle incl. diagonal, 2 flop/FMA).  Engine: 3-product f16
+            # split -> the f16 dense peak / 3 (each fp32 FMA costs three f16 MFMA FMAs).
             flops = L * np_ * np_ * (np_ + 1)
             achieved = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
             fast_syrk = np_ % 256 == 0 and not int(os.environ.get("LVAE_SYRK_GENERIC", "0"))
             x3 = fast_syrk or bool((_lib.load().lvae_gemm_engine_mask() >> 5) & 1)
             peak = F16_MFMA_PEAK_TFLOPS / X3_PRODUCTS if x3 else FP32_MFMA_PEAK_TFLOPS
-            res["roofline"] = {"kernel": "syrk_split_kernel + syrk_x3_kernel (S = K^-1 V K^-1)" if fast_syrk
-                               else "syrk_scaled_kernel (S = K^-1 V K^-1)", "bound": "mfma",
-                               "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                               "frac": (achieved / peak) if achieved else None,
-                               "traffic": pmc_traffic(("syrk_x3_kernel", "syrk_split_kernel") if fast_syrk else
-                                                      ("syrk_scaled_kernel<true>" if x3 else "syrk_scaled_kernel<false>",)), "padded_n": int(np_),
-                               "engine": ("f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)" if x3
-                                          else "fp32-input MFMA")}
+            syrk_line = {"kernel": "syrk_split_kernel + syrk_x3_kernel (S = K^-1 V K^-1)" if fast_syrk
+                         else "syrk_scaled_kernel (S = K^-1 V K^-1)", "bound": "mfma",
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": (achieved / peak) if achieved else None,
+                         "traffic": pmc_traffic(("syrk_x3_kernel", "syrk_split_kernel") if fast_syrk else
+                                                ("syrk_scaled_kernel<true>" if x3 else "syrk_scaled_kernel<false>",)),
+                         "padded_n": int(np_),
+                         "engine": ("f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)" if x3
+                                    else "fp32-input MFMA")}
+            if "roofline" in res:
+                res["roofline_secondary"] = syrk_line
+            else:
+                res["roofline"] = syrk_line
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(P, T, L)
             res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]

@@ -27,6 +27,7 @@
 // fp16, Pinv [L, 256, 256] fp32.  A [L, np, np]: lower 256-block tiles read, overwritten.
 // Kinv [L, np, np]: out, full symmetric.  np % 256 == 0.
 #include "mfma_x3.hpp"
+#include "prof.hpp"
 #include "x3_dma.hpp"
 
 #include <climits>
@@ -335,19 +336,19 @@ __device__ inline void u_tile(int t, int m, int& I, int& J) {
 // the C stream does not evict the planes from L2).  Measured at np = 4096, L = 16: C streaming alone
 // ~200 us, the GEMM alone ~200 us, together 293 us per launch (a 256 x 128 half-tile form with two
 // workgroups per CU moved 1.5x the plane bytes and took 350-410 us).
-//   only11: the single tile (k+1, k+1) (U1, feeding the next pivot); else that tile is skipped (U2)
+//   ONLY11: the single tile (k+1, k+1) (U1, feeding the next pivot); else that tile is skipped (U2)
 //   LAST:   -result to Kinv (I, J) and its mirror instead of in place
 // ------------------------------------------------------------------------------------------
-template <bool LAST, int CAUX = LAST ? 0 : 2>
+template <bool LAST, bool ONLY11 = false, int CAUX = LAST ? 0 : 2>
 __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S,
-                                                           float* __restrict__ Kinv, int np_, int k, int only11,
+                                                           float* __restrict__ Kinv, int np_, int k,
                                                            int ntl, int nwg) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int l = wgid / ntl;
   int I, J;
-  if (only11) {
+  if constexpr (ONLY11) {
     I = J = k + 1;
   } else {
     u_tile(wgid % ntl, np_ / kSwB - 1, I, J);
@@ -543,13 +544,16 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
     if (k + 1 < nt) {
       if (hipEventRecord(sd->fork, st) != hipSuccess) return LVAE_ERR_LAUNCH;
       if (hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
-      sw_update_kernel<false><<<L, 512, 0, sd->s>>>(A, S, Kinv, np_, k, 1, 1, L);
+      sw_update_kernel<false, true><<<L, 512, 0, sd->s>>>(A, S, Kinv, np_, k, 1, L);
       sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S.Pinv, logdet, info);
       if (hipEventRecord(sd->join, sd->s) != hipSuccess) return LVAE_ERR_LAUNCH;
-      if (ntl > 1) sw_update_kernel<false><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, 0, ntl, nwg);
+      if (ntl > 1) {
+        ProfScope ps(LVAE_PH_SWEEP_UPD, st);
+        sw_update_kernel<false><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, ntl, nwg);
+      }
       if (hipStreamWaitEvent(st, sd->join, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
     } else {
-      if (ntl > 0) sw_update_kernel<true><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, 0, ntl, nwg);
+      if (ntl > 0) sw_update_kernel<true><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, ntl, nwg);
       sw_finish_kernel<<<dim3(4 * (2 * (nt - 1) + 1), L), 256, 0, st>>>(A, S, Kinv, np_, nt);
     }
   }

@@ -168,7 +168,7 @@ def xview(t, stride_b, stride_l):
 
 
 PHASES = ["gram", "potrf", "potri", "kl_reduce", "syrk", "gram_bwd", "bwd_elem", "hensman_fwd", "hensman_bwd",
-          "natgrad"]
+          "natgrad", "sweep_update"]
 
 
 def prof_enable(on=True):
