@@ -16,7 +16,7 @@
 //             C_j = A_jk for j != k (the unswept column, transposed from row k where j < k) -> the
 //                 fp16 planes of 256 C_j;
 //             the previous pass's swept column Wbuf[(k-1) & 1] copied into its in-place tiles
-//   U1(k)     on a second, highest-priority stream: A_{k+1,k+1} += (-W_{k+1}) C_{k+1}^T, then
+//   U1(k)     on a second, highest-priority stream: A_{k+1,k+1} -= W_{k+1} C_{k+1}^T, then
 //   pivot(k+1)  -P^-1 by an in-register Gauss-Jordan sweep of the 256 x 256 block (one 1024-thread
 //             workgroup per dim), log|P|, info -- overlapped with
 //   U2(k)     A_ij += (-W_i) C_j^T for every other lower 256-tile (pre-split planes, DMA-staged, C
@@ -305,27 +305,23 @@ __global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, 
   }
 }
 
-// tile t of the lower triangle of an m x m tile grid in blocked order: row blocks of 4, inside a
-// block by column, then row.  64 half-tile workgroups in flight on one XCD then touch ~4 W and ~8 C
-// panels (3 MB, inside its 4 MB L2) instead of a few rows x every C panel (row-major order).
-__device__ inline void u_tile(int t, int m, int& I, int& J) {
-  int r, c;
-  sx_tri(t, r, c);  // row r of t in row-major order: t lies in row block r / 4 either way
-  const int base = (r >> 2) << 2, h = min(4, m - base);
-  int u = t - base * (base + 1) / 2;
-  if (u < h * base) {
-    J = u / h;
-    I = base + u % h;
-  } else {
-    u -= h * base;
-    int jj = 0;
-    while (u >= h - jj) {
-      u -= h - jj;
-      ++jj;
-    }
-    J = base + jj;
-    I = J + u;
-  }
+// ------------------------------------------------------------------------------------------
+// U1(k): A_{k+1,k+1} -= W_{k+1} C_{k+1}^T on its three lower 128-blocks: x3 tile GEMMs on the fp32
+// operands (W from Wbuf, C = the still unswept tile (k+1, k)), 3 L workgroups -- short, so the side
+// stream (U1 + the next pivot) stays within U2's time.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sw_u1_kernel(float* __restrict__ Aall, SwScratch S, int np_, int k) {
+  __shared__ __attribute__((aligned(16))) char lds[x3_lds_bytes()];
+  const int l = blockIdx.y, sm = blockIdx.x == 0 ? 0 : 1, sn = blockIdx.x == 2 ? 1 : 0, kp = k + 1;
+  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
+  float* A = Aall + l * np2;
+  float* T = A + ((int64_t)kp * kSwB + sm * kSwT) * np_ + kp * kSwB + sn * kSwT;
+  const float* Wr = S.W[k & 1] + l * col + (int64_t)kp * kSwBB + sm * kSwT * kSwB;
+  const float* Cr = A + ((int64_t)kp * kSwB + sn * kSwT) * np_ + k * kSwB;
+  Frag f;
+  frag_load(f, T, np_);
+  tile_gemm_x3<true, true, true>(Wr, kSwB, Cr, np_, 0, kSwB, f, (_Float16*)lds);
+  frag_foreach(f, [&](int r, int c, float v) { T[(int64_t)r * np_ + c] = v; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -336,10 +332,10 @@ __device__ inline void u_tile(int t, int m, int& I, int& J) {
 // the C stream does not evict the planes from L2).  Measured at np = 4096, L = 16: C streaming alone
 // ~200 us, the GEMM alone ~200 us, together 293 us per launch (a 256 x 128 half-tile form with two
 // workgroups per CU moved 1.5x the plane bytes and took 350-410 us).
-//   ONLY11: the single tile (k+1, k+1) (U1, feeding the next pivot); else that tile is skipped (U2)
+//   the tile (k+1, k+1) is U1's (sw_u1_kernel), except in the last pass
 //   LAST:   -result to Kinv (I, J) and its mirror instead of in place
 // ------------------------------------------------------------------------------------------
-template <bool LAST, bool ONLY11 = false, int CAUX = LAST ? 0 : 2>
+template <bool LAST, int CAUX = LAST ? 0 : 2>
 __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S,
                                                            float* __restrict__ Kinv, int np_, int k,
                                                            int ntl, int nwg) {
@@ -348,14 +344,10 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int l = wgid / ntl;
   int I, J;
-  if constexpr (ONLY11) {
-    I = J = k + 1;
-  } else {
-    u_tile(wgid % ntl, np_ / kSwB - 1, I, J);
-    I += I >= k;
-    J += J >= k;
-    if (!LAST && I == k + 1 && J == k + 1) return;
-  }
+  sx_tri_blocked(wgid % ntl, np_ / kSwB - 1, I, J);
+  I += I >= k;
+  J += J >= k;
+  if (!LAST && I == k + 1 && J == k + 1) return;  // U1's tile
   const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
   float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
@@ -544,7 +536,7 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
     if (k + 1 < nt) {
       if (hipEventRecord(sd->fork, st) != hipSuccess) return LVAE_ERR_LAUNCH;
       if (hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
-      sw_update_kernel<false, true><<<L, 512, 0, sd->s>>>(A, S, Kinv, np_, k, 1, L);
+      sw_u1_kernel<<<dim3(3, L), 256, 0, sd->s>>>(A, S, np_, k);
       sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S.Pinv, logdet, info);
       if (hipEventRecord(sd->join, sd->s) != hipSuccess) return LVAE_ERR_LAUNCH;
       if (ntl > 1) {

@@ -16,7 +16,8 @@
 // per-lane GLOBAL address of the DMA (its LDS side is lane-linear).
 //
 // Blocks are remapped so that each XCD (blockIdx % 8) works through a contiguous range of tiles
-// of one latent dim: neighbouring tiles share 256-row panels in that XCD's L2.
+// of one latent dim: neighbouring tiles share 256-row panels in that XCD's L2.  (The blocked order
+// of the sweep's update measured 10% slower here: with K = 4096 the panels stream through L2.)
 #include "x3_dma.hpp"
 
 namespace lvae {

@@ -34,6 +34,29 @@ __device__ inline void sx_tri(int t, int& I, int& J) {
   J = t - r * (r + 1) / 2;
 }
 
+// tile t of the lower triangle of an m x m tile grid in blocked order: row blocks of 4, inside a
+// block by column, then row.  64 half-tile workgroups in flight on one XCD then touch ~4 W and ~8 C
+// panels (3 MB, inside its 4 MB L2) instead of a few rows x every C panel (row-major order).
+__device__ inline void sx_tri_blocked(int t, int m, int& I, int& J) {
+  int r, c;
+  sx_tri(t, r, c);  // row r of t in row-major order: t lies in row block r / 4 either way
+  const int base = (r >> 2) << 2, h = min(4, m - base);
+  int u = t - base * (base + 1) / 2;
+  if (u < h * base) {
+    J = u / h;
+    I = base + u % h;
+  } else {
+    u -= h * base;
+    int jj = 0;
+    while (u >= h - jj) {
+      u -= h - jj;
+      ++jj;
+    }
+    J = base + jj;
+    I = J + u;
+  }
+}
+
 // one stage: 4 parts (A hi, A lo, B hi, B lo) x 16 wave-instructions of 1 KB; wave w issues
 // instructions 2w, 2w+1 of every part -> 8 global_load_lds per thread.
 __device__ inline void sx_issue(const _Float16* __restrict__ ah, const _Float16* __restrict__ al,
