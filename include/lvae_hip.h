@@ -1,9 +1,14 @@
 /*
  * lvae_hip.h -- C ABI of the MI355X-native Longitudinal-VAE GP-prior ELBO hot path.
  *
- * Every entry point is a plain C function over caller-owned device pointers: no allocation
- * inside, no global state, all work enqueued asynchronously on the caller's hipStream_t
- * (passed as void*).  Return value: 0 = ok, <0 = -(index of the bad argument),
+ * Every entry point is a plain C function over caller-owned device pointers: no allocation of
+ * device memory inside, all work enqueued asynchronously on the caller's hipStream_t (passed as
+ * void*), safe to call from several host threads.  Process-wide state is limited to (1) the
+ * opt-in phase timer (lvae_prof_*) and (2) the sweep's side stream (lvae_spd_sweep_f32,
+ * lvae_kl_closed_fwd_f32): one high-priority stream + fork / join event pair per (device, caller
+ * stream), created on first use, kept for the process lifetime, and guarded by a mutex held for
+ * each call's whole enqueue sequence.  The calls are graph-capturable (the side stream joins the
+ * capture through the fork event).  Return value: 0 = ok, <0 = -(index of the bad argument),
  * LVAE_ERR_LAUNCH on a HIP launch error.  Numerical failure (a non-positive-definite pivot) is
  * NOT a return code (the call is asynchronous): it is written to the device `info` array,
  * LAPACK-style (first failing column + 1, 0 = ok), and the Python layer raises
@@ -13,7 +18,7 @@
  *   covar_module(x1, x2).evaluate()       -> lvae_gram_*            (GP_model.py:31-144,
  *                                             kernel_gen.py:9-310, call sites elbo_functions.py:22,56,171-174)
  *   autograd of that Gram wrt (scale, lengthscale) -> lvae_gram_bwd_*
- *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_potrf_*, lvae_potri_*
+ *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_spd_sweep_f32
  *                                             (elbo_functions.py:26-29)
  *   KL_closed forward + autograd backward -> lvae_kl_closed_fwd_f32 / _bwd_f32 (elbo_functions.py:8-34)
  *   batched small fp64 factor + inverse   -> lvae_spd_inv_small_f64 (elbo_functions.py:176-186,
@@ -90,8 +95,11 @@ int lvae_gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2
 
 /* ---------------------------------------------------------------------------------------- */
 /* Regime B: exact KL over the full N x N covariance (elbo_functions.py:8-34), batched over L */
-/* latent dims, fp32 MFMA.  Covariance padded to Np = lvae_kl_closed_padded_n(n) (identity on  */
-/* the padding).                                                                            */
+/* latent dims.  Arithmetic: fp32 storage; every GEMM on the f16 matrix cores with the       */
+/* 3-product hi / lo split (fp32-equivalent, ~2^-22 of max|operand| per product; per-(dim,   */
+/* pass) power-of-two split scales from measured operand bounds, so any K scale / noise level */
+/* that fp32 itself can represent is safe).  Covariance padded to Np =                        */
+/* lvae_kl_closed_padded_n(n) (identity on the padding).                                     */
 /* ---------------------------------------------------------------------------------------- */
 int lvae_kl_closed_padded_n(int n);
 /* bytes of device workspace the fwd+bwd pair needs (kept between the two calls) */
@@ -117,36 +125,17 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
                            const double* gkl, double* dmu, double* dlogv, double* dparams, double* dnoise,
                            void* workspace, void* stream);
 
-/* A^-1 and log|A| of L padded SPD matrices by recursive Schur complements (the Regime B path):
- * A = [[A11, A21^T], [A21, A22]]: A11^-1, X = A21 A11^-1, S = A22 - X A21^T, S^-1, Y = S^-1 X,
- * A^-1 = [[A11^-1 + X^T Y, -Y^T], [-Y, S^-1]], log|A| = log|A11| + log|S|; leaves 128 x 128.
- * A [L, np, np] (lower 128-tiles read; A's lower tiles are overwritten by Schur complements),
- * W [L, np, np] scratch, Ainv [L, np, np] full symmetric out; logdet [L]; info [L] LAPACK-style.
- * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
-int lvae_spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info,
-                         void* stream);
-
 /* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
  * 256-wide pivot blocks -- the default Regime B inverse of lvae_kl_closed_fwd_f32: per pivot block k,
  * A_kk <- -P^-1, A_ik <- A_ik P^-1, A_ij <- A_ij - A_ik P^-1 A_kj (P = A_kk); after the last block
  * A = -K^-1.  np % 256 == 0.  A [L, np, np] (lower 256-block tiles read, overwritten);
  * scratch: lvae_spd_sweep_scratch_size(np, L) bytes, 256-B aligned; Ainv [L, np, np] full
  * symmetric out; logdet [L]; info [L] LAPACK-style (first bad column + 1).  The pivot inverses run
- * on a second (internal) stream joined back to `stream`.
+ * on a second (internal, per caller stream) stream joined back to `stream`.
  * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
 size_t lvae_spd_sweep_scratch_size(int np_, int L);
 int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
                        void* stream);
-
-/* Blocked factorisation of L padded SPD matrices (in place, fp32 MFMA): right-looking block LDL^T
- * with 128-wide pivot blocks, K = Lt Dt Lt^T (the Cholesky factor is Lt chol(Dt)).  On return W's
- * diagonal tiles hold D_k^-1, its strictly-lower tiles Lt; logdet[l] = log|A_l|, info[l] LAPACK-style.
- * A, W: [L, np, np] row-major, np a multiple of 128; only A's lower triangle is read.
- * Replaces torch.cholesky + the log-det (elbo_functions.py:26, 29). */
-int lvae_potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, void* stream);
-/* Ainv = A^-1 (full symmetric) from lvae_potrf_f32's W; A is used as scratch.
- * Replaces cholesky_solve(I, L) (elbo_functions.py:27-28). */
-int lvae_potri_f32(int np_, int L, float* A, float* W, float* Ainv, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Regime A: Hensman SVI, fp64 (elbo_functions.py:144-216; training.py:129-135)             */
@@ -241,18 +230,12 @@ int lvae_predict_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec
 /* the number of bracketed intervals into count[phase], and forgets them.                  */
 /* ---------------------------------------------------------------------------------------- */
 enum lvae_phase {
-  LVAE_PH_GRAM = 0, LVAE_PH_POTRF = 1, LVAE_PH_POTRI = 2, LVAE_PH_KL_REDUCE = 3, LVAE_PH_SYRK = 4,
+  LVAE_PH_GRAM = 0, LVAE_PH_POTRF = 1 /* the whole inverse (sweep) */, LVAE_PH_POTRI = 2 /* unused */, LVAE_PH_KL_REDUCE = 3, LVAE_PH_SYRK = 4,
   LVAE_PH_GRAM_BWD = 5, LVAE_PH_BWD_ELEM = 6, LVAE_PH_HENSMAN_FWD = 7, LVAE_PH_HENSMAN_BWD = 8,
   LVAE_PH_NATGRAD = 9, LVAE_PH_SWEEP_UPD = 10 /* the sweep's U2 launches, nested in POTRF */, LVAE_N_PHASES = 11
 };
 int lvae_prof_enable(int on);
 int lvae_prof_collect(double* ms, int32_t* count, int n_phases);
-
-/* GEMM engine of the Regime B tile GEMMs: bit c set = the fp32-accurate 3-product f16 split
- * (mfma_x3.hpp) for kernel class c (0 panel, 1 update, 2 trtri, 3 z, 4 lauum, 5 syrk,
- * 6 recursive inverse), clear = fp32-input MFMA.  Default 0x7f; LVAE_X3 in the environment
- * overrides it.                                                                              */
-int lvae_gemm_engine_mask(void);
 
 /* library identification: "lvae_hip <version> gfx950" */
 const char* lvae_version(void);

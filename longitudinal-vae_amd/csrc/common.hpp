@@ -23,6 +23,19 @@ constexpr int kWave = 64;
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Split scale of the fp32-accurate f16 GEMMs (mfma_x3.hpp, x3_dma.hpp): x sc = hi + lo in fp16.
+// The power of two 2^floor(log2(2^14 / bound)), clamped to [2^-40, 2^40] (bound 0 or inf / NaN ->
+// 1): every |x| <= bound splits without overflow, and the largest entries keep 2^13..2^14 -- the
+// split is then accurate to ~2^-22 of max|x| whatever the magnitude of the operand.
+__device__ inline float x3_scale(float bound) {
+  if (!(bound > 0.0f) || !(bound < 3.0e38f)) return 1.0f;
+  int e;
+  (void)frexpf(bound, &e);  // bound in [2^(e-1), 2^e)
+  e = 14 - e;
+  e = e < -40 ? -40 : (e > 40 ? 40 : e);
+  return ldexpf(1.0f, e);
+}
+
 // ------------------------------------------------------------------------------------------
 // wave / block reductions (wave64)
 // ------------------------------------------------------------------------------------------

@@ -2,19 +2,17 @@
 // analytic backward, batched over the L latent dims (replaces the Python loop at training.py:515-522).
 //
 //   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
-//   K_l = Lt Dt Lt^T (block LDL^T), logdet         (potrf_f32, MFMA + MFMA sweep of the pivot blocks)
-//   K^-1 = Lt^-T Dt^-1 Lt^-1                       (potri_f32, MFMA)
-//   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation)
+//   K^-1, log|K|                                   (spd_sweep_f32: block symmetric sweep, f16 x3 MFMA)
+//   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation; also the
+//                                                   split bound max |K^-1_ij| sqrt(v_j) of the S GEMM)
 //   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
 // backward (dL/dkl_l = g_l):
-//   S = K^-1 V K^-1                                (syrk_scaled_f32, MFMA, lower tiles)
+//   S = K^-1 V K^-1                                (syrk_x3_f32, f16 x3 MFMA, lower tiles)
 //   G = 1/2 (K^-1 - S - a a^T) -> dtheta, dnoise   (kl_gram_bwd, fused, never materialised)
 //   dmu = g a,  dlogv = g/2 (v d - 1)
 #include "common.hpp"
 #include "prof.hpp"
 
-#include <cstdlib>
-#include <string>
 
 namespace lvae {
 
@@ -24,17 +22,16 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L);
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
                 double* part, double* dparams, double* dnoise, hipStream_t st);
-int potrf_f32(int np_, int L, float* A, float* W, double* logdet, int32_t* info, hipStream_t st);
-int potri_f32(int np_, int L, float* A, float* W, float* Ainv, hipStream_t st);
-int spd_inverse_f32(int np_, int L, float* A, float* W, float* Ainv, double* logdet, int32_t* info, hipStream_t st);
-int syrk_scaled_f32(int np_, int L, const float* B, const float* v, float* S, hipStream_t st);
-int syrk_x3_f32(int np_, int L, const float* Kinv, const float* v, _Float16* planes, float* S, hipStream_t st);
+int syrk_x3_f32(int np_, int L, const float* Kinv, const float* sv, const uint32_t* bmax, _Float16* planes, float* S,
+                hipStream_t st);
 int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
                   hipStream_t st);
 size_t spd_sweep_scratch_bytes(int np_, int L);
 
 struct KLWorkspace {
-  float *A, *W, *Kinv, *v;
+  float *A, *Kinv, *v, *sv;
+  _Float16* planes;  // fp16 hi / lo planes of the S GEMM operand: 2 L np^2 halves
+  uint32_t* bmax;    // [L] fp32 bits of max |K^-1_ij| sqrt(v_j)
   char* sweep;
   double *mu, *alpha, *kdiag, *logdet, *part;
   size_t bytes;
@@ -47,9 +44,11 @@ struct KLWorkspace {
     };
     const size_t mat = (size_t)L * np_ * np_ * sizeof(float);
     A = (float*)take(mat);
-    W = (float*)take(mat);
+    planes = (_Float16*)take(mat);
     Kinv = (float*)take(mat);
     v = (float*)take((size_t)L * np_ * sizeof(float));
+    sv = (float*)take((size_t)L * np_ * sizeof(float));
+    bmax = (uint32_t*)take((size_t)L * sizeof(uint32_t));
     mu = (double*)take((size_t)L * np_ * sizeof(double));
     alpha = (double*)take((size_t)L * np_ * sizeof(double));
     kdiag = (double*)take((size_t)L * np_ * sizeof(double));
@@ -60,34 +59,46 @@ struct KLWorkspace {
   }
 };
 
-// mu / v into contiguous per-dim vectors (zero on the padding)
+// mu / v / sqrt v into contiguous per-dim vectors (zero on the padding)
 __global__ void kl_prep_kernel(const double* __restrict__ mu, const double* __restrict__ logv, int ld, int n, int np_,
-                               int L, double* __restrict__ muc, float* __restrict__ v) {
+                               int L, double* __restrict__ muc, float* __restrict__ v, float* __restrict__ sv) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x, l = blockIdx.y;
   if (i >= np_) return;
   const bool in = i < n;
   muc[(int64_t)l * np_ + i] = in ? mu[(int64_t)i * ld + l] : 0.0;
-  v[(int64_t)l * np_ + i] = in ? (float)exp(logv[(int64_t)i * ld + l]) : 0.f;
+  const double vv = in ? exp(logv[(int64_t)i * ld + l]) : 0.0;
+  v[(int64_t)l * np_ + i] = (float)vv;
+  sv[(int64_t)l * np_ + i] = (float)sqrt(vv);
 }
 
-// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]
+// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]; bmax[l] folds
+// max_j |Kinv[i][j]| sqrt(v_j) (the split bound of the S GEMM operand, syrk_x3.hip)
 __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ muc,
-                                                       int np_, double* __restrict__ alpha,
-                                                       double* __restrict__ kdiag) {
+                                                       const float* __restrict__ sv, int np_,
+                                                       double* __restrict__ alpha, double* __restrict__ kdiag,
+                                                       uint32_t* __restrict__ bmax) {
   const int l = blockIdx.y, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= np_) return;
   const float* row = Kinv + (int64_t)l * np_ * np_ + (int64_t)i * np_;
   const double* m = muc + (int64_t)l * np_;
+  const float* s = sv + (int64_t)l * np_;
   double acc = 0.0;
+  float bm = 0.f;
   for (int j = lane * 4; j < np_; j += 256) {
     const float4 k4 = *reinterpret_cast<const float4*>(row + j);
+    const float4 s4 = *reinterpret_cast<const float4*>(s + j);
     acc += (double)k4.x * m[j] + (double)k4.y * m[j + 1] + (double)k4.z * m[j + 2] + (double)k4.w * m[j + 3];
+    bm = fmaxf(fmaxf(bm, fmaxf(fabsf(k4.x) * s4.x, fabsf(k4.y) * s4.y)),
+               fmaxf(fabsf(k4.z) * s4.z, fabsf(k4.w) * s4.w));
   }
   acc = wave_sum(acc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
   if (lane == 0) {
     alpha[(int64_t)l * np_ + i] = acc;
     kdiag[(int64_t)l * np_ + i] = (double)row[i];
+    atomicMax(bmax + l, __float_as_uint(bm));
   }
 }
 
@@ -154,38 +165,18 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   {
     ProfScope ps(LVAE_PH_GRAM, st);
     LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
-    kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v);
+    kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v, ws.sv);
   }
   {
-    // K^-1 and log|K|.  Default: the block symmetric sweep (spd_sweep.hip: 16 rank-256 passes at
-    // np = 4096, pivot inverses overlapped on a second stream).  LVAE_KL_INV=ldl: block LDL^T
-    // (128-wide pivots) + triangular inverse + product; LVAE_KL_INV=rec: recursive Schur
-    // complements (multiplies by explicit inverses of blocks up to N/2 wide: at N = 4096 its
-    // dmu / dlogv errors reach 9e-5 of the 1e-4 budget).
-    static const int inv = [] {
-      const char* e = getenv("LVAE_KL_INV");
-      if (!e) return 0;
-      const std::string s(e);
-      return s == "ldl" ? 1 : (s == "rec" ? 2 : 0);
-    }();
-    if (inv == 0) {
-      ProfScope ps(LVAE_PH_POTRF, st);
-      LVAE_TRY(spd_sweep_f32(np_, L, ws.A, ws.sweep, ws.Kinv, ws.logdet, info, st));
-    } else if (inv == 2) {
-      ProfScope ps(LVAE_PH_POTRF, st);
-      LVAE_TRY(spd_inverse_f32(np_, L, ws.A, ws.W, ws.Kinv, ws.logdet, info, st));
-    } else {
-      {
-        ProfScope ps(LVAE_PH_POTRF, st);
-        LVAE_TRY(potrf_f32(np_, L, ws.A, ws.W, ws.logdet, info, st));
-      }
-      ProfScope ps(LVAE_PH_POTRI, st);
-      LVAE_TRY(potri_f32(np_, L, ws.A, ws.W, ws.Kinv, st));
-    }
+    // K^-1 and log|K|: the block symmetric sweep (spd_sweep.hip: 16 rank-256 passes at np = 4096,
+    // pivot inverses overlapped on a second stream)
+    ProfScope ps(LVAE_PH_POTRF, st);
+    LVAE_TRY(spd_sweep_f32(np_, L, ws.A, ws.sweep, ws.Kinv, ws.logdet, info, st));
   }
   {
     ProfScope ps(LVAE_PH_KL_REDUCE, st);
-    kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, np_, ws.alpha, ws.kdiag);
+    (void)hipMemsetAsync(ws.bmax, 0, sizeof(uint32_t) * L, st);
+    kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.alpha, ws.kdiag, ws.bmax);
     kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   }
   LVAE_CHECK_LAUNCH();
@@ -201,16 +192,11 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
-  // S = K^-1 V K^-1 into the (no longer needed) Gram buffer; the fp16 hi / lo planes of the
-  // split operand go to the (no longer needed) factor buffer W (2 x 2 B per element = its size).
-  // np a multiple of 256: the pre-split 256-tile kernel (syrk_x3.hip); else the generic tile GEMM.
+  // S = K^-1 V K^-1 into the (no longer needed) Gram buffer, through the fp16 hi / lo planes of
+  // K^-1 diag(sqrt v) (np is a multiple of 256: lvae_kl_closed_padded_n)
   {
-    static const bool generic = getenv("LVAE_SYRK_GENERIC") && atoi(getenv("LVAE_SYRK_GENERIC"));
     ProfScope ps(LVAE_PH_SYRK, st);
-    if (!generic && np_ % 256 == 0)
-      LVAE_TRY(syrk_x3_f32(np_, L, ws.Kinv, ws.v, (_Float16*)ws.W, ws.A, st));
-    else
-      LVAE_TRY(syrk_scaled_f32(np_, L, ws.Kinv, ws.v, ws.A, st));
+    LVAE_TRY(syrk_x3_f32(np_, L, ws.Kinv, ws.sv, ws.bmax, ws.planes, ws.A, st));
   }
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);

@@ -1,8 +1,9 @@
 // mfma_x3.hpp -- fp32-accurate 128x128 tile GEMM on the f16 matrix cores (3-product split).
 //
 // gfx950 has no xf32: fp32-input MFMA runs at 1/16 of the f16 rate (157 vs 2500 TFLOP/s dense).
-// Each fp32 operand x is split once, while it is staged into LDS, into x = hi + lo with hi, lo
-// fp16 (x scaled by 2^8 first so that lo stays a normal half for |x| >= 2^-11), and a product is
+// Each fp32 operand x is split once, while it is staged into LDS, into x sc = hi + lo with hi, lo
+// fp16 (sc a power of two from a bound on the operand's max |x|, x3_scale: the largest entries
+// land in [2^13, 2^14), far from fp16 overflow, and lo stays normal down to 2^-17 of them), and a product is
 // hi_a hi_b + hi_a lo_b + lo_a hi_b: three v_mfma_f32_32x32x16_f16 with fp32 accumulation.  The
 // dropped lo_a lo_b term and the split leave a relative error ~2^-22 per product -- between fp32
 // (2^-24) and anything a 16-bit format gives -- at 3/16 of the fp32-MFMA cost.
@@ -29,16 +30,17 @@ typedef _Float16 x3_half4 __attribute__((ext_vector_type(4)));
 constexpr int kX3BK = LVAE_X3_BK;              // K chunk per LDS stage
 constexpr int kX3Ld = kX3BK + 8;               // LDS row pitch in halves (16-B aligned rows)
 constexpr int kX3Op = kTM * kX3Ld;             // halves per operand part (hi or lo)
-constexpr float kX3Scale = 256.0f;             // per-operand scale (exact power of two)
-constexpr float kX3Unscale = 1.0f / 65536.0f;  // 1 / scale^2
 
 constexpr int x3_lds_bytes() { return 4 * kX3Op * (int)sizeof(_Float16); }
 
-__device__ inline void x3_split(float x, _Float16& hi, _Float16& lo) {
-  const float s = x * kX3Scale;
+// x = (hi + lo) / sc: sc is a power of two chosen by the caller from a bound on |x| (x3_scale) so
+// that |x sc| stays below 2^14 -- fp16 overflows at 65504 -- and the split stays exact in sc.
+__device__ inline void x3_split(float x, float sc, _Float16& hi, _Float16& lo) {
+  const float s = x * sc;
   hi = (_Float16)s;
   lo = (_Float16)(s - (float)hi);
 }
+
 
 // Register prefetch of one 128 x kX3BK fp32 chunk (NV = kX3BK / 8 float4 per thread).
 //  KCONT (ptr[row * ld + k]): thread t holds rows (t >> 3) + 32 i (i < NV/2... see below), k-quads.
@@ -86,9 +88,10 @@ struct X3Chunk {
   }
 };
 
-// Stage one prefetched fp32 chunk as hi / lo halves in [row][k] layout.
+// Stage one prefetched fp32 chunk as hi / lo halves of x * sc in [row][k] layout.
 template <bool KCONT>
-__device__ inline void x3_store(const X3Chunk<KCONT>& c, _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
+__device__ inline void x3_store(const X3Chunk<KCONT>& c, float sc, _Float16* __restrict__ hi,
+                                _Float16* __restrict__ lo) {
   const int t = threadIdx.x;
   if constexpr (KCONT) {
     constexpr int QPR = kX3BK / 4, RPP = 256 / QPR;
@@ -99,7 +102,7 @@ __device__ inline void x3_store(const X3Chunk<KCONT>& c, _Float16* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         _Float16 a, b;
-        x3_split(c.v[i][e], a, b);
+        x3_split(c.v[i][e], sc, a, b);
         h[e] = a;
         l[e] = b;
       }
@@ -117,7 +120,7 @@ __device__ inline void x3_store(const X3Chunk<KCONT>& c, _Float16* __restrict__ 
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           _Float16 a, b;
-          x3_split(c.v[4 * g + kk][e], a, b);
+          x3_split(c.v[4 * g + kk][e], sc, a, b);
           h[kk] = a;
           l[kk] = b;
         }
@@ -165,17 +168,19 @@ __device__ inline void frag_scale(Frag& f, float s) {
 }
 
 // acc (+/-)= op(A)[128 x K] op(B)[K x 128] over k in [kbeg, kend) (multiples of kX3BK),
-// fp32-accurate on the f16 matrix cores.  lds: x3_lds_bytes() bytes, 16-B aligned.
+// fp32-accurate on the f16 matrix cores.  lds: x3_lds_bytes() bytes, 16-B aligned.  sa / sb: the
+// split scales of op(A) / op(B) (x3_scale of a bound on each operand's max |entry|).
 template <bool AK, bool BKc, bool NEG = false>
 __device__ inline void tile_gemm_x3(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
-                                    int kbeg, int kend, Frag& f, _Float16* __restrict__ lds,
+                                    int kbeg, int kend, Frag& f, _Float16* __restrict__ lds, float sa, float sb,
                                     const float* __restrict__ ascale = nullptr) {
   if (kend <= kbeg) return;
   _Float16* ah = lds;
   _Float16* al = lds + kX3Op;
   _Float16* bh = lds + 2 * kX3Op;
   _Float16* bl = lds + 3 * kX3Op;
-  frag_scale(f, 1.0f / kX3Unscale);  // accumulate in scale^2 units (exact)
+  const float sab = sa * sb;
+  frag_scale(f, sab);  // accumulate in sa sb units (exact: powers of two)
   X3Chunk<AK> ca;
   X3Chunk<BKc> cb;
   ca.load(A, lda, kbeg);
@@ -184,8 +189,8 @@ __device__ inline void tile_gemm_x3(const float* __restrict__ A, int64_t lda, co
     if (ascale) ca.scale_k(ascale, k0);
     if constexpr (NEG) ca.negate();
     __syncthreads();  // previous chunk fully consumed
-    x3_store<AK>(ca, ah, al);
-    x3_store<BKc>(cb, bh, bl);
+    x3_store<AK>(ca, sa, ah, al);
+    x3_store<BKc>(cb, sb, bh, bl);
     __syncthreads();
     if (k0 + kX3BK < kend) {
       ca.load(A, lda, k0 + kX3BK);
@@ -193,7 +198,7 @@ __device__ inline void tile_gemm_x3(const float* __restrict__ A, int64_t lda, co
     }
     x3_mma_chunk(ah, al, bh, bl, f);
   }
-  frag_scale(f, kX3Unscale);
+  frag_scale(f, 1.0f / sab);
 }
 
 }  // namespace lvae

@@ -2,7 +2,8 @@
 // on the f16 matrix cores with the fp32-accurate 3-product split (see mfma_x3.hpp for the error
 // argument), specialised for throughput:
 //
-//   split : B = 256 K^-1 diag(sqrt v) is split ONCE into fp16 hi / lo planes (B = hi + lo; the
+//   split : B sc = K^-1 diag(sqrt v) sc is split ONCE into fp16 hi / lo planes (sc = x3_scale of
+//           max |B|, found by kl_alpha_kernel in the forward; B sc = hi + lo; the
 //           generic x3 tile GEMM re-splits every operand chunk for every output tile);
 //   syrk  : 256 x 256 output tiles, 512 threads = 8 waves (2 along M x 4 along N, 128 x 64 each,
 //           4 x 2 blocks of v_mfma_f32_32x32x16_f16, three products per block and k-step);
@@ -22,7 +23,8 @@
 
 namespace lvae {
 
-__global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict__ Kinv, const float* __restrict__ v,
+__global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict__ Kinv, const float* __restrict__ sv,
+                                                         const uint32_t* __restrict__ bmax,
                                                          _Float16* __restrict__ Bh, _Float16* __restrict__ Bl,
                                                          int np_, int64_t n4) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -32,11 +34,12 @@ __global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict
   const int l = (int)(i0 / per);
   const int k = (int)(i0 % np_);
   const sx_f32x4 x = *reinterpret_cast<const sx_f32x4*>(Kinv + i0);
-  const sx_f32x4 s = *reinterpret_cast<const sx_f32x4*>(v + (int64_t)l * np_ + k);
+  const sx_f32x4 s = *reinterpret_cast<const sx_f32x4*>(sv + (int64_t)l * np_ + k);
+  const float sc = x3_scale(__uint_as_float(bmax[l]));
   sx_half4 h, lo;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float y = x[q] * sqrtf(s[q]) * kSxScale;
+    const float y = x[q] * s[q] * sc;
     const _Float16 hh = (_Float16)y;
     h[q] = hh;
     lo[q] = (_Float16)(y - (float)hh);
@@ -46,7 +49,8 @@ __global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict
 }
 
 __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
-                                                      float* __restrict__ S, int np_, int ntl, int nwg) {
+                                                      const uint32_t* __restrict__ bmax, float* __restrict__ S,
+                                                      int np_, int ntl, int nwg) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];  // 128 KB, the only LDS object
   // XCD-contiguous remap (bijective): blocks sharing blockIdx % 8 take a contiguous wgid range
   const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
@@ -73,6 +77,7 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   sx_gemm(ah, al, bh, bl, ld, np_, lds, acc);
   // epilogue: C layout of 32x32 blocks -- row (e&3) + 8(e>>2) + 4(lane>>5), col lane&31
+  const float sc = x3_scale(__uint_as_float(bmax[l])), inv = 1.0f / (sc * sc);
   float* C = S + base + (int64_t)(I * kSxT + wm) * ld + J * kSxT + wn;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -81,19 +86,21 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * kh, col = 32 * b + r32;
-        C[(int64_t)row * ld + col] = acc[a][b][e] * kSxUnscale;
+        C[(int64_t)row * ld + col] = acc[a][b][e] * inv;
       }
 }
 
 // S (lower 256-tiles of [L, np, np] fp32) = K^-1 diag(v) K^-1; planes: 2 L np^2 halves of scratch.
-int syrk_x3_f32(int np_, int L, const float* Kinv, const float* v, _Float16* planes, float* S, hipStream_t st) {
+// sv = sqrt(v) [L, np]; bmax[l] = fp32 bits of max_ij |K^-1_ij| sv_j (the split bound of B).
+int syrk_x3_f32(int np_, int L, const float* Kinv, const float* sv, const uint32_t* bmax, _Float16* planes, float* S,
+                hipStream_t st) {
   if (np_ % kSxT) return -1;
   const int64_t per = (int64_t)np_ * np_, n4 = (int64_t)L * per / 4;
   _Float16* Bh = planes;
   _Float16* Bl = planes + (int64_t)L * per;
-  syrk_split_kernel<<<cdiv(n4, 256), 256, 0, st>>>(Kinv, v, Bh, Bl, np_, n4);
+  syrk_split_kernel<<<cdiv(n4, 256), 256, 0, st>>>(Kinv, sv, bmax, Bh, Bl, np_, n4);
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L;
-  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, S, np_, ntl, nwg);
+  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, bmax, S, np_, ntl, nwg);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -22,8 +22,6 @@ typedef float sx_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSxT = 256;                // output tile edge
 constexpr int kSxBK = 32;                // K chunk (halves) per LDS stage
 constexpr int kSxPart = kSxT * kSxBK;    // halves per operand part per stage (16 KB)
-constexpr float kSxScale = 256.0f;
-constexpr float kSxUnscale = 1.0f / 65536.0f;
 
 // linear index t of a lower-triangular tile grid (row-major) -> (I, J), J <= I
 __device__ inline void sx_tri(int t, int& I, int& J) {

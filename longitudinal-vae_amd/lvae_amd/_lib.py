@@ -86,8 +86,6 @@ SIGNATURES = {
                                       _I32, _VP]),
     "lvae_kl_closed_bwd_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _VP, _VP, _VP, _VP,
                                       _VP, _VP, _VP]),
-    "lvae_potrf_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP]),
-    "lvae_potri_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_spd_inv_small_f64": (_I32, [_I32, _I32, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),
     "lvae_gemm_small_f64": (_I32, [_I32, _I32, _I32, _I32, _I32, _D, _VP, _I32, _I64, _I64, _VP, _I32, _I64,
                                    _I64, _D, _VP, _I32, _I64, _I64, _I32, _I32, _VP]),
@@ -99,10 +97,8 @@ SIGNATURES = {
     "lvae_natgrad_workspace_size": (_SZ, [_I32, _I32]),
     "lvae_natgrad_update_f64": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _D, _VP, _VP, _VP, _VP]),
     "lvae_hensman_iH_offset": (_SZ, [_DIMS]),
-    "lvae_gemm_engine_mask": (_I32, []),
     "lvae_relu_maxpool2_fwd_f32": (_I32, [_VP, _I64, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _I32, _I32, _VP, _VP]),
-    "lvae_spd_inverse_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),

@@ -141,10 +141,13 @@ def gram(spec, params, x1, x2):
 #   KL = 1/2 ( tr(K^-1 V) + mu^T K^-1 mu - N + log|K| - sum log v ),  K = Gram + noise I
 # ------------------------------------------------------------------------------------------
 def kl_closed(spec, params, x, noise, mu, logv):
+    """Device-agnostic: on CPU tensors it is the CPU oracle; the large-N parity tests also evaluate
+    this same fp64 formula with the tensors on the GPU (PyTorch's fp64 Cholesky) as the checker."""
     n = x.shape[0]
-    K = gram(spec, params, x, x) + noise * torch.eye(n, dtype=x.dtype)
+    eye = torch.eye(n, dtype=x.dtype, device=x.device)
+    K = gram(spec, params, x, x) + noise * eye
     L = torch.linalg.cholesky(K)
-    Kinv = torch.cholesky_solve(torch.eye(n, dtype=x.dtype), L)
+    Kinv = torch.cholesky_solve(eye, L)
     logdetK = 2 * torch.log(torch.diagonal(L)).sum()
     quad = (mu * (Kinv @ mu)).sum()
     trace = (torch.exp(logv) * torch.diagonal(Kinv)).sum()
@@ -162,22 +165,22 @@ def kl_closed(spec, params, x, noise, mu, logv):
 def hensman_kld(spec0, params0, spec1, params1, noise, m, H, x, mu, logv, z, P_tot, P_b, T,
                 natural_gradient, eps):
     Lh, M = H.shape[0], H.shape[-1]
-    dt = x.dtype
+    dt, dev = x.dtype, x.device  # device-agnostic (large-shape tests also run this formula on the GPU)
     xs = x.reshape(P_b, T, x.shape[-1])
     K0xz = gram(spec0, params0, x, z)                                  # [L, B, M]
-    K0zz = gram(spec0, params0, z, z) + eps * torch.eye(M, dtype=dt)   # [L, M, M]
+    K0zz = gram(spec0, params0, z, z) + eps * torch.eye(M, dtype=dt, device=dev)   # [L, M, M]
     xs_l = xs.unsqueeze(1).expand(P_b, Lh, T, xs.shape[-1])
     K0 = gram(spec0, params0, xs_l, xs_l).transpose(0, 1)              # [L, P_b, T, T]
-    Bm = (gram(spec1, params1, xs_l, xs_l) + torch.eye(T, dtype=dt) * noise.reshape(Lh, 1, 1)).transpose(0, 1)
+    Bm = (gram(spec1, params1, xs_l, xs_l) + torch.eye(T, dtype=dt, device=dev) * noise.reshape(Lh, 1, 1)).transpose(0, 1)
     LK = torch.linalg.cholesky(K0zz)
-    iK = torch.cholesky_solve(torch.eye(M, dtype=dt), LK)
+    iK = torch.cholesky_solve(torch.eye(M, dtype=dt, device=dev), LK)
     LB = torch.linalg.cholesky(Bm)
-    iB = torch.cholesky_solve(torch.eye(T, dtype=dt), LB)
+    iB = torch.cholesky_solve(torch.eye(T, dtype=dt, device=dev), LB)
     Kst = K0xz.reshape(Lh, P_b, T, M)
     iBK = iB @ Kst
     Q = K0xz.transpose(1, 2) @ iBK.reshape(Lh, P_b * T, M)
     LH = torch.linalg.cholesky(H)
-    iH = torch.cholesky_solve(torch.eye(M, dtype=dt), LH)
+    iH = torch.cholesky_solve(torch.eye(M, dtype=dt, device=dev), LH)
     r = ((K0xz @ (iK @ m)).squeeze(-1) - mu.T).reshape(Lh, P_b, T, 1)
     A = (r.transpose(2, 3) @ iB @ r).sum()
     Bt = (torch.diagonal(iB, dim1=-2, dim2=-1).reshape(Lh, -1) * torch.exp(logv.T)).sum()

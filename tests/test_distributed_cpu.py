@@ -149,3 +149,102 @@ def test_varying_length_batches():
     assert flat == list(range(len(ids)))
     for b in batches:
         assert len({ids[i] for i in b}) <= 2
+
+
+CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+           cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                           {'cont_covariate': 0, 'cat_covariate': 3},
+                           {'cont_covariate': 1, 'cat_covariate': 4}],
+           bin_int_kernel=[], covariate_missing_val=[])
+SH_P, SH_T, SH_L = 8, 8, 4
+
+
+def _sharded_problem():
+    """Fixed weights / data of the latent-sharded closed-step test (identical on every process)."""
+    import lvae_amd as la
+    from lvae_amd.vae import ConvVAE
+    from lvae_amd.data import health_mnist_batch
+    from oracle import lvae_oracle as O
+    img, mask, X = health_mnist_batch(SH_P, SH_T, seed=12, dtype=torch.float64)
+    ref_vae = O.ConvVAE(SH_L).double()
+    ref_vae.load_state_dict(O.vae_weights(ref_vae, 5))
+    vae = ConvVAE(SH_L, 1296, p_input=0.0, p=0.0).double()
+    vae.load_state_dict(ref_vae.state_dict())
+    k = la.generate_kernel(**CFG, latent_dim=SH_L)
+    rng = np.random.default_rng(3)
+    with torch.no_grad():
+        for _, p in k.named_parameters():
+            p.copy_(torch.tensor(np.log(rng.uniform(0.5, 3.0, SH_L))))
+    eps = torch.randn(SH_P * SH_T, SH_L, generator=torch.Generator().manual_seed(2), dtype=torch.float64)
+    return img, mask, X, ref_vae, vae, k, eps
+
+
+def _oracle_kl(spec, params, noise, mu, logv, X):
+    from oracle import lvae_oracle as O
+    s = O.spec_full(**CFG)
+    return torch.stack([O.kl_closed(s, params[i], X, noise[i], mu[:, i], logv[:, i]) for i in range(params.shape[0])])
+
+
+def _sharded_worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lvae_amd as la
+        from lvae_amd.distributed import LatentShardedClosedStep, shard_bounds
+        img, mask, X, _, vae, k, eps = _sharded_problem()
+        lik = la.GaussianLikelihood(SH_L, noise=1.0)
+        opt = torch.optim.SGD(list(vae.parameters()) + list(k.parameters()), lr=0.0)
+        step = LatentShardedClosedStep(vae, k, lik, opt, weight=0.15, loss_function="mse", kl_fn=_oracle_kl)
+        lo, hi = shard_bounds(SH_P * SH_T, world, rank)
+        net, rl, _, gp = step(img[lo:hi], mask[lo:hi], X, eps[lo:hi])
+        q.put((rank, float(net), float(rl), float(gp),
+               torch.stack([p.grad for _, p in k.named_parameters()], 1).numpy().copy(),
+               [p.grad.numpy().copy() for p in vae.parameters()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_latent_sharded_closed_step():
+    """Regime B over 2 ranks (latent dims 0-1 / 2-3, images 0-31 / 32-63, gloo on CPU, the oracle KL
+    as the engine) equals one process with the whole batch (oracle.closed_step): the loss terms, the
+    raw kernel-parameter gradients and every network gradient, on both ranks."""
+    from oracle import lvae_oracle as O
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    img, mask, X, ref_vae, _, k, eps = _sharded_problem()
+    raw = torch.stack([p.detach().clone() for _, p in k.named_parameters()], 1).requires_grad_()
+    loss, recon, gp = O.closed_step(ref_vae, O.spec_full(**CFG), raw, torch.ones(SH_L, dtype=torch.float64), img,
+                                    mask, X, eps, 0.15)
+    for rank, net, rl, g, draw, vgrads in res:
+        assert abs(net - loss.item()) <= 1e-10 * abs(loss.item())
+        assert abs(rl - recon.item()) <= 1e-10 * abs(recon.item())
+        assert abs(g - gp.item()) <= 1e-10 * abs(gp.item())
+        assert np.allclose(draw, raw.grad.numpy(), rtol=1e-9, atol=1e-12)
+        for vg, (name, p) in zip(vgrads, ref_vae.named_parameters()):
+            ref = np.zeros_like(vg) if p.grad is None else p.grad.numpy()
+            assert np.allclose(vg, ref, rtol=1e-8, atol=1e-12), name
+    # both ranks hold the same reduced gradients
+    for a, b in zip(res[0][5], res[1][5]):
+        assert np.array_equal(a, b)
+
+
+def test_shard_bounds():
+    from lvae_amd.distributed import shard_bounds
+    for n, w in [(16, 8), (16, 3), (5, 8), (4096, 8)]:
+        spans = [shard_bounds(n, w, r) for r in range(w)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1

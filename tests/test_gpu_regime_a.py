@@ -366,3 +366,117 @@ def test_gpapprox_elbo_and_dubo_golden(hip):
     vd = la.validation_dubo(1, k0, k1, lik, X, torch.tensor(g["mu"], device=DEV)[:, None],
                             torch.tensor(g["logv"], device=DEV)[:, None], Z[None], P, T, float(g["eps"]))
     assert rel(vd, g["dubo"]) < 1e-9
+
+
+def _c4_problem(seed, benign):
+    """C3/C4 Regime A shapes: L = 16, M = 120 (the hard-coded inducing rows of LVAE.py:199-203 at
+    N >= 2060), P_b = 5 subjects x T = 16 of P_tot = 256 (N = 4096); random per-dim hyper-parameters;
+    (m, H) the LVAE.py:222-226 draw (m ~ N(0,1), H = X X^T / 100) or the benign (0, K0zz)."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    L, M, T, P_tot = 16, 120, 16, 256
+    N = P_tot * T
+    X = torch.tensor(health_mnist_covariates(P_tot, T, seed=seed))
+    gen = torch.Generator().manual_seed(seed)
+    mu = torch.randn(N, L, generator=gen, dtype=torch.float64)
+    lv = 0.1 * torch.randn(N, L, generator=gen, dtype=torch.float64)
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    rng = np.random.default_rng(seed)
+    raw0 = np.log(rng.uniform(0.5, 2.0, (L, len(list(k0.parameters())))))
+    raw1 = np.log(rng.uniform(0.5, 2.0, (L, len(list(k1.parameters())))))
+    set_raw(k0, raw0)
+    set_raw(k1, raw1)
+    s0, s1 = O.spec_split(**CFG, id_covariate=2)
+    if benign:
+        m = torch.zeros(L, M, 1, dtype=torch.float64)
+        H = O.gram(s0, O.constrain(torch.tensor(raw0)), z, z) + 1e-6 * torch.eye(M, dtype=torch.float64)
+    else:
+        m = torch.randn(L, M, 1, generator=gen, dtype=torch.float64)
+        Xh = torch.randn(L, M, M, generator=gen, dtype=torch.float64) / 10
+        H = Xh @ Xh.transpose(1, 2)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    return dict(L=L, M=M, T=T, P_tot=P_tot, X=X, mu=mu, lv=lv, z=z, k0=k0.to(DEV), k1=k1.to(DEV), lik=lik,
+                raw0=raw0, raw1=raw1, s0=s0, s1=s1, m=m, H=H)
+
+
+@pytest.mark.parametrize("benign", [False, True])
+def test_hensman_c4_shapes_vs_oracle(hip, benign):
+    """minibatch_KLD_upper_bound at the C3 / C4 Regime A shapes (L = 16, M = 120, P_b = 5, T = 16)
+    vs the fp64 oracle: the bound, grad_m / grad_H and every autograd gradient.
+
+    K0zz carries the 1e-6 jitter (cond ~1e8..1e10 at M = 120 with random hyper-parameters) and the
+    k1 / noise gradients contain Xq = c (iK H iK - iK), a difference of O(|iK|^2) terms, so fp64
+    itself determines them only to a few digits.  The test measures that: the oracle formula is
+    evaluated twice in fp64 -- LAPACK on the CPU and rocSOLVER / rocBLAS on the GPU -- and each
+    quantity must match within max(base, 10 x the two fp64 oracles' own spread); base = 1e-8 (bound),
+    1e-6 (gradients), as the golden tests."""
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    c = _c4_problem(41, benign)
+    L, M, T, P_tot = c["L"], c["M"], c["T"], c["P_tot"]
+    subjects = [7, 130, 64, 201, 12]
+    rows = torch.cat([torch.arange(s * T, (s + 1) * T) for s in subjects])
+    mu = c["mu"][rows].to(DEV).requires_grad_()
+    lv = c["lv"][rows].to(DEV).requires_grad_()
+    kld, gm, gH = minibatch_KLD_upper_bound(c["k0"], c["k1"], c["lik"], L, c["m"].to(DEV), c["H"].to(DEV),
+                                            c["X"][rows].to(DEV), mu, lv, c["z"].to(DEV), P_tot, 5, T, True, 1e-6)
+    kld.backward()
+    hip_vals = dict(kld=kld, dmu=mu.grad, dlogv=lv.grad,
+                    draw0=torch.stack([p.grad for _, p in c["k0"].named_parameters()], 1),
+                    draw1=torch.stack([p.grad for _, p in c["k1"].named_parameters()], 1), gm=gm, gH=gH)
+
+    def oracle(dev):
+        r0 = torch.tensor(c["raw0"], device=dev, requires_grad=True)
+        r1 = torch.tensor(c["raw1"], device=dev, requires_grad=True)
+        mu_r = c["mu"][rows].to(dev).requires_grad_()
+        lv_r = c["lv"][rows].to(dev).requires_grad_()
+        ref, gm_r, gH_r = O.hensman_kld(c["s0"], O.constrain(r0), c["s1"], O.constrain(r1),
+                                        torch.ones(L, dtype=torch.float64, device=dev), c["m"].to(dev),
+                                        c["H"].to(dev), c["X"][rows].to(dev), mu_r, lv_r, c["z"].to(dev), P_tot, 5, T,
+                                        True, 1e-6)
+        ref.backward()
+        return dict(kld=ref, dmu=mu_r.grad, dlogv=lv_r.grad, draw0=r0.grad, draw1=r1.grad, gm=gm_r, gH=gH_r)
+
+    cpu, gpu = oracle("cpu"), oracle(DEV)
+    base = dict(kld=1e-8, dmu=1e-6, dlogv=1e-6, draw0=1e-6, draw1=1e-6, gm=1e-6, gH=1e-6)
+    for key, b in base.items():
+        err, spread = rel(hip_vals[key], cpu[key]), rel(gpu[key], cpu[key])
+        print(f"C4 Regime A {'benign' if benign else 'LVAE-init'} {key}: err {err:.2e}, fp64 oracle spread {spread:.2e}")
+        assert err < max(b, 10 * spread), key
+
+
+def test_dp_contract_c4_eight_ranks(hip):
+    """The C4 data-parallel contract at its own shapes: 8 ranks x P_b = 5 subjects, simulated
+    sequentially on one GPU with ng_prior_share = 1/8.  The mean over ranks of the bound and of the
+    Adam gradients and the SUM of the natural-gradient directions equal one process with the 40-subject
+    union batch; each rank's mu / logv gradient rows equal 8x the union's rows.
+    The jitter is 1e-3 here (the reference's 1e-6 makes cond(K0zz) ~1e8..1e10, and then two fp64
+    evaluations of one bound already differ in the 9th digit -- test_hensman_c4_shapes_vs_oracle);
+    the identity itself holds for any jitter, and is checked to near round-off this way."""
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    c = _c4_problem(43, False)
+    L, T, P_tot, W, P_b = c["L"], c["T"], c["P_tot"], 8, 5
+    perm = torch.randperm(P_tot, generator=torch.Generator().manual_seed(5))[:W * P_b].tolist()
+    m, H, z = c["m"].to(DEV), c["H"].to(DEV), c["z"].to(DEV)
+    params = list(c["k0"].parameters()) + list(c["k1"].parameters())
+
+    def run(subjects, share):
+        for p in params:
+            p.grad = None
+        rows = torch.cat([torch.arange(s * T, (s + 1) * T) for s in subjects])
+        mu = c["mu"][rows].to(DEV).requires_grad_()
+        kld, gm, gH = minibatch_KLD_upper_bound(c["k0"], c["k1"], c["lik"], L, m, H, c["X"][rows].to(DEV), mu,
+                                                c["lv"][rows].to(DEV), z, P_tot, len(subjects), T, True, 1e-3,
+                                                ng_prior_share=share)
+        kld.backward()
+        return kld.detach(), gm, gH, [p.grad.clone() for p in params], mu.grad.detach()
+
+    u = run(perm, 1.0)
+    ranks = [run(perm[r * P_b:(r + 1) * P_b], 1.0 / W) for r in range(W)]
+    errs = dict(kld=rel(sum(r[0] for r in ranks) / W, u[0]),
+                grads=max(rel(sum(r[3][i] for r in ranks) / W, u[3][i]) for i in range(len(params))),
+                gm=rel(sum(r[1] for r in ranks), u[1]), gH=rel(sum(r[2] for r in ranks), u[2]),
+                dmu=rel(torch.cat([r[4] for r in ranks]) / W, u[4]))
+    print("8-rank DP contract errors:", errs)
+    assert errs["kld"] < 1e-10 and errs["dmu"] < 1e-10
+    assert errs["grads"] < 1e-8 and errs["gm"] < 1e-8 and errs["gH"] < 1e-8

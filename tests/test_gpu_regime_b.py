@@ -100,40 +100,6 @@ def test_kl_closed_vs_oracle(hip, P, L):
         assert rel(draw, r.grad) < 1e-4
 
 
-def test_potrf_potri(hip):
-    """Blocked MFMA block-LDL^T + inverse on random SPD matrices vs fp64 torch on the host:
-    Lt Dt Lt^T reconstructs A, log|A| and A^-1 match (np = 384: three 128-blocks)."""
-    import lvae_amd as la
-    lib = hip
-    L, n, nb = 2, 384, 128
-    gen = torch.Generator().manual_seed(1)
-    Xm = torch.randn(L, n, n, generator=gen, dtype=torch.float64) / n ** 0.5
-    A = Xm @ Xm.transpose(1, 2) + torch.eye(n, dtype=torch.float64)
-    Ad = torch.tril(A).float().to(DEV).contiguous()  # only the lower triangle is read
-    W = torch.zeros_like(Ad)
-    Ai = torch.zeros_like(Ad)
-    logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
-    info = torch.zeros(L, dtype=torch.int32, device=DEV)
-    P = la._lib
-    P.check(lib.lvae_potrf_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(logdet), P.ptr(info), P.stream_ptr()), "potrf")
-    torch.cuda.synchronize()
-    Wc = W.cpu().double()
-    Lt = torch.eye(n, dtype=torch.float64).repeat(L, 1, 1)
-    Dt = torch.zeros(L, n, n, dtype=torch.float64)
-    for I in range(n // nb):
-        sl = slice(I * nb, (I + 1) * nb)
-        Dt[:, sl, sl] = torch.linalg.inv(Wc[:, sl, sl])
-        for J in range(I):
-            sj = slice(J * nb, (J + 1) * nb)
-            Lt[:, sl, sj] = Wc[:, sl, sj]
-    assert int(info.abs().sum()) == 0
-    assert rel(Lt @ Dt @ Lt.transpose(1, 2), A) < 1e-5
-    assert rel(logdet.cpu(), torch.logdet(A)) < 1e-5
-    P.check(lib.lvae_potri_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(Ai), P.stream_ptr()), "potri")
-    torch.cuda.synchronize()
-    assert rel(Ai.cpu(), torch.linalg.inv(A)) < 1e-4
-
-
 def test_not_positive_definite_raises(hip):
     import lvae_amd as la
     from lvae_amd.data import health_mnist_covariates
@@ -179,29 +145,6 @@ def test_gram_batched_semantics(hip):
     (O.gram(s0, O.constrain(raw), X, Z) * G).sum().backward()
     got = torch.stack([p.grad.cpu() for _, p in k0.named_parameters()], 1)
     assert rel(got, raw.grad) < 1e-12
-
-
-@pytest.mark.parametrize("n", [128, 384, 640, 1024])
-def test_spd_inverse_recursive(hip, n):
-    """Recursive Schur-complement inverse (the Regime B path) vs fp64 torch: A^-1 and log|A|; odd
-    tile counts exercise the uneven split.  The upper triangle of A is never read."""
-    import lvae_amd as la
-    L = 2
-    gen = torch.Generator().manual_seed(n)
-    Xm = torch.randn(L, n, n, generator=gen, dtype=torch.float64) / n ** 0.5
-    A = Xm @ Xm.transpose(1, 2) + torch.eye(n, dtype=torch.float64)
-    Ad = (torch.tril(A) + 7.0 * torch.triu(torch.ones(n, n, dtype=torch.float64), 1)).float().to(DEV).contiguous()
-    W = torch.zeros_like(Ad)
-    Ai = torch.zeros_like(Ad)
-    logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
-    info = torch.zeros(L, dtype=torch.int32, device=DEV)
-    P = la._lib
-    P.check(hip.lvae_spd_inverse_f32(n, L, P.ptr(Ad), P.ptr(W), P.ptr(Ai), P.ptr(logdet), P.ptr(info),
-                                     P.stream_ptr()), "spd_inverse")
-    torch.cuda.synchronize()
-    assert int(info.abs().sum()) == 0
-    assert rel(Ai.cpu(), torch.linalg.inv(A)) < 1e-5
-    assert rel(logdet.cpu(), torch.logdet(A)) < 1e-6
 
 
 @pytest.mark.parametrize("n,L", [(256, 3), (512, 2), (768, 2), (1280, 2), (4096, 1)])
@@ -298,3 +241,234 @@ def test_relu_maxpool2_matches_torch(hip):
     ya.backward(g)
     yb.backward(g)
     assert torch.equal(xa.grad, xb.grad)
+
+
+def _random_hypers(k, L, rng, scale=(0.3, 1.5), ell=(1.0, 4.0)):
+    """[L, P] raw parameters: per-dim random scales and lengthscales (named_parameters order)."""
+    return np.stack([np.log(rng.uniform(*scale, L)) if "scale" in n else np.log(rng.uniform(*ell, L))
+                     for n, _ in k.named_parameters()], 1)
+
+
+def _kl_vs_oracle(P, L, raw, noise, seed, oracle_dev="cpu", dims_cpu=None, cfg=CFG, return_per_dim=False):
+    """HIP KL_closed_batched (values + all gradients) vs the fp64 oracle, per latent dim.
+    oracle_dev="cuda": the oracle's fp64 formula evaluated by PyTorch on the GPU (large N);
+    dims_cpu: dims additionally checked with the CPU oracle.  Returns the max relative errors."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    T = 16
+    X = torch.tensor(health_mnist_covariates(P, T, seed=seed))
+    gen = torch.Generator().manual_seed(seed)
+    mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    k = la.generate_kernel(**cfg, latent_dim=L).double()
+    set_raw(k, raw)
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    lik.noise = torch.as_tensor(noise, dtype=torch.float64)
+    mu_d, lv_d = mu.to(DEV).requires_grad_(), lv.to(DEV).requires_grad_()
+    kl = la.KL_closed_batched(kd, X.to(DEV), lik, mu_d, lv_d)
+    w = torch.arange(1, L + 1, device=DEV, dtype=torch.float64)
+    (kl * w).sum().backward()
+    draw = torch.stack([p.grad for _, p in kd.named_parameters()], 1)  # [L, P]
+    assert torch.isfinite(kl).all() and torch.isfinite(mu_d.grad).all() and torch.isfinite(draw).all()
+    spec = O.spec_full(**cfg)
+    nz = torch.as_tensor(noise, dtype=torch.float64).expand(L)
+    worst = dict(kl=0.0, dmu=0.0, dlogv=0.0, draw=0.0)
+    per_dim = {}
+    for dev, dims in ((oracle_dev, range(L)), ("cpu", dims_cpu or [])):
+        for l in dims:
+            r = torch.tensor(raw[l], device=dev, requires_grad=True)
+            m_ = mu[:, l].to(dev).clone().requires_grad_()
+            v_ = lv[:, l].to(dev).clone().requires_grad_()
+            ref = O.kl_closed(spec, O.constrain(r), X.to(dev), float(nz[l]), m_, v_)
+            ((l + 1) * ref).backward()
+            errs = dict(kl=rel(kl[l], ref), dmu=rel(mu_d.grad[:, l], m_.grad), dlogv=rel(lv_d.grad[:, l], v_.grad),
+                        draw=rel(draw[l], r.grad))
+            for key, e in errs.items():
+                worst[key] = max(worst[key], e)
+            per_dim.setdefault(l, {}).update({f"{dev}:{k}": v for k, v in errs.items()})
+    if return_per_dim:
+        return worst, per_dim
+    return worst
+
+
+def _cond(spec, raw, X, noise, dev=DEV):
+    K = O.gram(spec, O.constrain(torch.tensor(raw, device=dev)), X.to(dev), X.to(dev))
+    ev = torch.linalg.eigvalsh(K + noise * torch.eye(X.shape[0], dtype=torch.float64, device=dev))
+    return float(ev[-1] / ev[0])
+
+
+def test_kl_closed_headline_workload(hip):
+    """The bench's own workload: N = 4096 (P = 256 x T = 16), L = 16 batched, every dim with its own
+    random scales (0.3..1.5), lengthscales (1..4) and noise (0.5..1) around the sample config's init
+    (cond(K) up to ~1e4) -- KL and every gradient vs the fp64 oracle within the north-star 1e-4.  All
+    16 dims against the oracle formula run in fp64 on the GPU, dims 0 and 15 also on the CPU oracle."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    L, P = 16, 256
+    rng = np.random.default_rng(16)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    raw = _random_hypers(k, L, rng, scale=(0.3, 1.5), ell=(1.0, 4.0))
+    noise = torch.tensor(rng.uniform(0.5, 1.0, L))
+    worst, per = _kl_vs_oracle(P, L, raw, noise, seed=16, oracle_dev="cuda", dims_cpu=[0, 15], return_per_dim=True)
+    X = torch.tensor(health_mnist_covariates(P, 16, seed=16))
+    spec = O.spec_full(**CFG)
+    for l in range(L):
+        print(f"dim {l}: cond(K) {_cond(spec, raw[l], X, float(noise[l])):.2e}", per[l])
+    print("headline workload max rel errors:", worst)
+    for key, e in worst.items():
+        assert e < 1e-4, (key, e)
+
+
+def test_kl_closed_high_cond(hip):
+    """Wider hyper-parameter draws at N = 4096 (scales 0.2..3, lengthscales 0.5..6, noise 0.05..1:
+    cond(K) up to ~1e6).  fp32-equivalent arithmetic resolves K^-1 to ~cond(K) 2^-22 of its max
+    entry, so: the KL within 1e-4, and each dim's gradients within max(1e-4, 4 cond(K) 2^-22)
+    (per-dim cond from the fp64 eigenvalues) -- the measured errors are printed against that bound."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    L, P = 8, 256
+    rng = np.random.default_rng(17)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    raw = _random_hypers(k, L, rng, scale=(0.2, 3.0), ell=(0.5, 6.0))
+    noise = torch.tensor(rng.uniform(0.05, 1.0, L))
+    worst, per = _kl_vs_oracle(P, L, raw, noise, seed=17, oracle_dev="cuda", return_per_dim=True)
+    X = torch.tensor(health_mnist_covariates(P, 16, seed=17))
+    spec = O.spec_full(**CFG)
+    for l in range(L):
+        cond = _cond(spec, raw[l], X, float(noise[l]))
+        bound = max(1e-4, 4 * cond * 2.0 ** -22)
+        print(f"dim {l}: cond(K) {cond:.2e} bound {bound:.2e}", per[l])
+        assert per[l]["cuda:kl"] < 1e-4
+        for key in ("dmu", "dlogv", "draw"):
+            assert per[l][f"cuda:{key}"] < bound, (l, key)
+
+
+@pytest.mark.parametrize("noise", [1e-3, 1e-4])
+def test_kl_closed_small_noise(hip, noise):
+    """Small likelihood noise: K^-1 entries ~1/noise (1e3..1e4) would overflow an fp16 split with a
+    fixed scale; the per-(dim, pass) split scales keep the sweep finite and info == 0.  The fp32
+    result is then as good as fp32 allows: KL within max(1e-4, 20 cond(K) 2^-24) of the fp64 oracle
+    (cond measured on the fp64 K of the oracle)."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    L, P, T = 2, 64, 16
+    rng = np.random.default_rng(int(1 / noise))
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    raw = _random_hypers(k, L, rng)
+    X = torch.tensor(health_mnist_covariates(P, T, seed=3))
+    spec = O.spec_full(**CFG)
+    conds = []
+    for l in range(L):
+        K = O.gram(spec, O.constrain(torch.tensor(raw[l])), X, X) + noise * torch.eye(P * T, dtype=torch.float64)
+        ev = torch.linalg.eigvalsh(K)
+        conds.append(float(ev[-1] / ev[0]))
+    worst = _kl_vs_oracle(P, L, raw, noise, seed=3)
+    tol = max(1e-4, 20 * max(conds) * 2.0 ** -24)
+    print(f"noise {noise}: cond(K) {max(conds):.3e}, tol {tol:.2e}, errors {worst}")
+    assert worst["kl"] < tol and worst["dmu"] < tol and worst["dlogv"] < tol
+
+
+def test_kl_closed_c5_single_dim(hip):
+    """C5 shape (N = 16384: P = 1024 x T = 16), one latent dim, the reference kernel set: KL and all
+    gradients vs the oracle's fp64 formula evaluated on the GPU (a CPU fp64 inverse at this size takes
+    minutes).  Sweep error grows with N and cond(K); bound 1e-4."""
+    import lvae_amd as la
+    L, P = 1, 1024
+    rng = np.random.default_rng(1024)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    raw = _random_hypers(k, L, rng)
+    worst = _kl_vs_oracle(P, L, raw, 1.0, seed=1024, oracle_dev="cuda")
+    print("C5 single dim max rel errors:", worst)
+    for key, e in worst.items():
+        assert e < 1e-4, (key, e)
+
+
+C5_CFG_EXT = "RBF(time) + Cat(subject) + Per(time) + Lin(disease_time)"
+
+
+def _c5_kernel(L):
+    """The C5 stress kernel (BASELINE configs[4]): the sample config's R = 5 components plus the
+    periodic and linear extensions -- PARITY UNPINNED (no reference kernel; checked against the
+    oracle's own restatement only)."""
+    import lvae_amd as la
+    from lvae_amd.kernels import AdditiveKernel, LinearKernel, PeriodicKernel, ScaleKernel
+    base = la.generate_kernel(**CFG, latent_dim=L)
+    return AdditiveKernel(list(base.kernels) + [ScaleKernel(PeriodicKernel(0, L, 1.5, 6.0), L),
+                                                ScaleKernel(LinearKernel(1), L, scale=0.05)])
+
+
+def _c5_spec():
+    return O.spec_full(**CFG) + [[("per", 0)], [("lin", 1)]]
+
+
+@pytest.mark.parametrize("P,L,dev", [(16, 2, "cpu"), (64, 2, "cpu"), (1024, 1, "cuda")])
+def test_kl_closed_periodic_linear(hip, P, L, dev):
+    """Periodic + linear extension kernels (parity unpinned: the reference has neither) through the
+    exact KL: values and gradients (incl. period / lengthscale of the periodic factor) vs the oracle
+    restatement; N = 16384 (C5) on the GPU-evaluated fp64 oracle."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    T = 16
+    X = torch.tensor(health_mnist_covariates(P, T, seed=P))
+    gen = torch.Generator().manual_seed(P)
+    mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    k = _c5_kernel(L).double()
+    rng = np.random.default_rng(P)
+    with torch.no_grad():
+        for _, p in k.named_parameters():
+            p.add_(torch.tensor(rng.uniform(-0.3, 0.3, L)))
+    raw = torch.stack([p.detach().clone() for _, p in k.named_parameters()], 1)
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    mu_d, lv_d = mu.to(DEV).requires_grad_(), lv.to(DEV).requires_grad_()
+    kl = la.KL_closed_batched(kd, X.to(DEV), lik, mu_d, lv_d)
+    kl.sum().backward()
+    spec = _c5_spec()
+    for l in range(L):
+        r = raw[l].to(dev).clone().requires_grad_()
+        m_, v_ = mu[:, l].to(dev).clone().requires_grad_(), lv[:, l].to(dev).clone().requires_grad_()
+        ref = O.kl_closed(spec, O.constrain(r), X.to(dev), 1.0, m_, v_)
+        ref.backward()
+        assert rel(kl[l], ref) < 1e-4
+        assert rel(mu_d.grad[:, l], m_.grad) < 1e-4
+        assert rel(lv_d.grad[:, l], v_.grad) < 1e-4
+        assert rel(torch.stack([p.grad[l] for _, p in kd.named_parameters()]), r.grad) < 1e-4
+
+
+def test_closed_step_vs_oracle(hip):
+    """One full standard_training step with type_KL='closed' (training.py:484-592): ConvVAE forward /
+    backward over all N = 1024 images, the exact KL of L = 4 dims, the step composition
+    recon + weight * KL / L -- net, recon and KL terms plus the raw kernel-parameter and network
+    gradients vs oracle.closed_step (fp32 conv vs fp64 reference: 1e-4)."""
+    import lvae_amd as la
+    from lvae_amd.steps import ClosedStep
+    from lvae_amd.vae import ConvVAE
+    from lvae_amd.data import health_mnist_batch
+    L, P, T = 4, 64, 16
+    img, mask, X = health_mnist_batch(P, T, seed=8, dtype=torch.float64)
+    ref_vae = O.ConvVAE(L).double()
+    ref_vae.load_state_dict(O.vae_weights(ref_vae, 21))
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).double()
+    vae.load_state_dict(ref_vae.state_dict())
+    vae = vae.float().to(DEV)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    rng = np.random.default_rng(8)
+    set_raw(k, _random_hypers(k, L, rng))
+    raw = torch.stack([p.detach().clone() for _, p in k.named_parameters()], 1).requires_grad_()
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    eps = torch.randn(P * T, L, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
+    loss, recon, gp = O.closed_step(ref_vae, O.spec_full(**CFG), raw, torch.ones(L, dtype=torch.float64), img, mask,
+                                    X, eps, 0.15)
+    opt = torch.optim.SGD(list(vae.parameters()) + list(kd.parameters()), lr=0.0)
+    step = ClosedStep(vae, kd, lik, opt, weight=0.15, loss_function="mse")
+    net, rl, _, g = step(img.float().to(DEV), mask.float().to(DEV), X.to(DEV), eps.float().to(DEV))
+    assert rel(net, loss) < 1e-4
+    assert rel(rl, recon) < 1e-4
+    assert rel(g, gp) < 1e-4
+    assert rel(torch.stack([p.grad for _, p in kd.named_parameters()], 1), raw.grad) < 1e-4
+    for (name, p), (_, q) in zip(vae.named_parameters(), ref_vae.named_parameters()):
+        if q.grad is not None:  # (_log_vy has no gradient under loss='mse')
+            assert rel(p.grad, q.grad) < 1e-3, name
