@@ -1,13 +1,19 @@
-"""Benchmark: ELBO-steps/s of the L-VAE exact-KL training step (BASELINE.json configs[2]:
-Health-MNIST-shaped N=4096 observations (P=256 subjects x T=16), L=16 latent dims, one MI355X).
+"""Benchmark: ELBO-steps/s of the L-VAE training step (BASELINE.json: Health-MNIST N=4096, L=16).
 
-One step = full-batch ConvVAE forward/backward over the N images (fp32, PyTorch-ROCm) + the
-exact GP-prior KL of all L latent dims (HIP: Gram, blocked MFMA Cholesky, inverse, reductions)
-forward and backward + Adam (training.py:484-592, type_KL='closed', loss='mse').
+Headline (`value`): the exact-KL step of standard_training (type_KL='closed', loss='mse';
+training.py:484-592) at BASELINE configs[2] = N = 4096 observations (P = 256 subjects x T = 16),
+L = 16 latent dims: full-batch ConvVAE forward / backward (fp32, PyTorch-ROCm) + the exact GP-prior
+KL of all L dims forward and backward (HIP: Gram, block-sweep inverse, S GEMM, Gram adjoint) + Adam.
+  N = 1: one process.  N > 1: the SAME step (same objective, same N and L) with the latent dims
+  sharded over the ranks and the images split over them (lvae_amd.distributed.
+  LatentShardedClosedStep): strong scaling, value = whole-job ELBO-steps/s.
 
-Multi-GPU (torchrun, one process per GPU): data parallel over subject mini-batches -- every rank
-runs the step on its own N-observation batch of subjects, gradients all-reduced over RCCL; weak
-scaling, value = total ELBO-steps/s over all ranks.
+Sub-record `regime_a` (BASELINE configs[3], the path config/LVAE_config_sample.txt selects): the
+Hensman SVI step (training.py:90-140) at L = 16, M = 120, P_b = 5 subjects x T = 16 per rank, data
+parallel over subject mini-batches for N > 1 (weak scaling), replayed as HIP graphs.
+
+Sub-record `c2` (BASELINE configs[1], N = 1 only): HIP Gram + sweep inverse + log-det vs PyTorch-ROCm
+Gram + torch.linalg.cholesky (+ cholesky_inverse) at N = 1024, L = 8.
 
 Prints ONE JSON line on rank 0 (the driver's contract); diagnostics go to stderr.
 """
@@ -15,6 +21,8 @@ import argparse
 import json
 import math
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -30,41 +38,39 @@ CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
                            {'cont_covariate': 0, 'cat_covariate': 3},
                            {'cont_covariate': 1, 'cat_covariate': 4}],
            bin_int_kernel=[], covariate_missing_val=[])
-FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense f16/bf16 MFMA peak (~2.5 PF, no sparsity)
 X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product (mfma_x3.hpp)
-# Memory-side bytes per syrk launch from the committed rocprofv3 PMC passes (scripts/pmc.sh ->
-# profiles/r1_v6_pmc_summary.json: FETCH_SIZE / WRITE_SIZE in KiB per dispatch; FETCH_SIZE x 2 for
-# 16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM").  Counts L2 misses incl.
-# Infinity-Cache hits, so it bounds HBM traffic from above.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_v7_pmc_summary.json")
-
-
-def pmc_traffic(kernels):
-    """Sum over the named kernels (one dispatch each per step) of FETCH_SIZE x 2 + WRITE_SIZE, bytes."""
-    try:
-        d = json.load(open(PMC_SUMMARY))
-        tot = 0.0
-        for name in kernels:
-            f = [v["mean"] for k, v in d["FETCH_SIZE"].items() if name in k]
-            w = [v["mean"] for k, v in d["WRITE_SIZE"].items() if name in k]
-            if not (f and w):
-                return None
-            tot += (2 * f[0] + w[0]) * 1024
-        return tot
-    except (OSError, KeyError, ValueError):
-        return None
-HBM_PEAK_GBS = 8000.0
+DTYPE = "f16x3-split (fp32-equivalent)"
+# Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
+# FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2_pmc_summary.json")
+U2_NAME = "sw_update_kernel<false,"      # the sweep's rank-256 update U2 (spd_sweep.hip)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def setup_dist(ngpu):
+def pmc_traffic(kernels):
+    """Sum over the named kernels (one dispatch each) of FETCH_SIZE x 2 + WRITE_SIZE, bytes."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+        tot = 0.0
+        for name in kernels:
+            f = [v["mean"] for k, v in d["FETCH_SIZE"].items() if name in k.replace(" ", "")]
+            w = [v["mean"] for k, v in d["WRITE_SIZE"].items() if name in k.replace(" ", "")]
+            if not (f and w):
+                return None
+            tot += (2 * f[0] + w[0]) * 1024
+        return tot
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def setup_dist():
     """One process per GPU (torchrun env).  Returns (world, rank, device index).  RCCL ("nccl") by
-    default; LVAE_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on fewer GPUs
-    (device = LOCAL_RANK mod the visible GPU count)."""
+    default; LVAE_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on fewer GPUs."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -82,177 +88,89 @@ def setup_dist(ngpu):
     return world, rank, dev
 
 
-def cpu_baseline(P, T, L, dims_timed=1):
-    """Time the CPU oracle (fp64 torch, the reference's op sequence) on a bounded sample of the same
-    step: ConvVAE fwd/bwd on all N images + KL_closed fwd/bwd of `dims_timed` latent dims, then
-    extrapolate the KL part to L dims."""
+def host_info():
+    """lscpu model / sockets / physical cores, and the NUMA node of GPU0 if sysfs shows it."""
+    info = {"threads_used": torch.get_num_threads(), "os_cpu_count": os.cpu_count(), "machine": platform.machine()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {k.strip(): v.strip() for k, v in (ln.split(":", 1) for ln in out.splitlines() if ":" in ln)}
+        info["model"] = kv.get("Model name")
+        info["sockets"] = kv.get("Socket(s)")
+        info["cores_per_socket"] = kv.get("Core(s) per socket")
+        info["threads_per_core"] = kv.get("Thread(s) per core")
+    except (OSError, subprocess.SubprocessError, ValueError):
+        pass
+    try:
+        import glob
+        for p in sorted(glob.glob("/sys/class/drm/card*/device/numa_node")):
+            info["gpu0_numa_node"] = int(open(p).read().strip())
+            break
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def sync_barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baselines (the oracle, fp64 torch-CPU, the reference's op sequence) -- rank 0, N = 1 only
+# ------------------------------------------------------------------------------------------
+def cpu_baseline_closed(P, T, L, threads8_dims=1):
+    """All L latent dims of the C3 step: ConvVAE fwd/bwd on all N images + KL_closed fwd/bwd of
+    every dim (fp64), timed once at the box's thread count; plus an 8-thread figure (ConvVAE + one
+    dim, extrapolated to L dims) for comparison with the survey container's numbers."""
     from oracle import lvae_oracle as O
     from lvae_amd.data import health_mnist_batch
     img, mask, X = health_mnist_batch(P, T, seed=0, dtype=torch.float64)
     torch.manual_seed(0)
     vae = O.ConvVAE(L).double()
     spec = O.spec_full(**CFG)
-    raw = torch.zeros(L, O.n_params(spec), dtype=torch.float64)
-    raw[:, :] = torch.log(torch.tensor(math.log(2.0)))
+    raw = torch.full((L, O.n_params(spec)), math.log(math.log(2.0)), dtype=torch.float64)
     N = P * T
     eps = torch.randn(N, L, dtype=torch.float64)
-    t0 = time.perf_counter()
-    mu, logv = vae.encode(img)
-    recon = vae.decode(mu + eps * torch.exp(0.5 * logv))
-    mse, _ = vae.loss_function(recon, img, mask)
-    mse.sum().backward(retain_graph=True)
-    t_vae = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    for l in range(dims_timed):
-        r = raw[l].clone().requires_grad_()
-        m_ = mu[:, l].detach().clone().requires_grad_()
-        v_ = logv[:, l].detach().clone().requires_grad_()
-        O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_).backward()
-    t_dim = (time.perf_counter() - t0) / dims_timed
-    t_step = t_vae + L * t_dim
-    return dict(value=1.0 / t_step, unit="ELBO-steps/s", cores=torch.get_num_threads(), kind="port",
-                sample=(f"oracle fp64 torch-CPU: ConvVAE fwd/bwd on all {N} images ({t_vae:.2f} s) + KL_closed "
-                        f"fwd/bwd of {dims_timed} of {L} latent dims ({t_dim:.2f} s/dim), step = vae + L x dim "
-                        f"= {t_step:.1f} s"))
 
+    def step(dims):
+        t0 = time.perf_counter()
+        mu, logv = vae.encode(img)
+        recon = vae.decode(mu + eps * torch.exp(0.5 * logv))
+        mse, _ = vae.loss_function(recon, img, mask)
+        mse.sum().backward(retain_graph=True)
+        t_vae = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for l in range(dims):
+            r = raw[l].clone().requires_grad_()
+            m_ = mu[:, l].detach().clone().requires_grad_()
+            v_ = logv[:, l].detach().clone().requires_grad_()
+            O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_).backward()
+        return t_vae, time.perf_counter() - t0
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--P", type=int, default=256, help="subjects per rank (N = P*T)")
-    ap.add_argument("--T", type=int, default=16)
-    ap.add_argument("--L", type=int, default=16)
-    ap.add_argument("--regime", choices=["closed", "hensman"], default="closed",
-                    help="closed: exact-KL step (headline, configs[2]); hensman: SVI mini-batch step (configs[3])")
-    ap.add_argument("--P_b", type=int, default=5, help="hensman: subjects per batch per rank")
-    ap.add_argument("--M", type=int, default=120, help="hensman: inducing points")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-phase-timing", action="store_true")
-    args = ap.parse_args()
-
-    world, rank, local = setup_dist(args.gpus)
-    if args.regime == "hensman":
-        return main_hensman(args, world, rank, local)
-    dev = torch.device("cuda", local)
-    import lvae_amd as la
-    from lvae_amd import _lib
-    from lvae_amd.data import health_mnist_batch
-    from lvae_amd.steps import ClosedStep
-    from lvae_amd.vae import ConvVAE
-
-    la.set_sync_checks(False)
-    P, T, L = args.P, args.T, args.L
-    N = P * T
-    torch.manual_seed(1234)  # identical initial weights on every rank
-    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(dev)
-    kernel = la.generate_kernel(**CFG, latent_dim=L).to(dev)
-    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(dev)
-    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3)
-    img, mask, X = health_mnist_batch(P, T, seed=100 + rank, device=dev)
-    gen = torch.Generator(device=dev).manual_seed(7 + rank)
-    eps = torch.randn(N, L, device=dev, generator=gen)
-
-    hook = None
-    if world > 1:
-        from lvae_amd.distributed import GradAllReduce
-        hook = GradAllReduce(list(vae.parameters()) + list(kernel.parameters()), world)
-    step = ClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True,
-                      grad_hook=hook)
-
-    for _ in range(args.warmup):
-        out = step(img, mask, X, eps)
-    torch.cuda.synchronize()
-    la.check_pending()
-
-    phase = {}
-    if not args.no_phase_timing:
-        _lib.prof_enable(True)
-        _lib.prof_collect()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step(img, mask, X, eps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if not args.no_phase_timing:
-        phase = _lib.prof_collect()
-        _lib.prof_enable(False)
-    la.check_pending()
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    net, recon, nll, gp = [float(v) for v in out]
-    log(f"rank {rank}: last step net={net:.4f} recon={recon:.4f} gp={gp:.4f}; phases(ms total over {args.steps} "
-        f"steps)={ {k: round(v[0], 3) for k, v in phase.items() if v[1]} }")
-
-    if rank == 0:
-        ms_per_step = 1000.0 * elapsed / args.steps
-        value = world * args.steps / elapsed
-        np_ = _lib.load().lvae_kl_closed_padded_n(N)
-        res = {"metric": "ELBO-steps/sec (exact-KL L-VAE step, Health-MNIST N=4096 L=16)", "value": value,
-               "unit": "ELBO-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-               "dtype": "fp32", "data": "synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)",
-               "config": {"workload": f"closed-form KL step, N={N} (P={P} subjects x T={T}) per rank, L={L}, "
-                                      f"R=5 additive components (config/LVAE_config_sample.txt)",
-                          "N": N, "L": L, "parallelism": f"dp{world} over subject batches"}}
-        if phase:
-            potrf_ms = phase["potrf"][0] / args.steps
-            syrk_ms = phase["syrk"][0] / args.steps
-            res["gp_cholesky_gflops"] = L * N ** 3 / 3 / (potrf_ms * 1e-3) / 1e9 if potrf_ms > 0 else None
-            res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
-            # dominant kernel: the sweep's rank-256 update U2 (sw_update_kernel<false, false>, nt - 1
-            # launches per step, 31% of the step's GPU time).  Algorithmic bytes per launch: every
-            # updated lower 256-tile is read and written once in fp32 -> 2 x 4 B x 256^2 per tile,
-            # (nt-1) nt / 2 - 1 tiles per dim (the grid without row / column k and tile (k+1, k+1)),
-            # x L.  The W / C operand planes are L2-resident re-reads, not algorithmic traffic.
-            nt = np_ // 256
-            upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
-            tiles = ((nt - 1) * nt // 2 - 1) * L
-            upd_bytes = 2 * 4 * 256 * 256 * tiles
-            if upd_n and np_ % 256 == 0:
-                avg_s = upd_ms / upd_n * 1e-3
-                ach = upd_bytes / avg_s / 1e9
-                res["roofline"] = {"kernel": "sw_update_kernel<false, false> (sweep rank-256 update U2, spd_sweep.hip)",
-                                   "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": ach / HBM_PEAK_GBS,
-                                   "traffic": pmc_traffic(("sw_update_kernel<false, false",)),
-                                   "algorithmic_bytes_per_launch": upd_bytes, "avg_launch_us": avg_s * 1e6,
-                                   "launches_per_step": upd_n / args.steps, "padded_n": int(np_)}
-            # secondary: S = K^-1 V K^-1, the largest single launch (one per step).  Algorithmic flops
-            # = L * N^2 (N+1) (lower triangle incl. diagonal, 2 flop/FMA).  Engine: 3-product f16
-            # split -> the f16 dense peak / 3 (each fp32 FMA costs three f16 MFMA FMAs).
-            flops = L * np_ * np_ * (np_ + 1)
-            achieved = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
-            fast_syrk = np_ % 256 == 0 and not int(os.environ.get("LVAE_SYRK_GENERIC", "0"))
-            x3 = fast_syrk or bool((_lib.load().lvae_gemm_engine_mask() >> 5) & 1)
-            peak = F16_MFMA_PEAK_TFLOPS / X3_PRODUCTS if x3 else FP32_MFMA_PEAK_TFLOPS
-            syrk_line = {"kernel": "syrk_split_kernel + syrk_x3_kernel (S = K^-1 V K^-1)" if fast_syrk
-                         else "syrk_scaled_kernel (S = K^-1 V K^-1)", "bound": "mfma",
-                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": (achieved / peak) if achieved else None,
-                         "traffic": pmc_traffic(("syrk_x3_kernel", "syrk_split_kernel") if fast_syrk else
-                                                ("syrk_scaled_kernel<true>" if x3 else "syrk_scaled_kernel<false>",)),
-                         "padded_n": int(np_),
-                         "engine": ("f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)" if x3
-                                    else "fp32-input MFMA")}
-            if "roofline" in res:
-                res["roofline_secondary"] = syrk_line
-            else:
-                res["roofline"] = syrk_line
-        if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(P, T, L)
-            res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    nthreads = torch.get_num_threads()
+    t_vae, t_kl = step(L)
+    t_step = t_vae + t_kl
+    res = dict(value=1.0 / t_step, unit="ELBO-steps/s", cores=nthreads, kind="port",
+               sample=(f"oracle fp64 torch-CPU, {nthreads} threads: ConvVAE fwd/bwd on all {N} images ({t_vae:.2f} s) "
+                       f"+ KL_closed fwd/bwd of all {L} latent dims ({t_kl:.2f} s) = {t_step:.1f} s per step"))
+    try:
+        torch.set_num_threads(8)
+        v8, k8 = step(threads8_dims)
+        res["threads8"] = {"value": 1.0 / (v8 + L * k8 / threads8_dims), "unit": "ELBO-steps/s",
+                           "sample": f"8 threads: ConvVAE {v8:.2f} s + {threads8_dims} dim(s) {k8:.2f} s, x{L} dims"}
+    finally:
+        torch.set_num_threads(nthreads)
+    res["host"] = host_info()
+    return res
 
 
 def cpu_baseline_hensman(P, T, L, M, P_b, steps=12):
@@ -263,8 +181,8 @@ def cpu_baseline_hensman(P, T, L, M, P_b, steps=12):
     torch.manual_seed(0)
     vae = O.ConvVAE(L).double()
     s0, s1 = O.spec_split(**CFG, id_covariate=2)
-    raw0 = torch.full((L, O.n_params(s0)), math.log(2.0), dtype=torch.float64, requires_grad=True)
-    raw1 = torch.full((L, O.n_params(s1)), math.log(2.0), dtype=torch.float64, requires_grad=True)
+    raw0 = torch.full((L, O.n_params(s0)), math.log(math.log(2.0)), dtype=torch.float64, requires_grad=True)
+    raw1 = torch.full((L, O.n_params(s1)), math.log(math.log(2.0)), dtype=torch.float64, requires_grad=True)
     N = P * T
     z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
     m = torch.zeros(L, M, 1, dtype=torch.float64)
@@ -286,14 +204,116 @@ def cpu_baseline_hensman(P, T, L, M, P_b, steps=12):
                        f"{steps - 2} steps after 2 warm-up: {1000 * t:.1f} ms/step")
 
 
-def main_hensman(args, world, rank, local):
-    """Hensman SVI training steps (training.py:91-135), data parallel over subject mini-batches."""
-    dev = torch.device("cuda", local)
+# ------------------------------------------------------------------------------------------
+# Regime B: the headline exact-KL step
+# ------------------------------------------------------------------------------------------
+def run_closed(args, world, rank, dev):
     import lvae_amd as la
     from lvae_amd import _lib
     from lvae_amd.data import health_mnist_batch
+    from lvae_amd.steps import ClosedStep
+    from lvae_amd.distributed import LatentShardedClosedStep, shard_bounds
+    from lvae_amd.vae import ConvVAE
+
+    la.set_sync_checks(False)
+    P, T, L = args.P, args.T, args.L
+    N = P * T
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(dev)
+    kernel = la.generate_kernel(**CFG, latent_dim=L).to(dev)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(dev)
+    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3)
+    img, mask, X = health_mnist_batch(P, T, seed=100, device=dev)   # the same data set on every rank
+    gen = torch.Generator(device=dev).manual_seed(7)
+    eps = torch.randn(N, L, device=dev, generator=gen)
+    if world > 1:
+        lo, hi = shard_bounds(N, world, rank)
+        step = LatentShardedClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True)
+        inputs = (img[lo:hi].contiguous(), mask[lo:hi].contiguous(), X, eps[lo:hi].contiguous())
+        d0, d1 = shard_bounds(L, world, rank)
+    else:
+        step = ClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True)
+        inputs = (img, mask, X, eps)
+        d0, d1 = 0, L
+
+    for _ in range(args.warmup):
+        out = step(*inputs)
+    torch.cuda.synchronize()
+    la.check_pending()
+    if not args.no_phase_timing:
+        _lib.prof_enable(True)
+        _lib.prof_collect()
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step(*inputs)
+    sync_barrier(world)
+    elapsed = time.perf_counter() - t0
+    phase = {}
+    if not args.no_phase_timing:
+        phase = _lib.prof_collect()
+        _lib.prof_enable(False)
+    la.check_pending()
+    elapsed = max_over_ranks(elapsed, world, dev)
+    net, recon, nll, gp = [float(v) for v in out]
+    log(f"rank {rank}: dims [{d0},{d1}) last step net={net:.4f} recon={recon:.4f} gp={gp:.4f}; "
+        f"phases(ms over {args.steps} steps)={ {k: round(v[0], 3) for k, v in phase.items() if v[1]} }")
+    Lr = d1 - d0
+    res = {"metric": "ELBO-steps/sec (exact-KL L-VAE step, Health-MNIST N=4096 L=16)",
+           "value": args.steps / elapsed, "unit": "ELBO-steps/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+           "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": DTYPE,
+           "data": "synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)",
+           "config": {"workload": f"closed-form KL step (standard_training, type_KL='closed'): N={N} (P={P} subjects "
+                                  f"x T={T}), L={L}, R=5 additive components (config/LVAE_config_sample.txt)",
+                      "N": N, "L": L,
+                      "parallelism": ("single GPU" if world == 1 else
+                                      f"latent dims sharded over {world} ranks ({Lr} dims/rank on rank 0), images "
+                                      f"split {N // world}/rank, 1 all-gather + 2 all-reduces per step")}}
+    if phase and Lr > 0:
+        np_ = _lib.load().lvae_kl_closed_padded_n(N)
+        inv_ms = phase["potrf"][0] / args.steps
+        syrk_ms = phase["syrk"][0] / args.steps
+        res["gp_cholesky_gflops"] = Lr * N ** 3 / 3 / (inv_ms * 1e-3) / 1e9 if inv_ms > 0 else None
+        res["gp_cholesky_gflops_basis"] = (f"L*N^3/3 (the LAPACK potrf count, SURVEY.md §8(d)) / time of the whole "
+                                           f"inverse phase (block-sweep K^-1 + log|K|, {inv_ms:.2f} ms/step on rank 0)")
+        res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
+        # dominant kernel: the sweep's rank-256 update U2 (nt - 1 launches per step).  Algorithmic
+        # bytes per launch: every updated lower 256-tile read and written once in fp32 -> 2 x 4 B x
+        # 256^2 per tile, ((nt-1) nt / 2 - 1) tiles per dim, x the dims of this rank.
+        nt = np_ // 256
+        upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
+        tiles = ((nt - 1) * nt // 2 - 1) * Lr
+        upd_bytes = 2 * 4 * 256 * 256 * tiles
+        if upd_n:
+            avg_s = upd_ms / upd_n * 1e-3
+            ach = upd_bytes / avg_s / 1e9
+            res["roofline"] = {"kernel": "sw_update_kernel<false, 2> (sweep rank-256 update U2, spd_sweep.hip)",
+                               "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic((U2_NAME,)) if world == 1 else None,
+                               "algorithmic_bytes_per_launch": upd_bytes, "avg_launch_us": avg_s * 1e6,
+                               "launches_per_step": upd_n / args.steps, "padded_n": int(np_)}
+        # secondary: S = K^-1 V K^-1 (one launch per step): L N^2 (N+1) flop (lower triangle incl.
+        # the diagonal); engine: 3-product f16 split -> the f16 dense peak / 3
+        flops = Lr * np_ * np_ * (np_ + 1)
+        ach = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
+        peak = F16_MFMA_PEAK_TFLOPS / X3_PRODUCTS
+        res["roofline_secondary"] = {"kernel": "syrk_split_kernel + syrk_x3_kernel (S = K^-1 V K^-1)", "bound": "mfma",
+                                     "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                                     "frac": (ach / peak) if ach else None,
+                                     "traffic": pmc_traffic(("syrk_x3_kernel", "syrk_split_kernel")) if world == 1 else None,
+                                     "engine": "f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)"}
+    return res
+
+
+# ------------------------------------------------------------------------------------------
+# Regime A: Hensman SVI step, HIP-graph replayed
+# ------------------------------------------------------------------------------------------
+def run_hensman(args, world, rank, dev):
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_batch
     from lvae_amd.samplers import hensman_batches, SubjectSampler
-    from lvae_amd.steps import HensmanStep
+    from lvae_amd.steps import GraphedStep, HensmanStep
     from lvae_amd.vae import ConvVAE
 
     la.set_sync_checks(False)
@@ -310,7 +330,7 @@ def main_hensman(args, world, rank, local):
         H = k0(z, z).evaluate() + 1e-6 * torch.eye(M, dtype=torch.float64, device=dev)
     m = torch.zeros(L, M, 1, dtype=torch.float64, device=dev)
     opt = torch.optim.Adam([{"params": k0.parameters()}, {"params": k1.parameters()},
-                            {"params": vae.parameters()}], lr=1e-3)
+                            {"params": vae.parameters()}], lr=1e-3, capturable=True)
     hook = ngr = None
     if world > 1:
         from lvae_amd.distributed import GradAllReduce, allreduce_tensors
@@ -322,54 +342,161 @@ def main_hensman(args, world, rank, local):
     batches = [b.to(dev) for b in hensman_batches(perm, P_b, T, rank, world) if b is not None and len(b) == P_b * T]
     gen = torch.Generator(device=dev).manual_seed(7 + rank)
     eps = torch.randn(P_b * T, L, device=dev, generator=gen)
+    rows = batches[0].clone()
+    s_img, s_mask, s_X = img.index_select(0, rows), mask.index_select(0, rows), X.index_select(0, rows)
 
-    def run(n):
-        out = None
-        for i in range(n):
-            rows = batches[i % len(batches)]
-            out = step(img.index_select(0, rows), mask.index_select(0, rows), X.index_select(0, rows), eps)
-        return out
+    def load(i):  # next batch into the static inputs (device gathers, no host sync)
+        r = batches[i % len(batches)]
+        torch.index_select(img, 0, r, out=s_img)
+        torch.index_select(mask, 0, r, out=s_mask)
+        torch.index_select(X, 0, r, out=s_X)
 
-    run(args.warmup)
+    graphed = GraphedStep(step, (s_img, s_mask, s_X, eps), warmup=max(args.warmup, 2))
+    for i in range(args.warmup):
+        load(i)
+        graphed()
     torch.cuda.synchronize()
-    la.check_pending()
-    if not args.no_phase_timing:
-        _lib.prof_enable(True)
-        _lib.prof_collect()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    graphed.check()
+    sync_barrier(world)
     t0 = time.perf_counter()
-    out = run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    phase = {}
-    if not args.no_phase_timing:
-        phase = _lib.prof_collect()
-        _lib.prof_enable(False)
-    la.check_pending()
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    log(f"rank {rank}: last step (net, recon, nll, kld) = {[round(float(v), 4) for v in out]}")
+    for i in range(args.h_steps):
+        load(i)
+        out = graphed()
+    sync_barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    graphed.check()
+    log(f"rank {rank}: Hensman last step (net, recon, nll, kld) = {[round(float(v), 4) for v in out]}")
+    value = args.h_steps / elapsed
+    return {"metric": "ELBO-steps/sec (Hensman SVI step, training.py:90-140)", "value": value,
+            "unit": "ELBO-steps/s", "ms_per_step": 1000.0 * elapsed / args.h_steps, "steps": args.h_steps,
+            "samples_per_sec": value * world * P_b * T, "scaling": "weak",
+            "dtype": "fp64 GP (f64 MFMA / VALU) + fp32 ConvVAE",
+            "config": {"workload": f"Hensman step: P_tot={P} subjects x T={T} (N={N}), L={L}, M={M}, P_b={P_b} "
+                                   f"subjects per rank per step, natural gradient, one HIP graph per step"
+                                   + (" (two around the all-reduces)" if world > 1 else ""),
+                       "parallelism": f"dp{world} over subject mini-batches"}}
+
+
+# ------------------------------------------------------------------------------------------
+# C2: HIP Gram + inverse vs PyTorch-ROCm Gram + torch.linalg.cholesky (N = 1024, L = 8)
+# ------------------------------------------------------------------------------------------
+def torch_gram_f32(params, X):
+    """The sample-config additive Gram (+ noise = 1 on the diagonal) in plain PyTorch fp32 ops."""
+    x = X.to(torch.float32)
+    t, dt, subj, gen, dis = x[:, 0], x[:, 1], x[:, 2], x[:, 3], x[:, 4]
+    p = params.to(torch.float32)[:, :, None, None]
+    rbf = lambda a, ell: torch.exp(-(a[:, None] - a[None, :]) ** 2 / (2 * ell ** 2))
+    cat = lambda a: (a[:, None] == a[None, :]).to(torch.float32)
+    K = (p[:, 0] * cat(subj) + p[:, 1] * rbf(t, p[:, 2]) + p[:, 3] * cat(subj) * rbf(t, p[:, 4])
+         + p[:, 5] * cat(gen) * rbf(t, p[:, 6]) + p[:, 7] * cat(dis) * rbf(dt, p[:, 8]))
+    return K + torch.eye(x.shape[0], device=x.device)
+
+
+def run_c2(dev, reps=20):
+    import lvae_amd as la
+    from lvae_amd import _lib
+    from lvae_amd.data import health_mnist_covariates
+    P, T, L = 64, 16, 8
+    N = P * T
+    X = torch.tensor(health_mnist_covariates(P, T, seed=2), device=dev)
+    k = la.generate_kernel(**CFG, latent_dim=L).to(dev)
+    spec, params = la.kernel_spec_and_params(k)
+    params = params.detach().contiguous()
+    lib = _lib.load()
+    np_ = lib.lvae_kl_closed_padded_n(N)
+    A = torch.empty(L, np_, np_, dtype=torch.float32, device=dev)
+    Kinv = torch.empty_like(A)
+    scr = torch.empty(int(lib.lvae_spd_sweep_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
+    logdet = torch.empty(L, dtype=torch.float64, device=dev)
+    info = torch.empty(L, dtype=torch.int32, device=dev)
+    noise = torch.ones(L, dtype=torch.float64, device=dev)
+    xv = _lib.xview(X, 0, 0)
+
+    def hip():
+        _lib.check(lib.lvae_gram_f32(spec, xv, xv, 1, L, N, N, _lib.ptr(params), _lib.ptr(noise), _lib.ptr(A), 0,
+                                     np_ * np_, np_, _lib.stream_ptr()), "gram")
+        _lib.check(lib.lvae_spd_sweep_f32(np_, L, _lib.ptr(A), _lib.ptr(scr), _lib.ptr(Kinv), _lib.ptr(logdet),
+                                          _lib.ptr(info), _lib.stream_ptr()), "sweep")
+
+    def torch_chol():
+        Lc = torch.linalg.cholesky(torch_gram_f32(params, X))
+        return Lc
+
+    def torch_chol_inv():
+        Lc = torch_chol()
+        return torch.cholesky_inverse(Lc), 2 * torch.log(torch.diagonal(Lc, dim1=-2, dim2=-1)).sum(-1)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    t_hip, t_chol, t_inv = timed(hip), timed(torch_chol), timed(torch_chol_inv)
+    ref_inv, ref_ld = torch_chol_inv()
+    err = float((Kinv[:, :N, :N] - ref_inv).abs().max() / ref_inv.abs().max())
+    flop = L * N ** 3 / 3
+    return {"config": f"N={N} (P={P} x T={T}), L={L}, sample-config kernel, fp32",
+            "hip_gram_sweep_inverse_ms": t_hip, "torch_gram_cholesky_ms": t_chol,
+            "torch_gram_cholesky_inverse_ms": t_inv,
+            "speedup_vs_torch_cholesky": t_chol / t_hip, "speedup_vs_torch_cholesky_inverse": t_inv / t_hip,
+            "gp_cholesky_gflops_hip": flop / (t_hip * 1e-3) / 1e9,
+            "gp_cholesky_gflops_torch": flop / (t_chol * 1e-3) / 1e9,
+            "hip_vs_torch_inverse_max_rel_diff": err,
+            "logdet_max_rel_diff": float(((logdet.float() - ref_ld).abs() / ref_ld.abs()).max()),
+            "note": "HIP: lvae_gram_f32 + lvae_spd_sweep_f32 (K^-1 and log|K|); torch: PyTorch fp32 Gram + "
+                    "torch.linalg.cholesky (rocSOLVER) [+ cholesky_inverse + log-det for the same outputs]"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--P", type=int, default=256, help="subjects (N = P*T)")
+    ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--L", type=int, default=16)
+    ap.add_argument("--P_b", type=int, default=5, help="Regime A: subjects per batch per rank")
+    ap.add_argument("--M", type=int, default=120, help="Regime A: inducing points")
+    ap.add_argument("--h-steps", dest="h_steps", type=int, default=100, help="Regime A timed steps")
+    ap.add_argument("--regime", choices=["both", "closed", "hensman"], default="both")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-phase-timing", action="store_true")
+    ap.add_argument("--no-c2", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = setup_dist()
+    dev = torch.device("cuda", local)
+    res = None
+    if args.regime in ("both", "closed"):
+        res = run_closed(args, world, rank, dev)
+    if args.regime in ("both", "hensman"):
+        ra = run_hensman(args, world, rank, dev)
+        if res is None:
+            res = dict(ra, n_gpus=world, warmup=args.warmup, higher_is_better=True, vs_baseline=None,
+                       data="synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)")
+        else:
+            res["regime_a"] = ra
     if rank == 0:
-        value = world * args.steps / elapsed
-        res = {"metric": "ELBO-steps/sec (Hensman SVI L-VAE step, Health-MNIST N=4096 L=16)", "value": value,
-               "unit": "ELBO-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "fp64 GP / fp32 conv",
-               "data": "synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)",
-               "config": {"workload": f"Hensman step: P_tot={P} subjects x T={T} (N={N}), L={L}, M={M}, "
-                                      f"P_b={P_b} subjects per rank per step",
-                          "samples_per_sec": value * P_b * T, "parallelism": f"dp{world} over subject batches"}}
-        if phase:
-            res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
-        if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline_hensman(P, T, L, M, P_b)
-            res["vs_cpu_baseline"] = value / world / res["cpu_baseline"]["value"]
+        if world == 1 and not args.no_c2 and args.regime != "hensman":
+            res["c2"] = run_c2(dev)
+        if world == 1 and not args.no_cpu_baseline:
+            if args.regime in ("both", "closed"):
+                res["cpu_baseline"] = cpu_baseline_closed(args.P, args.T, args.L)
+                res["vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]
+            if args.regime in ("both", "hensman"):
+                cb = cpu_baseline_hensman(args.P, args.T, args.L, args.M, args.P_b)
+                ra = res["regime_a"] if "regime_a" in res else res
+                ra["cpu_baseline"] = cb
+                ra["vs_cpu_baseline"] = ra["value"] / cb["value"]
+                if "regime_a" not in res:
+                    res["vs_cpu_baseline"] = ra["vs_cpu_baseline"]
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -88,10 +88,13 @@ int lvae_gram_f32(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, in
 
 /* Adjoint of lvae_gram_*: dparams[l, p] (+)= sum_{b,i,j} G[b,l,i,j] * d out[b,l,i,j] / d params[l,p]
  * (diag term excluded; d/d diag is returned separately in ddiag[l] = sum_{b,i} G[b,l,i,i] when
- * ddiag != NULL).  G strided like out.  Results are ADDED to dparams / ddiag (fp64). */
+ * ddiag != NULL).  G strided like out.  Results are ADDED to dparams / ddiag (fp64), in a fixed
+ * order (deterministic).  workspace: lvae_gram_bwd_workspace_size(nb, L, n1, n2) bytes.        */
+size_t lvae_gram_bwd_workspace_size(int nb, int L, int n1, int n2);
 int lvae_gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1,
                       int n2, const double* params, const double* G, int64_t gstride_b,
-                      int64_t gstride_l, int64_t ldg, double* dparams, double* ddiag, void* stream);
+                      int64_t gstride_l, int64_t ldg, double* dparams, double* ddiag, void* workspace,
+                      void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Regime B: exact KL over the full N x N covariance (elbo_functions.py:8-34), batched over L */

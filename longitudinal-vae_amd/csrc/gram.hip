@@ -4,7 +4,7 @@
 // covariate row blocks are staged in LDS (coalesced fp64 reads of the [n, Q] index arrays), each
 // thread produces 16 elements of one column (consecutive lanes -> consecutive columns, so the
 // stores are coalesced).  The Gram is HBM-write-bound: per element 4 B (f32) / 8 B (f64) out.
-#include "common.hpp"
+#include "gram_bwd.hpp"
 
 namespace lvae {
 
@@ -45,18 +45,34 @@ __global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lva
   }
 }
 
-// Adjoint, generic strided G (fp64): one workgroup per latent dim (deterministic; the
-// Hensman-sized Grams are a few 10^4 elements), accumulating per-slot sums then reducing.
+// Adjoint, generic strided G (fp64), several Grams in one launch (the Hensman backward contracts
+// four: K0xz, K0zz, K0_p with spec0 and B_p with spec1).  Stage 1: grid (chunks over all jobs, L),
+// each workgroup takes kGBChunk consecutive elements of one job's [nb, n1, n2] G, accumulates the
+// per-slot sums of g dk/dparam in registers, reduces them over its waves, and writes one partial
+// row part[l][chunk][slot] (slot NS-1: sum of the diagonal of G, the noise adjoint).  Stage 2: one
+// workgroup per latent dim sums the chunks of every (job, slot) and adds them to the job's dparams /
+// ddiag in a fixed order -- deterministic, and no single-workgroup loop over the whole Gram.
+constexpr int kGBMaxJobs = 4;
+constexpr int kGBChunk = 1024;  // elements per workgroup (4 per thread)
+
+
+struct GramBwdJobs {
+  DevSpec s[2];
+  GramBwdJob j[kGBMaxJobs];
+  int njobs, total_chunks;
+};
+
 template <int MC, int MF>
-__global__ __launch_bounds__(256) void gram_bwd_kernel(DevSpec s, lvae_xview x1, lvae_xview x2, int nb, int L,
-                                                       int n1, int n2, const double* __restrict__ params,
-                                                       const double* __restrict__ G, int64_t gsb, int64_t gsl,
-                                                       int64_t ldg, double* __restrict__ dparams,
-                                                       double* __restrict__ ddiag) {
+__global__ __launch_bounds__(256) void gram_bwd_part_kernel(GramBwdJobs J, int L, double* __restrict__ part) {
+  constexpr int NS = MC + MC * MF * 2 + 1;
   __shared__ double sp[64];
-  __shared__ double red[4];
-  const int l = blockIdx.x, tid = threadIdx.x;
-  if (tid < s.n_params) sp[tid] = params[(int64_t)l * s.n_params + tid];
+  __shared__ double wred[4][NS];
+  const int c = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+  int jb = 0;
+  while (jb + 1 < J.njobs && c >= J.j[jb + 1].chunk0) ++jb;
+  const GramBwdJob& job = J.j[jb];
+  const DevSpec& s = J.s[job.spec];
+  if (tid < job.n_params) sp[tid] = job.params[(int64_t)l * job.n_params + tid];
   __syncthreads();
   double acc_s[MC];
   double acc_f[MC][MF][2];
@@ -67,37 +83,63 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(DevSpec s, lvae_xview x1,
     for (int f = 0; f < MF; ++f) acc_f[r][f][0] = acc_f[r][f][1] = 0.0;
   }
   double dd = 0.0;
-  const int64_t per_b = (int64_t)n1 * n2, total = per_b * nb;
-  for (int64_t e = tid; e < total; e += 256) {
+  const int64_t per_b = (int64_t)job.n1 * job.n2, total = per_b * job.nb;
+  const int64_t e0 = (int64_t)(c - job.chunk0) * kGBChunk;
+  for (int64_t e = e0 + tid; e < e0 + kGBChunk && e < total; e += 256) {
     const int b = (int)(e / per_b);
     const int64_t rem = e - b * per_b;
-    const int i = (int)(rem / n2), j = (int)(rem - (int64_t)i * n2);
-    const double g = G[b * gsb + l * gsl + i * ldg + j];
+    const int i = (int)(rem / job.n2), j = (int)(rem - (int64_t)i * job.n2);
+    const double g = job.G[b * job.gsb + l * job.gsl + i * job.ldg + j];
     if (g == 0.0) continue;
-    const double* xi = x1.ptr + b * x1.stride_b + l * x1.stride_l + i * x1.ld;
-    const double* xj = x2.ptr + b * x2.stride_b + l * x2.stride_l + j * x2.ld;
+    const double* xi = job.x1.ptr + b * job.x1.stride_b + l * job.x1.stride_l + i * job.x1.ld;
+    const double* xj = job.x2.ptr + b * job.x2.stride_b + l * job.x2.stride_l + j * job.x2.ld;
     kernel_grad_acc<MC, MF, double, double>(s, xi, xj, sp, g, acc_s, acc_f);
     if (i == j) dd += g;
   }
+  const int w = tid >> 6, lane = tid & 63;
 #pragma unroll
   for (int r = 0; r < MC; ++r) {
-    const double v = block_sum<256>(acc_s[r], red);
-    if (tid == 0 && r < s.n_comp) dparams[(int64_t)l * s.n_params + s.scale_idx[r]] += v;
+    const double v = wave_sum(acc_s[r]);
+    if (lane == 0) wred[w][r] = v;
 #pragma unroll
-    for (int f = 0; f < MF; ++f) {
+    for (int f = 0; f < MF; ++f)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const double w = block_sum<256>(acc_f[r][f][q], red);
-        if (tid == 0) {
-          const int pi = slot_param<MC, MF>(s, MC + (r * MF + f) * 2 + q);
-          if (pi >= 0) dparams[(int64_t)l * s.n_params + pi] += w;
-        }
+        const double u = wave_sum(acc_f[r][f][q]);
+        if (lane == 0) wred[w][MC + (r * MF + f) * 2 + q] = u;
       }
-    }
   }
-  if (ddiag) {
-    const double v = block_sum<256>(dd, red);
-    if (tid == 0) ddiag[l] += v;
+  {
+    const double v = wave_sum(dd);
+    if (lane == 0) wred[w][NS - 1] = v;
+  }
+  __syncthreads();
+  double* out = part + ((int64_t)l * J.total_chunks + c) * NS;
+  for (int sl = tid; sl < NS; sl += 256) out[sl] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
+}
+
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void gram_bwd_sum_kernel(GramBwdJobs J, const double* __restrict__ part) {
+  constexpr int NS = MC + MC * MF * 2 + 1;
+  __shared__ double red[kGBMaxJobs][NS];
+  const int l = blockIdx.x, tid = threadIdx.x;
+  for (int t = tid; t < J.njobs * NS; t += 256) {
+    const int jb = t / NS, sl = t % NS;
+    const GramBwdJob& job = J.j[jb];
+    double v = 0.0;
+    for (int c = job.chunk0; c < job.chunk0 + job.nchunks; ++c) v += part[((int64_t)l * J.total_chunks + c) * NS + sl];
+    red[jb][sl] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int jb = 0; jb < J.njobs; ++jb) {
+    const GramBwdJob& job = J.j[jb];
+    const DevSpec& s = J.s[job.spec];
+    for (int sl = 0; sl < NS - 1; ++sl) {
+      const int pi = slot_param<MC, MF>(s, sl);
+      if (pi >= 0) job.dparams[(int64_t)l * job.n_params + pi] += red[jb][sl];
+    }
+    if (job.ddiag) job.ddiag[l] += red[jb][NS - 1];
   }
 }
 
@@ -463,17 +505,47 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
   return 0;
 }
 
-int gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
-                 const double* params, const double* G, int64_t gsb, int64_t gsl, int64_t ldg, double* dparams,
-                 double* ddiag, hipStream_t st) {
-  const int bucket = spec_bucket(spec);
-  if (!bucket) return -1;
-  if (nb < 1 || L < 1) return -4;
-  const DevSpec ds = to_dev(spec);
-  if (bucket == 1)
-    gram_bwd_kernel<8, 2><<<L, 256, 0, st>>>(ds, x1, x2, nb, L, n1, n2, params, G, gsb, gsl, ldg, dparams, ddiag);
-  else
-    gram_bwd_kernel<16, 4><<<L, 256, 0, st>>>(ds, x1, x2, nb, L, n1, n2, params, G, gsb, gsl, ldg, dparams, ddiag);
+// Adjoints of up to kGBMaxJobs Grams in two launches (see gram_bwd_part_kernel); `jobs` hold
+// host-side descriptors whose .spec indexes specs[0..1].  part: gram_bwd_part_bytes(...) bytes.
+size_t gram_bwd_part_bytes(const GramBwdJob* jobs, int njobs, int L) {
+  int64_t chunks = 0;
+  for (int q = 0; q < njobs; ++q) chunks += cdiv((int64_t)jobs[q].nb * jobs[q].n1 * jobs[q].n2, kGBChunk);
+  return (size_t)L * (size_t)(chunks > 0 ? chunks : 1) * (16 + 16 * 4 * 2 + 1) * sizeof(double);
+}
+
+int gram_bwd_multi_f64(const lvae_kernel_spec* const* specs, const GramBwdJob* jobs, int njobs, int L, double* part,
+                       hipStream_t st) {
+  if (njobs < 1 || njobs > kGBMaxJobs || L < 1) return -4;
+  GramBwdJobs J;
+  int bucket = 1;
+  for (int q = 0; q < 2; ++q) {
+    if (!specs[q]) {
+      J.s[q] = J.s[0];
+      continue;
+    }
+    const int bk = spec_bucket(specs[q]);
+    if (!bk) return -1;
+    bucket = bk > bucket ? bk : bucket;
+    J.s[q] = to_dev(specs[q]);
+  }
+  int chunks = 0;
+  for (int q = 0; q < njobs; ++q) {
+    J.j[q] = jobs[q];
+    J.j[q].n_params = specs[jobs[q].spec]->n_params;
+    J.j[q].chunk0 = chunks;
+    J.j[q].nchunks = cdiv((int64_t)jobs[q].nb * jobs[q].n1 * jobs[q].n2, kGBChunk);
+    chunks += J.j[q].nchunks;
+  }
+  J.njobs = njobs;
+  J.total_chunks = chunks;
+  if (chunks == 0) return 0;
+  if (bucket == 1) {
+    gram_bwd_part_kernel<8, 2><<<dim3(chunks, L), 256, 0, st>>>(J, L, part);
+    gram_bwd_sum_kernel<8, 2><<<L, 256, 0, st>>>(J, part);
+  } else {
+    gram_bwd_part_kernel<16, 4><<<dim3(chunks, L), 256, 0, st>>>(J, L, part);
+    gram_bwd_sum_kernel<16, 4><<<L, 256, 0, st>>>(J, part);
+  }
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -494,11 +566,26 @@ int lvae_gram_f32(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, in
   return lvae::gram_launch<float>(spec, x1, x2, nb, L, n1, n2, params, diag, out, osb, osl, ldo, stream);
 }
 
+size_t lvae_gram_bwd_workspace_size(int nb, int L, int n1, int n2) {
+  lvae::GramBwdJob j{};
+  j.nb = nb, j.n1 = n1, j.n2 = n2;
+  return lvae::gram_bwd_part_bytes(&j, 1, L);
+}
+
 int lvae_gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
                       const double* params, const double* G, int64_t gsb, int64_t gsl, int64_t ldg, double* dparams,
-                      double* ddiag, void* stream) {
-  return lvae::gram_bwd_f64(spec, x1, x2, nb, L, n1, n2, params, G, gsb, gsl, ldg, dparams, ddiag,
-                            (hipStream_t)stream);
+                      double* ddiag, void* workspace, void* stream) {
+  if (!spec) return -1;
+  if (nb < 1 || L < 1 || n1 < 0 || n2 < 0) return -4;
+  if (!params) return -8;
+  if (!G) return -9;
+  if (!dparams) return -13;
+  if (!workspace) return -15;
+  lvae::GramBwdJob j{};
+  j.spec = 0, j.x1 = x1, j.x2 = x2, j.nb = nb, j.n1 = n1, j.n2 = n2, j.params = params, j.G = G;
+  j.gsb = gsb, j.gsl = gsl, j.ldg = ldg, j.dparams = dparams, j.ddiag = ddiag;
+  const lvae_kernel_spec* specs[2] = {spec, nullptr};
+  return lvae::gram_bwd_multi_f64(specs, &j, 1, L, (double*)workspace, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -19,13 +19,12 @@
 //   dB_p = c (iB - s s^T - iB V iB - iB K0 iB)_p - iBK_p Xq iBK_p^T
 //   (Adam path) dm = 2c iK K0xz^T s + g t,  dH = c iK Q iK + h (iK - iH)
 #include "common.hpp"
+#include "gram_bwd.hpp"
 #include "prof.hpp"
 
 namespace lvae {
 
-int gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2, int nb, int L, int n1, int n2,
-                 const double* params, const double* G, int64_t gsb, int64_t gsl, int64_t ldg, double* dparams,
-                 double* ddiag, hipStream_t st);
+
 int spd_inv_small_f64(int n, int batch, const double* A, int64_t stride, double* Ainv, int64_t stride_out,
                       double* logdet, int32_t* info, hipStream_t st);
 int spd_inv_small2_f64(int n, int nb0, const double* A0, int64_t stride0, double* Ainv0, int64_t stride_out0,
@@ -47,7 +46,7 @@ struct HWs {
   // vectors
   double *t, *v1, *w, *a, *tM;  // [L,M]
   double *y, *r, *s, *u;        // [L,B]
-  double *ldK, *ldB, *ldH, *epsv, *part;
+  double *ldK, *ldB, *ldH, *epsv, *part, *gpart;
   int32_t* info;
   size_t bytes;
   HWs(char* base, const lvae_hensman_dims& d) {
@@ -73,6 +72,9 @@ struct HWs {
     epsv = take(L);
     part = take(L * 16);
     info = (int32_t*)take(L * (2 + d.P_b));
+    // Gram-adjoint partials of the four Grams (gram.hip, kGBChunk = 1024 elements per chunk, <= 145 slots)
+    const size_t chunks = (B * M + 1023) / 1024 + (M * M + 1023) / 1024 + 2 * ((TT + 1023) / 1024);
+    gpart = take(L * chunks * 145);
     bytes = off;
   }
 };
@@ -431,10 +433,15 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   (void)hipMemsetAsync(dparams1, 0, sizeof(double) * L * spec1->n_params, st);
   if (dnoise) (void)hipMemsetAsync(dnoise, 0, sizeof(double) * L, st);
   const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
-  LVAE_TRY(gram_bwd_f64(spec0, xv, zv, 1, L, B, M, params0, w.dK0xz, 0, BM, M, dparams0, nullptr, st));
-  LVAE_TRY(gram_bwd_f64(spec0, zv, zv, 1, L, M, M, params0, w.dK0zz, 0, MM, M, dparams0, nullptr, st));
-  LVAE_TRY(gram_bwd_f64(spec0, xs, xs, P_b, L, T, T, params0, w.GK0, TT, P_b * TT, T, dparams0, nullptr, st));
-  LVAE_TRY(gram_bwd_f64(spec1, xs, xs, P_b, L, T, T, params1, w.GB, TT, P_b * TT, T, dparams1, dnoise, st));
+  {
+    const GramBwdJob jobs[4] = {
+        {0, xv, zv, 1, B, M, 0, params0, w.dK0xz, 0, BM, M, dparams0, nullptr, 0, 0},
+        {0, zv, zv, 1, M, M, 0, params0, w.dK0zz, 0, MM, M, dparams0, nullptr, 0, 0},
+        {0, xs, xs, P_b, T, T, 0, params0, w.GK0, TT, P_b * TT, T, dparams0, nullptr, 0, 0},
+        {1, xs, xs, P_b, T, T, 0, params1, w.GB, TT, P_b * TT, T, dparams1, dnoise, 0, 0}};
+    const lvae_kernel_spec* specs[2] = {spec0, spec1};
+    LVAE_TRY(gram_bwd_multi_f64(specs, jobs, 4, L, w.gpart, st));
+  }
   // Adam path: gradients wrt m and H
   if (!d.natural_gradient && dm && dH) {
     LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, w.v1, 1, M, 0, 0.0, w.tM, 1, M, 0, L, 1, st));

@@ -32,6 +32,7 @@ struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
   _Float16* planes;  // fp16 hi / lo planes of the S GEMM operand: 2 L np^2 halves
   uint32_t* bmax;    // [L] fp32 bits of max |K^-1_ij| sqrt(v_j)
+  float* rmax;       // [L, np] per-row maxima of the same
   char* sweep;
   double *mu, *alpha, *kdiag, *logdet, *part;
   size_t bytes;
@@ -49,6 +50,7 @@ struct KLWorkspace {
     v = (float*)take((size_t)L * np_ * sizeof(float));
     sv = (float*)take((size_t)L * np_ * sizeof(float));
     bmax = (uint32_t*)take((size_t)L * sizeof(uint32_t));
+    rmax = (float*)take((size_t)L * np_ * sizeof(float));
     mu = (double*)take((size_t)L * np_ * sizeof(double));
     alpha = (double*)take((size_t)L * np_ * sizeof(double));
     kdiag = (double*)take((size_t)L * np_ * sizeof(double));
@@ -71,12 +73,12 @@ __global__ void kl_prep_kernel(const double* __restrict__ mu, const double* __re
   sv[(int64_t)l * np_ + i] = (float)sqrt(vv);
 }
 
-// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]; bmax[l] folds
-// max_j |Kinv[i][j]| sqrt(v_j) (the split bound of the S GEMM operand, syrk_x3.hip)
+// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]; rmax[l][i] =
+// max_j |Kinv[i][j]| sqrt(v_j) (reduced to the split bound of the S GEMM operand by kl_finalize)
 __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ muc,
                                                        const float* __restrict__ sv, int np_,
                                                        double* __restrict__ alpha, double* __restrict__ kdiag,
-                                                       uint32_t* __restrict__ bmax) {
+                                                       float* __restrict__ rmax) {
   const int l = blockIdx.y, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= np_) return;
@@ -98,28 +100,39 @@ __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__
   if (lane == 0) {
     alpha[(int64_t)l * np_ + i] = acc;
     kdiag[(int64_t)l * np_ + i] = (double)row[i];
-    atomicMax(bmax + l, __float_as_uint(bm));
+    rmax[(int64_t)l * np_ + i] = bm;
   }
 }
 
 __global__ __launch_bounds__(256) void kl_finalize_kernel(const double* __restrict__ muc, const double* __restrict__ logv,
                                                           int ld, const double* __restrict__ alpha,
                                                           const double* __restrict__ kdiag,
-                                                          const double* __restrict__ logdet, int n, int np_,
-                                                          double* __restrict__ kl) {
+                                                          const double* __restrict__ logdet,
+                                                          const float* __restrict__ rmax, int n, int np_,
+                                                          double* __restrict__ kl, uint32_t* __restrict__ bmax) {
   __shared__ double red[4];
+  __shared__ float fred[4];
   const int l = blockIdx.x, tid = threadIdx.x;
   double quad = 0.0, tr = 0.0, slv = 0.0;
+  float bm = 0.f;
   for (int i = tid; i < n; i += 256) {
     const double lv = logv[(int64_t)i * ld + l];
     quad += muc[(int64_t)l * np_ + i] * alpha[(int64_t)l * np_ + i];
     tr += exp(lv) * kdiag[(int64_t)l * np_ + i];
     slv += lv;
   }
+  for (int i = tid; i < np_; i += 256) bm = fmaxf(bm, rmax[(int64_t)l * np_ + i]);
   quad = block_sum<256>(quad, red);
   tr = block_sum<256>(tr, red);
   slv = block_sum<256>(slv, red);
-  if (tid == 0) kl[l] = 0.5 * (tr + quad - (double)n + logdet[l] - slv);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
+  if ((tid & 63) == 0) fred[tid >> 6] = bm;
+  __syncthreads();
+  if (tid == 0) {
+    kl[l] = 0.5 * (tr + quad - (double)n + logdet[l] - slv);
+    bmax[l] = __float_as_uint(fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3])));
+  }
 }
 
 __global__ void kl_bwd_elem_kernel(const double* __restrict__ logv, int ld, int n, int np_, int L,
@@ -175,9 +188,9 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   }
   {
     ProfScope ps(LVAE_PH_KL_REDUCE, st);
-    (void)hipMemsetAsync(ws.bmax, 0, sizeof(uint32_t) * L, st);
-    kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.alpha, ws.kdiag, ws.bmax);
-    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
+    kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.alpha, ws.kdiag, ws.rmax);
+    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, ws.rmax, n, np_, kl,
+                                          ws.bmax);
   }
   LVAE_CHECK_LAUNCH();
   return 0;

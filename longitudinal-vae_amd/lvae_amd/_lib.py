@@ -78,8 +78,9 @@ _DIMS = ctypes.POINTER(HensmanDims)
 SIGNATURES = {
     "lvae_gram_f64": (_I32, [_SPEC, XView, XView, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I64, _I64, _I64, _VP]),
     "lvae_gram_f32": (_I32, [_SPEC, XView, XView, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _I64, _I64, _I64, _VP]),
+    "lvae_gram_bwd_workspace_size": (_SZ, [_I32, _I32, _I32, _I32]),
     "lvae_gram_bwd_f64": (_I32, [_SPEC, XView, XView, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _I64, _I64, _VP,
-                                 _VP, _VP]),
+                                 _VP, _VP, _VP]),
     "lvae_kl_closed_padded_n": (_I32, [_I32]),
     "lvae_kl_closed_workspace_size": (_SZ, [_I32, _I32]),
     "lvae_kl_closed_fwd_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _I32, _VP, _VP, _VP,

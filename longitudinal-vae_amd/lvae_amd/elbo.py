@@ -32,10 +32,16 @@ def _check_info(info, what):
         _PENDING.append((info, what))
 
 
-def check_pending():
+def take_pending():
+    """The deferred info checks recorded since the last check (and forget them) -- a captured graph
+    keeps these: its replays rewrite the same info tensors (steps.GraphedStep)."""
     global _PENDING
     pend, _PENDING = _PENDING, []
-    for info, what in pend:
+    return pend
+
+
+def check_pending(pend=None):
+    for info, what in (take_pending() if pend is None else pend):
         bad = info.nonzero()
         if bad.numel():
             l = int(bad[0, 0])

@@ -317,10 +317,11 @@ class _GramFn(torch.autograd.Function):
         G = g.reshape(nb, L, n1, n2).to(torch.float64).contiguous()
         dp = torch.zeros_like(p)
         dd = torch.zeros(L, dtype=torch.float64, device=p.device) if ctx.has_diag else None
+        ws = torch.empty(int(lib.lvae_gram_bwd_workspace_size(nb, L, n1, n2)), dtype=torch.uint8, device=p.device)
         rc = lib.lvae_gram_bwd_f64(ctx.spec, _lib.xview(x1e, x1e.stride(0), x1e.stride(1)),
                                    _lib.xview(x2e, x2e.stride(0), x2e.stride(1)), nb, L, n1, n2, _lib.ptr(p),
                                    _lib.ptr(G), G.stride(0), G.stride(1), G.stride(2), _lib.ptr(dp), _lib.ptr(dd),
-                                   _lib.stream_ptr())
+                                   _lib.ptr(ws), _lib.stream_ptr())
         _lib.check(rc, "gram_bwd")
         ddiag = None if dd is None else dd.reshape(ctx.diag_shape)
         return dp, ddiag, None, None, None

@@ -40,6 +40,9 @@ class GaussianLikelihood(nn.Module):
     @noise.setter
     def noise(self, value):
         with torch.no_grad():
+            if isinstance(value, (int, float)):  # a device fill: no host copy, so graph-capturable
+                self._log_noise.fill_(math.log(value - math.exp(MIN_LOG)))
+                return
             v = torch.as_tensor(value, dtype=torch.float64, device=self._log_noise.device)
             self._log_noise.copy_(torch.log(v - math.exp(MIN_LOG)).expand_as(self._log_noise))
 

@@ -1,13 +1,17 @@
 """One optimisation step of each training driver, as tensors-in / tensors-out (no host syncs).
 
-closed_step   : standard_training with type_KL='closed' (training.py:484-592)
-hensman_step  : hensman_training batch body incl. the natural-gradient update (training.py:91-135)
-Both return detached device scalars; callers read them when they choose (the reference's
-per-step ``.item()`` calls, training.py:137-140, are the sync points this removes).
+ClosedStep   : standard_training with type_KL='closed' (training.py:484-592)
+HensmanStep  : hensman_training batch body incl. the natural-gradient update (training.py:91-135)
+GraphedStep  : either step replayed as HIP graphs (torch.cuda.CUDAGraph is a hipGraph on ROCm)
+
+Both steps return detached device scalars; callers read them when they choose (the reference's
+per-step ``.item()`` calls, training.py:137-140, are the sync points this removes).  Each step is
+split into ``forward_backward`` (everything up to the gradients) and ``apply`` (optimiser + state
+updates) so that a data-parallel all-reduce can sit between two captured graphs.
 """
 import torch
 
-from .elbo import KL_closed_batched, minibatch_KLD_upper_bound, natural_gradient_update
+from .elbo import KL_closed_batched, minibatch_KLD_upper_bound, natural_gradient_update, take_pending
 
 
 class ClosedStep:
@@ -17,7 +21,7 @@ class ClosedStep:
         self.weight, self.loss_function, self.constrain_scales = weight, loss_function, constrain_scales
         self.grad_hook = grad_hook  # e.g. the data-parallel all-reduce
 
-    def __call__(self, img, mask, X, eps=None):
+    def forward_backward(self, img, mask, X, eps=None):
         self.opt.zero_grad(set_to_none=False)
         recon, mu, log_var = self.vae(img, eps)
         mse, nll = self.vae.loss_function(recon, img, mask)
@@ -31,20 +35,31 @@ class ClosedStep:
             gp = kl.sum()
             net = nll_loss + gp
         net.backward()
+        return net.detach(), recon_loss.detach(), nll_loss.detach(), gp.detach()
+
+    def communicate(self):
         if self.grad_hook is not None:
             self.grad_hook()
+
+    def apply(self):
         self.opt.step()
         if self.constrain_scales:
             self.lik.noise = 1.0
-        return net.detach(), recon_loss.detach(), nll_loss.detach(), gp.detach()
+
+    def __call__(self, img, mask, X, eps=None):
+        out = self.forward_backward(img, mask, X, eps)
+        self.communicate()
+        self.apply()
+        return out
 
 
 class HensmanStep:
     """hensman_training batch body (training.py:91-135), loss 'mse' or 'nll'.
 
-    State: the inducing posterior (m [L,M,1], H [L,M,M]) lives here and is updated in place by the
-    natural-gradient step (training.py:129-135) when natural_gradient is on; otherwise m and H are
-    leaf tensors the optimiser owns (H enters as H H^T, training.py:108).
+    State: the inducing posterior (m [L,M,1], H [L,M,M]) lives here and is updated IN PLACE by the
+    natural-gradient step (training.py:129-135) when natural_gradient is on (so a captured graph
+    replays it); otherwise m and H are leaf tensors the optimiser owns (H enters as H H^T,
+    training.py:108).
     Data parallel: pass ``world`` and a ``grad_hook`` (all-reduce of the Adam gradients) and
     ``ng_reduce`` (SUM all-reduce of the natural-gradient directions, see lvae_hensman_dims)."""
 
@@ -57,8 +72,9 @@ class HensmanStep:
         self.weight, self.loss_function = weight, loss_function
         self.ng, self.ng_lr, self.eps = natural_gradient, natural_gradient_lr, eps
         self.world, self.grad_hook, self.ng_reduce = world, grad_hook, ng_reduce
+        self._gm = self._gH = None
 
-    def __call__(self, img, mask, X, eps=None):
+    def forward_backward(self, img, mask, X, eps=None):
         self.opt.zero_grad(set_to_none=False)
         recon, mu, log_var = self.vae(img, eps)
         mse, nll = self.vae.loss_function(recon, img, mask)
@@ -77,11 +93,71 @@ class HensmanStep:
         else:
             net = nll_loss + kld
         net.backward()
+        self._gm, self._gH = gm, gH
+        return net.detach(), recon_loss.detach(), nll_loss.detach(), kld.detach()
+
+    def communicate(self):
         if self.grad_hook is not None:
             self.grad_hook()
+        if self.ng and self.ng_reduce is not None:
+            self.ng_reduce([self._gm, self._gH])
+
+    def apply(self):
         self.opt.step()
         if self.ng:
-            if self.ng_reduce is not None:
-                self.ng_reduce([gm, gH])
-            self.m, self.H = natural_gradient_update(self.m, self.H, gm, gH, self.ng_lr)
-        return net.detach(), recon_loss.detach(), nll_loss.detach(), kld.detach()
+            m2, H2 = natural_gradient_update(self.m, self.H, self._gm, self._gH, self.ng_lr)
+            with torch.no_grad():
+                self.m.copy_(m2.reshape(self.m.shape).to(self.m.dtype))
+                self.H.copy_(H2.to(self.H.dtype))
+
+    def __call__(self, img, mask, X, eps=None):
+        out = self.forward_backward(img, mask, X, eps)
+        self.communicate()
+        self.apply()
+        return out
+
+
+class GraphedStep:
+    """A ClosedStep / HensmanStep replayed as HIP graphs.
+
+    ``inputs`` are static device tensors (img, mask, X, eps) the caller refills in place between
+    replays (e.g. ``index_select(..., out=)`` of the next batch).  With no communication the whole
+    step is one graph; with a ``grad_hook`` / ``ng_reduce`` (data parallel) the step is two graphs
+    around the eager collectives.  The optimiser must be capturable (torch.optim.Adam(...,
+    capturable=True)); numerical-failure checks are deferred (set_sync_checks(False)) and
+    ``check()`` reads the captured info arrays, which every replay rewrites."""
+
+    def __init__(self, step, inputs, warmup=3):
+        self.step, self.inputs = step, inputs
+        comm = getattr(step, "grad_hook", None) is not None or getattr(step, "ng_reduce", None) is not None
+        self.stream = torch.cuda.Stream()
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):  # warm-up: allocations, MIOpen / hipBLASLt plans, side streams
+            for _ in range(warmup):
+                step(*inputs)
+        torch.cuda.current_stream().wait_stream(self.stream)
+        torch.cuda.synchronize()
+        take_pending()
+        self.g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g1, stream=self.stream):
+            self.out = step.forward_backward(*inputs)
+            if not comm:
+                step.apply()
+        self.g2 = None
+        if comm:
+            self.g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g2, stream=self.stream):
+                step.apply()
+        self.pending = take_pending()
+        self.comm = comm
+
+    def __call__(self):
+        self.g1.replay()
+        if self.comm:
+            self.step.communicate()
+            self.g2.replay()
+        return self.out
+
+    def check(self):
+        from .elbo import check_pending
+        check_pending(self.pending)

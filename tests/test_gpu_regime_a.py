@@ -480,3 +480,56 @@ def test_dp_contract_c4_eight_ranks(hip):
     print("8-rank DP contract errors:", errs)
     assert errs["kld"] < 1e-10 and errs["dmu"] < 1e-10
     assert errs["grads"] < 1e-8 and errs["gm"] < 1e-8 and errs["gH"] < 1e-8
+
+
+def test_graphed_hensman_step_matches_eager(hip):
+    """The HIP-graph replay of the Hensman step (GraphedStep: forward, backward, capturable Adam and
+    the in-place natural-gradient update in one graph) reproduces the eager step, step after step,
+    with a new batch gathered into the static inputs before every replay."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_batch
+    from lvae_amd.steps import GraphedStep, HensmanStep
+    from lvae_amd.vae import ConvVAE
+    L, M, T, P, P_b = 4, 40, 16, 32, 5
+    img, mask, X = health_mnist_batch(P, T, seed=6, device=DEV)
+    N = P * T
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
+    batches = [torch.cat([torch.arange(s * T, (s + 1) * T) for s in ss]).to(DEV)
+               for ss in ([3, 9, 20, 1, 27], [4, 11, 30, 0, 7], [2, 5, 8, 13, 21], [6, 10, 12, 14, 15])]
+    eps = torch.randn(P_b * T, L, generator=torch.Generator().manual_seed(0)).to(DEV)
+
+    def make():
+        torch.manual_seed(3)
+        vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+        k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+        k0, k1 = k0.to(DEV), k1.to(DEV)
+        lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+        with torch.no_grad():
+            H = k0(z, z).evaluate() + 1e-6 * torch.eye(M, dtype=torch.float64, device=DEV)
+        m = torch.zeros(L, M, 1, dtype=torch.float64, device=DEV)
+        opt = torch.optim.Adam(list(k0.parameters()) + list(k1.parameters()) + list(vae.parameters()), lr=1e-3,
+                               capturable=True)
+        return HensmanStep(vae, k0, k1, lik, opt, m, H, z, P, T), vae, k0
+
+    la.set_sync_checks(False)
+    try:
+        eager, vae_e, k0_e = make()
+        eager(img[batches[0]], mask[batches[0]], X[batches[0]], eps)  # = the graph's warm-up step
+        outs_e = [[float(v) for v in eager(img[b], mask[b], X[b], eps)] for b in batches]
+        graph_step, vae_g, k0_g = make()
+        s = (img[batches[0]].clone(), mask[batches[0]].clone(), X[batches[0]].clone(), eps)
+        g = GraphedStep(graph_step, s, warmup=1)
+        outs_g = []
+        for b in batches:
+            torch.index_select(img, 0, b, out=s[0])
+            torch.index_select(mask, 0, b, out=s[1])
+            torch.index_select(X, 0, b, out=s[2])
+            outs_g.append([float(v) for v in g()])
+        g.check()
+    finally:
+        la.set_sync_checks(True)
+    for a, b in zip(outs_e, outs_g):
+        assert np.allclose(a, b, rtol=1e-6), (a, b)
+    assert rel(graph_step.m, eager.m) < 1e-6 and rel(graph_step.H, eager.H) < 1e-6
+    for (n, p), (_, q) in zip(k0_g.named_parameters(), k0_e.named_parameters()):
+        assert rel(p, q) < 1e-9, n
