@@ -402,11 +402,13 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
     if (lane == 0) wred[wv][NS - 1] = v;
   }
   __syncthreads();
-  double* out = part + ((int64_t)l * ntiles + blockIdx.x) * NS;
-  for (int sl = tid; sl < NS; sl += 256) out[sl] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
+  for (int sl = tid; sl < NS; sl += 256)
+    part[((int64_t)l * NS + sl) * ntiles + blockIdx.x] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
 }
 
-// Reduce the tile partials: dparams[l, :] = gkl[l] * sum over tiles (slot -> param), dnoise[l].
+// Reduce the tile partials: dparams[l, p(slot)] = gkl[l] * sum over tiles, dnoise[l] (slot NS-1).
+// Partials are laid out [l][slot][tile] (coalesced sums); one workgroup per (slot, l).  Every
+// parameter has exactly one slot (slot_param is injective), so the writes never collide.
 template <int MC, int MF>
 __global__ __launch_bounds__(256) void kl_gram_bwd_reduce(DevSpec s, const double* __restrict__ part, int ntiles,
                                                           const double* __restrict__ gkl,
@@ -414,21 +416,18 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_reduce(DevSpec s, const doubl
                                                           double* __restrict__ dnoise) {
   constexpr int NS = MC + MC * MF * 2 + 1;
   __shared__ double red[4];
-  const int l = blockIdx.x, tid = threadIdx.x;
-  const double g = gkl[l];
-  for (int p = tid; p < s.n_params; p += 256) dparams[(int64_t)l * s.n_params + p] = 0.0;
-  __syncthreads();
-  for (int slot = 0; slot < NS; ++slot) {
-    double v = 0.0;
-    for (int t = tid; t < ntiles; t += 256) v += part[((int64_t)l * ntiles + t) * NS + slot];
-    v = block_sum<256>(v, red);
-    if (tid == 0) {
-      if (slot == NS - 1) {
-        if (dnoise) dnoise[l] = g * v;
-      } else {
-        const int pi = slot_param<MC, MF>(s, slot);
-        if (pi >= 0) dparams[(int64_t)l * s.n_params + pi] += g * v;
-      }
+  const int slot = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+  const int pi = slot == NS - 1 ? -2 : slot_param<MC, MF>(s, slot);
+  if (pi == -1) return;  // an unused slot (uniform over the workgroup)
+  const double* p = part + ((int64_t)l * NS + slot) * ntiles;
+  double v = 0.0;
+  for (int t = tid; t < ntiles; t += 256) v += p[t];
+  v = block_sum<256>(v, red);
+  if (tid == 0) {
+    if (pi == -2) {
+      if (dnoise) dnoise[l] = gkl[l] * v;
+    } else {
+      dparams[(int64_t)l * s.n_params + pi] = gkl[l] * v;
     }
   }
 }
@@ -496,10 +495,10 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
   dim3 grid(ntiles, L);
   if (bucket == 1) {
     kl_gram_bwd_tiles<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part, ntiles);
-    kl_gram_bwd_reduce<8, 2><<<L, 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
+    kl_gram_bwd_reduce<8, 2><<<dim3(8 + 8 * 2 * 2 + 1, L), 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
   } else {
     kl_gram_bwd_tiles<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part, ntiles);
-    kl_gram_bwd_reduce<16, 4><<<L, 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
+    kl_gram_bwd_reduce<16, 4><<<dim3(16 + 16 * 4 * 2 + 1, L), 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
   }
   LVAE_CHECK_LAUNCH();
   return 0;

@@ -108,8 +108,13 @@ class LatentShardedClosedStep:
             raise ValueError(f"rank rows {n_loc} x world {W} != N = {N} (equal image shards required)")
         # (mu, logvar) of all N rows on every rank: one all-gather of [N/W, 2L]
         loc = torch.cat([mu.detach(), log_var.detach()], 1).contiguous()
-        full = torch.empty(N, 2 * L, dtype=loc.dtype, device=loc.device)
-        dist.all_gather_into_tensor(full, loc, group=self.group)
+        if dist.get_backend(self.group) == "nccl":
+            full = torch.empty(N, 2 * L, dtype=loc.dtype, device=loc.device)
+            dist.all_gather_into_tensor(full, loc, group=self.group)
+        else:  # gloo (CPU tests, multi-rank rehearsals on one GPU): list form
+            parts = [torch.empty_like(loc) for _ in range(W)]
+            dist.all_gather(parts, loc, group=self.group)
+            full = torch.cat(parts, 0)
         d0, d1 = shard_bounds(L, W, r)
         coef = self.weight / L if self.loss_function == "mse" else 1.0
         gmv = torch.zeros(N, 2 * L, dtype=loc.dtype, device=loc.device)
