@@ -144,168 +144,17 @@ __global__ __launch_bounds__(256) void gram_bwd_sum_kernel(GramBwdJobs J, const 
 }
 
 // ------------------------------------------------------------------------------------------
-// Column-vectorised tile evaluation for the Regime B kernels.  Thread (w, jj) of a 256-thread
-// workgroup owns column jj of a 64x64 tile and rows ii = w + 4k, k < 16.  The (uniform) spec is
-// walked once per 16 elements instead of once per element, each factor is applied to all 16
-// rows at once (row covariates are wave-uniform LDS broadcasts), and RBF factors use the native
-// exp2 with a per-factor constant: ~30 VALU ops per element instead of a spec interpreter per
-// element.  Category comparisons and covariate differences stay in fp64 (exact 0/1, as the
-// reference's double compare).
+// Regime B Gram tiles, 4 x 4 micro-tiles.  A 256-thread workgroup owns a 64 x 64 tile; thread
+// (tr, tc) = (tid >> 4, tid & 15) owns rows 4 tr + a and columns 4 tc + c (a, c < 4): per factor
+// it reads 4 row and 4 column covariates (fp64, LDS) for 16 elements and the tile rows go out /
+// come in as float4 (16 B per lane, 256 contiguous bytes per row and 16 lanes).  The (uniform)
+// spec is walked once per 16 elements.  Category / binary tests and covariate differences stay in
+// fp64 (exact 0/1 and exact differences, as the reference's double arithmetic); factor values,
+// products and sums are fp32 (the covariance is fp32); RBF / periodic use the native exp2.
 // ------------------------------------------------------------------------------------------
-constexpr int kTK = kGT / 4;  // rows per thread
 constexpr float kLog2e = 1.4426950408889634f;
+typedef float g_f32x4 __attribute__((ext_vector_type(4)));
 
-template <int MC, int MF>
-__device__ __attribute__((always_inline)) inline void tile_kernel_f32(const DevSpec& s, const double* __restrict__ sx1, int ii0,
-                                       const double* __restrict__ xj, const float* __restrict__ p,
-                                       float (&out)[kTK]) {
-#pragma unroll
-  for (int k = 0; k < kTK; ++k) out[k] = 0.f;
-#pragma unroll
-  for (int r = 0; r < MC; ++r) {
-    const bool on_r = r < s.n_comp;
-    float prod[kTK];
-    const float sc = p[s.scale_idx[r]];
-#pragma unroll
-    for (int k = 0; k < kTK; ++k) prod[k] = sc;
-#pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      if (!on_r || f >= s.n_fac[r]) continue;
-      const int d = s.dim[r][f];
-      const double b = xj[d];
-      const int kind = s.kind[r][f];
-      if (kind == LVAE_CAT) {
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) prod[k] = (sx1[(ii0 + 4 * k) * kMaxQ + d] == b) ? prod[k] : 0.f;
-      } else if (kind == LVAE_BIN) {
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) prod[k] = (sx1[(ii0 + 4 * k) * kMaxQ + d] + b == 2.0) ? prod[k] : 0.f;
-      } else if (kind == LVAE_RBF) {
-        const float ell = p[s.param_idx[r][f]];
-        const float c = -0.5f * kLog2e / (ell * ell);
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) {
-          const float df = float(sx1[(ii0 + 4 * k) * kMaxQ + d] - b);
-          prod[k] *= __builtin_amdgcn_exp2f(c * df * df);
-        }
-      } else if (kind == LVAE_PER) {
-        const float ell = p[s.param_idx[r][f]], per = p[s.param_idx[r][f] + 1];
-        const float c = -2.f * kLog2e / (ell * ell), w = float(M_PI) / per;
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) {
-          const float sn = sinf(w * float(fabs(sx1[(ii0 + 4 * k) * kMaxQ + d] - b)));
-          prod[k] *= __builtin_amdgcn_exp2f(c * sn * sn);
-        }
-      } else {  // LVAE_LIN
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) prod[k] *= float(sx1[(ii0 + 4 * k) * kMaxQ + d] * b);
-      }
-    }
-    if (on_r) {
-#pragma unroll
-      for (int k = 0; k < kTK; ++k) out[k] += prod[k];
-    }
-  }
-}
-
-// acc_s[r] += sum_k g_k dk/dscale_r ; acc_f[r][f][q] += sum_k g_k dk/dparam_q(r,f)   (same walk as above;
-// the factor derivatives are recomputed in a second pass so only prod[] stays live)
-template <int MC, int MF>
-__device__ __attribute__((always_inline)) inline void tile_kernel_grad_f32(const DevSpec& s, const double* __restrict__ sx1, int ii0,
-                                            const double* __restrict__ xj, const float* __restrict__ p,
-                                            const float (&g)[kTK], double* __restrict__ wrow, int lane) {
-#pragma unroll
-  for (int r = 0; r < MC; ++r) {
-    const bool on_r = r < s.n_comp;
-    float gp[kTK];
-#pragma unroll
-    for (int k = 0; k < kTK; ++k) gp[k] = g[k];
-    // pass 1: gp = g * prod_f phi_f
-#pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      if (!on_r || f >= s.n_fac[r]) continue;
-      const int d = s.dim[r][f];
-      const double b = xj[d];
-      const int kind = s.kind[r][f];
-      if (kind == LVAE_CAT) {
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) gp[k] = (sx1[(ii0 + 4 * k) * kMaxQ + d] == b) ? gp[k] : 0.f;
-      } else if (kind == LVAE_BIN) {
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) gp[k] = (sx1[(ii0 + 4 * k) * kMaxQ + d] + b == 2.0) ? gp[k] : 0.f;
-      } else if (kind == LVAE_RBF) {
-        const float ell = p[s.param_idx[r][f]];
-        const float c = -0.5f * kLog2e / (ell * ell);
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) {
-          const float df = float(sx1[(ii0 + 4 * k) * kMaxQ + d] - b);
-          gp[k] *= __builtin_amdgcn_exp2f(c * df * df);
-        }
-      } else if (kind == LVAE_PER) {
-        const float ell = p[s.param_idx[r][f]], per = p[s.param_idx[r][f] + 1];
-        const float c = -2.f * kLog2e / (ell * ell), w = float(M_PI) / per;
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) {
-          const float sn = sinf(w * float(fabs(sx1[(ii0 + 4 * k) * kMaxQ + d] - b)));
-          gp[k] *= __builtin_amdgcn_exp2f(c * sn * sn);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) gp[k] *= float(sx1[(ii0 + 4 * k) * kMaxQ + d] * b);
-      }
-    }
-    float ts = 0.f;
-#pragma unroll
-    for (int k = 0; k < kTK; ++k) ts += gp[k];
-    if (on_r) {
-      const float v = wave_sum(ts);
-      if (lane == 0) wrow[r] = v;
-    }
-    const float sc = p[s.scale_idx[r]];
-    // pass 2: d log phi_f / d param for the parametrised factors
-#pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      if (!on_r || f >= s.n_fac[r]) continue;
-      const int kind = s.kind[r][f];
-      if (kind != LVAE_RBF && kind != LVAE_PER) { } else {
-      const int d = s.dim[r][f];
-      const double b = xj[d];
-      const float ell = p[s.param_idx[r][f]];
-      float t0 = 0.f, t1 = 0.f;
-      if (kind == LVAE_RBF) {
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) {
-          const float df = float(sx1[(ii0 + 4 * k) * kMaxQ + d] - b);
-          t0 += gp[k] * df * df;
-        }
-        const float v = wave_sum(sc * t0 / (ell * ell * ell));
-        if (lane == 0) wrow[MC + (r * MF + f) * 2] = v;
-      } else {
-        const float per = p[s.param_idx[r][f] + 1], w = float(M_PI) / per;
-#pragma unroll
-        for (int k = 0; k < kTK; ++k) {
-          const float ad = float(fabs(sx1[(ii0 + 4 * k) * kMaxQ + d] - b));
-          const float u = w * ad, sn = sinf(u);
-          t0 += gp[k] * sn * sn;
-          t1 += gp[k] * ad * sinf(2.f * u);
-        }
-        const float v0 = wave_sum(sc * 4.f * t0 / (ell * ell * ell));
-        const float v1 = wave_sum(sc * 2.f * float(M_PI) * t1 / (ell * ell * per * per));
-        if (lane == 0) {
-          wrow[MC + (r * MF + f) * 2] = v0;
-          wrow[MC + (r * MF + f) * 2 + 1] = v1;
-        }
-      }
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Regime B: lower-triangular tiles of the padded [np, np] covariance, f32 out, + noise on the
-// diagonal, identity on the padding rows/cols (keeps log|K| and the leading block of K^-1).
-// Tile t of the lower triangle -> (I, J), I >= J.
-// ------------------------------------------------------------------------------------------
 __device__ inline void tri_index(int t, int& I, int& J) {
   int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
   while ((r + 1) * (r + 2) / 2 <= t) ++r;
@@ -314,45 +163,220 @@ __device__ inline void tri_index(int t, int& I, int& J) {
   J = t - r * (r + 1) / 2;
 }
 
+// stage the covariates of rows [i0, i0 + 64) and [j0, j0 + 64) (zero beyond n) into LDS.  Layout
+// [dim][slot]: row r of the tile sits at slot (r & 3) * 16 + (r >> 2), so the 16 lanes that read
+// rows 4 tc + c (c fixed) touch 16 consecutive doubles -- conflict-free ds_read_b64 (a row-major
+// [row][dim] image puts those 16 reads on one bank pair: 16-way conflicts).
+constexpr int kMaxQB = 16;  // covariate columns the Regime B kernels stage (spec dims < 16)
+__device__ inline int cov_slot(int r) { return (r & 3) * 16 + (r >> 2); }
+__device__ inline void stage_cov(const double* __restrict__ x, int ldx, int n, int qs, int i0, int j0,
+                                 double* __restrict__ sx1, double* __restrict__ sx2) {
+  for (int e = threadIdx.x; e < kGT * qs; e += 256) {
+    const int r = e / qs, q = e % qs;
+    sx1[q * kGT + cov_slot(r)] = (i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
+    sx2[q * kGT + cov_slot(r)] = (j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
+  }
+}
+
+// sin(pi t) for t = |d| / p >= 0: reduced to pi r, r = t - rint(t) in [-1/2, 1/2] in fp64 (the
+// period is exact), then the native sine (sin^2 has period pi, so the sign flip of the reduction
+// cancels in every use; per_sin2 gives sin(2 pi t) = sin(2 pi r) for the period derivative)
+__device__ inline float per_sin(double t) { return __sinf(float(M_PI) * float(t - rint(t))); }
+__device__ inline float per_sin2(double t) { return __sinf(2.f * float(M_PI) * float(t - rint(t))); }
+
+// factor (kind, dim d, params pf) on the thread's 4 x 4 micro-tile: v[a][c] *= phi(x_i, x_j)
+__device__ inline void apply_factor(int kind, int d, const float* __restrict__ pf, const double* __restrict__ sx1,
+                                    const double* __restrict__ sx2, int tr, int tc, float (&v)[4][4]) {
+  double xr[4], xc[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xc[c] = sx2[d * kGT + c * 16 + tc];
+  if (kind == LVAE_CAT) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] == xc[c]) ? v[a][c] : 0.f;
+  } else if (kind == LVAE_BIN) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] + xc[c] == 2.0) ? v[a][c] : 0.f;
+  } else if (kind == LVAE_RBF) {
+    const float ell = pf[0], cf = -0.5f * kLog2e / (ell * ell);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float df = float(xr[a] - xc[c]);
+        v[a][c] *= __builtin_amdgcn_exp2f(cf * df * df);
+      }
+  } else if (kind == LVAE_PER) {
+    const float ell = pf[0], cf = -2.f * kLog2e / (ell * ell);
+    const double ip = 1.0 / (double)pf[1];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float sn = per_sin(fabs(xr[a] - xc[c]) * ip);
+        v[a][c] *= __builtin_amdgcn_exp2f(cf * sn * sn);
+      }
+  } else {  // LVAE_LIN
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[a][c] *= float(xr[a] * xc[c]);
+  }
+}
+
+// the adjoint's per-factor sums over the micro-tile: u0 = sum v d^2 (RBF) or sum v sin^2 u (PER),
+// u1 = sum v |d| sin 2u (PER); the ingredients are recomputed so only v stays live
+__device__ inline void factor_sums(int kind, int d, const float* __restrict__ pf, const double* __restrict__ sx1,
+                                   const double* __restrict__ sx2, int tr, int tc, const float (&v)[4][4], float& u0,
+                                   float& u1) {
+  double xr[4], xc[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xc[c] = sx2[d * kGT + c * 16 + tc];
+  u0 = u1 = 0.f;
+  if (kind == LVAE_RBF) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float df = float(xr[a] - xc[c]);
+        u0 += v[a][c] * df * df;
+      }
+  } else {  // LVAE_PER
+    const double ip = 1.0 / (double)pf[1];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double ad = fabs(xr[a] - xc[c]), t = ad * ip;
+        const float sn = per_sin(t);
+        u0 += v[a][c] * sn * sn;
+        u1 += v[a][c] * float(ad) * per_sin2(t);
+      }
+  }
+}
+
+// covariate prefetch: each thread carries up to kPre (row, dim) values of the next tile's two
+// row blocks in registers while the current tile is evaluated
+constexpr int kPre = (kGT * kMaxQB + 255) / 256;
+struct CovPrefetch {
+  double a[kPre], b[kPre];
+  __device__ inline void load(const double* __restrict__ x, int ldx, int n, int qs, int i0, int j0) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int e = threadIdx.x + 256 * u, r = e / qs, q = e % qs;
+      const bool ok = e < kGT * qs;
+      a[u] = (ok && i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
+      b[u] = (ok && j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
+    }
+  }
+  __device__ inline void store(int qs, double* __restrict__ sx1, double* __restrict__ sx2) const {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int e = threadIdx.x + 256 * u, r = e / qs, q = e % qs;
+      if (e < kGT * qs) {
+        sx1[q * kGT + cov_slot(r)] = a[u];
+        sx2[q * kGT + cov_slot(r)] = b[u];
+      }
+    }
+  }
+};
+
+// Lower 64-tiles of the padded [np, np] covariance, f32 out, + noise on the diagonal, identity on
+// the padding rows / cols (keeps log|K| and the leading block of K^-1).  Grid (G, L): workgroup g
+// of dim l fills the tiles t = g, g + G, ... (t -> (I, J), I >= J), prefetching the next tile's
+// covariates under the current tile's arithmetic.  HBM-write-bound: 4 B per element.
 template <int MC, int MF>
 __global__ __launch_bounds__(256) void gram_sq_fill_kernel(DevSpec s, const double* __restrict__ x, int ldx,
                                                            int n, int np_, int qs,
                                                            const double* __restrict__ params,
                                                            const double* __restrict__ noise,
-                                                           float* __restrict__ K) {
-  __shared__ double sx1[kGT * kMaxQ];
-  __shared__ double sx2[kGT * kMaxQ];
+                                                           float* __restrict__ K, int ntiles) {
+  __shared__ double sx1[kGT * kMaxQB];
+  __shared__ double sx2[kGT * kMaxQB];
   __shared__ float sp[64];
-  int I, J;
-  tri_index(blockIdx.x, I, J);
-  const int l = blockIdx.y, tid = threadIdx.x;
-  const int i0 = I * kGT, j0 = J * kGT;
+  const int G = gridDim.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
   if (tid < s.n_params) sp[tid] = float(params[(int64_t)l * s.n_params + tid]);
-  for (int e = tid; e < kGT * qs; e += 256) {
-    const int r = e / qs, q = e % qs;
-    sx1[r * kMaxQ + q] = (i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
-    sx2[r * kMaxQ + q] = (j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
-  }
-  __syncthreads();
   const float nz = float(noise[l]);
-  const int jj = tid & 63, j = j0 + jj, w = tid >> 6;
-  float v[kTK];
-  tile_kernel_f32<MC, MF>(s, sx1, w, &sx2[jj * kMaxQ], sp, v);
   float* o = K + (int64_t)l * np_ * np_;
+  int t = blockIdx.x, I, J;
+  if (t >= ntiles) return;
+  tri_index(t, I, J);
+  CovPrefetch pf;
+  pf.load(x, ldx, n, qs, I * kGT, J * kGT);
+  pf.store(qs, sx1, sx2);
+  __syncthreads();
+  for (; t < ntiles; t += G) {
+    const int i0 = I * kGT, j0 = J * kGT;
+    int In = 0, Jn = 0;
+    const bool more = t + G < ntiles;
+    if (more) {
+      tri_index(t + G, In, Jn);
+      pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
+    }
+    float out[4][4] = {};
+#pragma unroll 1
+    for (int r = 0; r < s.n_comp; ++r) {  // (rolled: the spec is uniform; keeps the live set small)
+      float v[4][4];
+      const float sc = sp[s.scale_idx[r]];
 #pragma unroll
-  for (int k = 0; k < kTK; ++k) {
-    const int i = i0 + w + 4 * k;
-    float e = v[k];
-    if (i == j) e += nz;
-    if (i >= n || j >= n) e = (i == j) ? 1.0f : 0.0f;
-    o[(int64_t)i * np_ + j] = e;
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[a][c] = sc;
+#pragma unroll 1
+      for (int f = 0; f < s.n_fac[r]; ++f) {
+        const int pi = s.param_idx[r][f];
+        apply_factor(s.kind[r][f], s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[a][c] += v[a][c];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int i = i0 + 4 * tr + a;
+      g_f32x4 w;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = j0 + 4 * tc + c;
+        float e = out[a][c];
+        if (i == j) e += nz;
+        if (i >= n || j >= n) e = (i == j) ? 1.0f : 0.0f;
+        w[c] = e;
+      }
+      *reinterpret_cast<g_f32x4*>(o + (int64_t)i * np_ + j0 + 4 * tc) = w;
+    }
+    if (more) {
+      __syncthreads();  // every reader of this tile's covariates is done
+      pf.store(qs, sx1, sx2);
+      __syncthreads();
+      I = In, J = Jn;
+    }
   }
 }
 
-// Fused adjoint for the exact KL: per lower 64x64 tile, G = 1/2 (Kinv - S - a a^T) is formed on the
-// fly from the symmetric K^-1 (f32), S = K^-1 V K^-1 (f32, lower tiles) and a = K^-1 mu (f64);
-// per-slot partial sums of sum_ij w_ij G_ij dK_ij/dtheta go to part[l][tile][slot]
-// (w = 2 strictly below the diagonal, 1 on it).  Slot NS-1 holds sum_i G_ii (noise).
+// Fused adjoint for the exact KL: G = 1/2 (Kinv - S - a a^T) formed on the fly from the symmetric
+// K^-1 (f32), S = K^-1 V K^-1 (f32, lower tiles) and a = K^-1 mu (f64), contracted with dK/dtheta.
+// Grid (G, L): workgroup g of dim l loops over the lower 64-tiles t = g, g + G, ...; every thread
+// keeps fp32 sums per PARAMETER (one slot per parameter -- each has exactly one -- plus the noise
+// slot kNoiseSlot) in its private LDS column over 4 tiles (64 elements), then folds the wave sums
+// into fp64 LDS accumulators; one partial per (dim, slot, workgroup) -> part[l][slot][g].  Raw sums
+// (kl_gram_bwd_reduce applies the per-parameter constants):
+//   scale s_r           sum w g prod_r                              (d k / d s_r = prod_r)
+//   RBF lengthscale     sum w g k_r d^2                              x 1 / l^3
+//   PER l / period      sum w g k_r sin^2 u,  sum w g k_r |d| sin 2u  x 4 / l^3,  2 pi / (l^2 p^2)
+//   noise               sum_i G_ii
+// with k_r = s_r prod_r and w = 2 strictly below the diagonal, 1 on it.
+constexpr int kNoiseSlot = 64;
+constexpr int kBwdSlots = 65;
+
 template <int MC, int MF>
 __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double* __restrict__ x, int ldx, int n,
                                                          int np_, int qs, const double* __restrict__ params,
@@ -360,76 +384,142 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
                                                          const float* __restrict__ S,
                                                          const double* __restrict__ alpha,
                                                          double* __restrict__ part, int ntiles) {
-  constexpr int NS = MC + MC * MF * 2 + 1;
-  __shared__ double sx1[kGT * kMaxQ];
-  __shared__ double sx2[kGT * kMaxQ];
+  __shared__ double sx1[kGT * kMaxQB];
+  __shared__ double sx2[kGT * kMaxQB];
   __shared__ float sp[64];
-  __shared__ double sa1[kGT], sa2[kGT];
-  int I, J;
-  tri_index(blockIdx.x, I, J);
-  const int l = blockIdx.y, tid = threadIdx.x;
-  const int i0 = I * kGT, j0 = J * kGT;
-  if (tid < s.n_params) sp[tid] = float(params[(int64_t)l * s.n_params + tid]);
-  for (int e = tid; e < kGT * qs; e += 256) {
-    const int r = e / qs, q = e % qs;
-    sx1[r * kMaxQ + q] = (i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
-    sx2[r * kMaxQ + q] = (j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
-  }
-  if (tid < kGT) sa1[tid] = alpha[(int64_t)l * np_ + i0 + tid];
-  else if (tid < 2 * kGT) sa2[tid - kGT] = alpha[(int64_t)l * np_ + j0 + tid - kGT];
-  __shared__ double wred[4][NS];
-  for (int e = tid; e < 4 * NS; e += 256) (&wred[0][0])[e] = 0.0;
-  __syncthreads();
-  float dd = 0.f;
-  const int jj = tid & 63, j = j0 + jj, wv = tid >> 6;
+  __shared__ float sa1[kGT], sa2[kGT];
+  __shared__ double wred[4][kBwdSlots];
+  // per-thread fp32 sums (thread-private columns: no races): slots 0..n_params-1, then the noise
+  // at row n_params (dynamic LDS: (n_params + 1) x 256 floats)
+  extern __shared__ float tacc_dyn[];
+  const int G = gridDim.x, g0 = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  const int lane = tid & 63, wv = tid >> 6, np_s = s.n_params;
+  auto tacc = [&](int q) -> float& { return tacc_dyn[(q == kNoiseSlot ? np_s : q) * 256 + tid]; };
+  if (tid < np_s) sp[tid] = float(params[(int64_t)l * np_s + tid]);
+  for (int e = tid; e < 4 * kBwdSlots; e += 256) (&wred[0][0])[e] = 0.0;
+  for (int q = 0; q < np_s; ++q) tacc(q) = 0.f;
+  tacc(kNoiseSlot) = 0.f;
   const float* ki = Kinv + (int64_t)l * np_ * np_;
   const float* si = S + (int64_t)l * np_ * np_;
-  float g[kTK];
+  float dd = 0.f;
+  int since_flush = 0;
+  for (int t = g0; t < ntiles; t += G) {
+    int I, J;
+    tri_index(t, I, J);
+    const int i0 = I * kGT, j0 = J * kGT;
+    // this tile's K^-1 / S rows first: their latency overlaps the covariate staging and barriers
+    g_f32x4 kv4[4], sv4[4];
 #pragma unroll
-  for (int k = 0; k < kTK; ++k) {
-    const int ii = wv + 4 * k, i = i0 + ii;
-    const int64_t o = (int64_t)i * np_ + j;
-    float gv = 0.5f * (ki[o] - si[o] - float(sa1[ii] * sa2[jj]));
-    const bool in = i < n && j < n && j <= i;
-    if (i == j && in) dd += gv;
-    g[k] = in ? ((i == j) ? gv : 2.f * gv) : 0.f;
-  }
-  // per-slot wave sums land in wred[wave][slot] (unused slots stay 0) -> 4-wave sum per tile
-  const int lane = tid & 63;
-  tile_kernel_grad_f32<MC, MF>(s, sx1, wv, &sx2[jj * kMaxQ], sp, g, wred[wv], lane);
-  {
-    const float v = wave_sum(dd);
-    if (lane == 0) wred[wv][NS - 1] = v;
+    for (int a = 0; a < 4; ++a) {
+      const int64_t o = (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc;
+      kv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(ki + o));
+      sv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(si + o));
+    }
+    __syncthreads();  // previous tile's LDS readers done
+    stage_cov(x, ldx, n, qs, i0, j0, sx1, sx2);
+    if (tid < kGT) sa1[tid] = float(alpha[(int64_t)l * np_ + i0 + tid]);
+    else if (tid < 2 * kGT) sa2[tid - kGT] = float(alpha[(int64_t)l * np_ + j0 + tid - kGT]);
+    __syncthreads();
+    float g[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int i = i0 + 4 * tr + a;
+      const g_f32x4 kv = kv4[a], sv = sv4[a];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = j0 + 4 * tc + c;
+        const float gv = 0.5f * (kv[c] - sv[c] - sa1[4 * tr + a] * sa2[4 * tc + c]);
+        const bool in = i < n && j < n && j <= i;
+        if (in && i == j) dd += gv;
+        g[a][c] = in ? ((i == j) ? gv : 2.f * gv) : 0.f;
+      }
+    }
+#pragma unroll 1
+    for (int r = 0; r < s.n_comp; ++r) {
+      float v[4][4];
+      const float sc = sp[s.scale_idx[r]];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[a][c] = g[a][c];
+#pragma unroll 1
+      for (int f = 0; f < s.n_fac[r]; ++f) {
+        const int pi = s.param_idx[r][f];
+        apply_factor(s.kind[r][f], s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
+      }
+      // v = g prod_r: the scale's slot; g k_r = sc v for the parametrised factors
+      float ssum = 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ssum += v[a][c];
+      tacc(s.scale_idx[r]) += ssum;
+#pragma unroll 1
+      for (int f = 0; f < s.n_fac[r]; ++f) {
+        const int kind = s.kind[r][f];
+        if (kind == LVAE_RBF || kind == LVAE_PER) {
+          const int pi = s.param_idx[r][f];
+          float u0, u1;
+          factor_sums(kind, s.dim[r][f], sp + pi, sx1, sx2, tr, tc, v, u0, u1);
+          tacc(pi) += sc * u0;
+          if (kind == LVAE_PER) tacc(pi + 1) += sc * u1;
+        }
+      }
+    }
+    if (++since_flush == 4 || t + G >= ntiles) {  // fold the fp32 sums into the fp64 wave slots
+      since_flush = 0;
+      tacc(kNoiseSlot) += dd;
+      dd = 0.f;
+      for (int q = 0; q < kBwdSlots; ++q) {
+        if (q >= np_s && q != kNoiseSlot) continue;  // (uniform)
+        const float w = wave_sum(tacc(q));
+        if (lane == 0) wred[wv][q] += (double)w;
+        tacc(q) = 0.f;
+      }
+    }
   }
   __syncthreads();
-  for (int sl = tid; sl < NS; sl += 256)
-    part[((int64_t)l * NS + sl) * ntiles + blockIdx.x] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
+  for (int sl = tid; sl < kBwdSlots; sl += 256)
+    part[((int64_t)l * kBwdSlots + sl) * G + g0] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
 }
 
-// Reduce the tile partials: dparams[l, p(slot)] = gkl[l] * sum over tiles, dnoise[l] (slot NS-1).
-// Partials are laid out [l][slot][tile] (coalesced sums); one workgroup per (slot, l).  Every
-// parameter has exactly one slot (slot_param is injective), so the writes never collide.
-template <int MC, int MF>
-__global__ __launch_bounds__(256) void kl_gram_bwd_reduce(DevSpec s, const double* __restrict__ part, int ntiles,
+// per-parameter derivative constants of kl_gram_bwd_tiles' raw sums (host-built from the spec):
+// type 0 scale (1), 1 RBF lengthscale (1 / l^3), 2 PER lengthscale (4 / l^3), 3 PER period
+// (2 pi / (l^2 p^2), l at index ell[p])
+struct BwdParamInfo {
+  int8_t type[64];
+  int8_t ell[64];
+};
+
+// dparams[l, p] = gkl[l] c_p sum_g part[l][p][g]; dnoise[l] from kNoiseSlot.  Grid (n_params + 1, L).
+__global__ __launch_bounds__(256) void kl_gram_bwd_reduce(BwdParamInfo pinfo, int n_params,
+                                                          const double* __restrict__ part, int G,
+                                                          const double* __restrict__ params,
                                                           const double* __restrict__ gkl,
                                                           double* __restrict__ dparams,
                                                           double* __restrict__ dnoise) {
-  constexpr int NS = MC + MC * MF * 2 + 1;
   __shared__ double red[4];
-  const int slot = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
-  const int pi = slot == NS - 1 ? -2 : slot_param<MC, MF>(s, slot);
-  if (pi == -1) return;  // an unused slot (uniform over the workgroup)
-  const double* p = part + ((int64_t)l * NS + slot) * ntiles;
+  const int b = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+  const int slot = b == n_params ? kNoiseSlot : b;
+  const double* p = part + ((int64_t)l * kBwdSlots + slot) * G;
   double v = 0.0;
-  for (int t = tid; t < ntiles; t += 256) v += p[t];
+  for (int t = tid; t < G; t += 256) v += p[t];
   v = block_sum<256>(v, red);
-  if (tid == 0) {
-    if (pi == -2) {
-      if (dnoise) dnoise[l] = gkl[l] * v;
-    } else {
-      dparams[(int64_t)l * s.n_params + pi] = gkl[l] * v;
-    }
+  if (tid != 0) return;
+  if (slot == kNoiseSlot) {
+    if (dnoise) dnoise[l] = gkl[l] * v;
+    return;
   }
+  const double* pl = params + (int64_t)l * n_params;
+  double c = 1.0;
+  const int ty = pinfo.type[b];
+  if (ty == 1) c = 1.0 / (pl[b] * pl[b] * pl[b]);
+  else if (ty == 2) c = 4.0 / (pl[b] * pl[b] * pl[b]);
+  else if (ty == 3) {
+    const double ell = pl[pinfo.ell[b]];
+    c = 2.0 * M_PI / (ell * ell * pl[b] * pl[b]);
+  }
+  dparams[(int64_t)l * n_params + b] = gkl[l] * c * v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -467,21 +557,30 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
                  const double* params, const double* noise, float* K, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
-  if (!bucket || qs > kMaxQ || qs > ldx) return -1;
+  if (!bucket || qs > kMaxQB || qs > ldx) return -1;
   const DevSpec ds = to_dev(spec);
-  const int nt = np_ / kGT;
-  dim3 grid(nt * (nt + 1) / 2, L);
+  const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2;
+  int G = (2048 + L - 1) / L;  // ~8 resident workgroups per CU, 2 rounds
+  G = G < ntiles ? G : ntiles;
+  dim3 grid(G, L);
   if (bucket == 1)
-    gram_sq_fill_kernel<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K);
+    gram_sq_fill_kernel<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles);
   else
-    gram_sq_fill_kernel<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K);
+    gram_sq_fill_kernel<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
 
+// workgroups per latent dim of the adjoint: ~1536 in all, each looping over ~ntiles / G tiles
+static int kl_gram_bwd_groups(int np_, int L) {
+  const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2;
+  int G = (1536 + L - 1) / L;  // 2 full rounds of 256 CUs x 3 resident workgroups
+  G = G < 8 ? 8 : G;
+  return G < ntiles ? G : ntiles;
+}
+
 size_t kl_gram_bwd_partials_bytes(int np_, int L) {
-  const int nt = np_ / kGT;
-  return (size_t)L * (nt * (nt + 1) / 2) * (16 + 16 * 4 * 2 + 1) * sizeof(double);
+  return (size_t)L * kl_gram_bwd_groups(np_, L) * kBwdSlots * sizeof(double);
 }
 
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
@@ -489,17 +588,29 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
                 double* part, double* dparams, double* dnoise, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
-  if (!bucket || qs > kMaxQ) return -1;
+  if (!bucket || qs > kMaxQB || spec->n_params > 64) return -1;
   const DevSpec ds = to_dev(spec);
-  const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2;
-  dim3 grid(ntiles, L);
-  if (bucket == 1) {
-    kl_gram_bwd_tiles<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part, ntiles);
-    kl_gram_bwd_reduce<8, 2><<<dim3(8 + 8 * 2 * 2 + 1, L), 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
-  } else {
-    kl_gram_bwd_tiles<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part, ntiles);
-    kl_gram_bwd_reduce<16, 4><<<dim3(16 + 16 * 4 * 2 + 1, L), 256, 0, st>>>(ds, part, ntiles, gkl, dparams, dnoise);
-  }
+  BwdParamInfo pinfo{};
+  for (int r = 0; r < spec->n_comp; ++r)
+    for (int f = 0; f < spec->n_fac[r]; ++f) {
+      const int pi = spec->param_idx[r][f];
+      if (spec->kind[r][f] == LVAE_RBF) pinfo.type[pi] = 1;
+      if (spec->kind[r][f] == LVAE_PER) {
+        pinfo.type[pi] = 2;
+        pinfo.type[pi + 1] = 3;
+        pinfo.ell[pi + 1] = (int8_t)pi;
+      }
+    }
+  const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2, G = kl_gram_bwd_groups(np_, L);
+  const size_t dyn = (size_t)(spec->n_params + 1) * 256 * sizeof(float);
+  if (bucket == 1)
+    kl_gram_bwd_tiles<8, 2><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part,
+                                                           ntiles);
+  else
+    kl_gram_bwd_tiles<16, 4><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part,
+                                                            ntiles);
+  kl_gram_bwd_reduce<<<dim3(spec->n_params + 1, L), 256, 0, st>>>(pinfo, spec->n_params, part, G, params, gkl,
+                                                                  dparams, dnoise);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

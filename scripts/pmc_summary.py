@@ -10,7 +10,7 @@ from collections import defaultdict
 
 def main(out_dir):
     res = {}
-    for path in glob.glob(os.path.join(out_dir, "*", "*counter_collection.csv")):
+    for path in glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True):
         acc = defaultdict(lambda: [0.0, 0])
         counter = None
         with open(path) as f:
@@ -25,9 +25,13 @@ def main(out_dir):
             res.setdefault(c, {})[name] = {"mean": s / n, "dispatches": n}
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
         json.dump(res, f, indent=1)
+    keys = os.environ.get("PMC_KERNELS", "").split(",")
     for c, d in res.items():
-        for name, v in sorted(d.items(), key=lambda kv: -kv[1]["mean"] * kv[1]["dispatches"])[:12]:
-            print(f"{c:12s} {v['mean']:14.1f} x{v['dispatches']:4d}  {name[:100]}")
+        items = sorted(d.items(), key=lambda kv: -kv[1]["mean"] * kv[1]["dispatches"])
+        if keys != [""]:
+            items = [kv for kv in items if any(k in kv[0] for k in keys)]
+        for name, v in items[:12]:
+            print(f"{c:24s} {v['mean']:16.1f} x{v['dispatches']:4d}  {name[:90]}")
 
 
 if __name__ == "__main__":
