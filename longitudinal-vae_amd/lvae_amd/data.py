@@ -68,6 +68,9 @@ class HealthMNISTDatasetConv:
         self.pixels = torch.from_numpy(data).to(self.device)   # [N, 1296] uint8
         self.masks = torch.from_numpy(mask).to(self.device)    # [N, 1296] uint8
         self.labels = torch.from_numpy(lab).to(self.device)    # [N, 6] fp32
+        # ToTensor's uint8 / 255 as a 256-entry table computed on the host: a device fp32 division
+        # need not round like the host's, a table gather is bit-exact
+        self.lut = (torch.arange(256, dtype=torch.float32) / 255.0).to(self.device)
 
     def __len__(self):
         return self.pixels.shape[0]
@@ -88,7 +91,7 @@ class HealthMNISTDatasetConv:
         """Device batch for row indices ``idx``: digit [B,1,36,36] fp32 (= ToTensor: uint8 / 255),
         label [B,6] fp32, mask [B,1,1296] uint8 (as the default collate of the reference items)."""
         idx = torch.as_tensor(idx, dtype=torch.int64, device=self.device)
-        digit = self.pixels.index_select(0, idx).reshape(-1, 1, 36, 36).to(torch.float32).div_(255.0)
+        digit = self.lut[self.pixels.index_select(0, idx).to(torch.int64)].reshape(-1, 1, 36, 36)
         return {"digit": digit, "label": self.labels.index_select(0, idx), "idx": idx,
                 "mask": self.masks.index_select(0, idx).reshape(-1, 1, 1296)}
 

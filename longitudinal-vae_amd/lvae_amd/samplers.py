@@ -2,11 +2,20 @@
 
 A Hensman batch is P_b whole subjects: a shuffled subject order, each subject's T rows kept
 contiguous, cut into batches of P_b*T rows (BatchSampler(SubjectSampler, P_b*T, drop_last=False)).
-The reference draws the order with an unseeded np.random.shuffle (utils.py:53); here the order is
-an explicit, seedable permutation so runs are reproducible and ranks agree on it.
+The reference draws the order with np.random.shuffle on NumPy's global legacy state (utils.py:53,
+76).  seed=None keeps exactly that (so np.random.seed(s) reproduces the reference's orders bit for
+bit, tests/golden/samplers.npz); an explicit seed gives a private generator, so data-parallel
+ranks agree on the order without touching global state.
 """
 import numpy as np
 import torch
+
+
+def _shuffler(seed):
+    """In-place shuffle: NumPy's global legacy np.random.shuffle (the reference's) for seed=None."""
+    if seed is None:
+        return np.random.shuffle
+    return np.random.default_rng(seed).shuffle
 
 
 class SubjectSampler:
@@ -14,11 +23,11 @@ class SubjectSampler:
 
     def __init__(self, P, T, seed=None):
         self.P, self.T = P, T
-        self.rng = np.random.default_rng(seed)
+        self.shuffle = _shuffler(seed)
 
     def permutation(self):
         r = np.arange(self.P)
-        self.rng.shuffle(r)
+        self.shuffle(r)
         return r
 
     def __iter__(self):
@@ -49,20 +58,21 @@ def hensman_batches(perm, P_b, T, rank=0, world=1):
 
 
 class VaryingLengthSubjectSampler:
-    """(row, subject) pairs in shuffled subject order for subjects of varying length (utils.py:61-87);
-    subjects are contiguous runs of the id column."""
+    """(row, subject) pairs in shuffled subject order for subjects of varying length (utils.py:61-87).
+    As the reference: subject s (in order of first appearance of its id) spans rows from its first
+    occurrence to the next subject's first occurrence (contiguous runs in Health-MNIST files)."""
 
     def __init__(self, subject_ids, seed=None):
-        ids = np.asarray(subject_ids)
-        change = np.flatnonzero(np.r_[True, ids[1:] != ids[:-1]])
-        self.start = change
-        self.end = np.r_[change[1:], len(ids)]
-        self.P = len(change)
-        self.rng = np.random.default_rng(seed)
+        ids = np.asarray(subject_ids).astype(np.int64)
+        _, first = np.unique(ids, return_index=True)
+        self.start = np.sort(first)
+        self.end = np.r_[self.start[1:], len(ids)]
+        self.P = len(self.start)
+        self.shuffle = _shuffler(seed)
 
     def __iter__(self):
         r = np.arange(self.P)
-        self.rng.shuffle(r)
+        self.shuffle(r)
         for s in r:
             for i in range(self.start[s], self.end[s]):
                 yield i, s

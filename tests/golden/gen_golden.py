@@ -7,6 +7,7 @@ The reference is imported read-only with the harness shims SURVEY.md §8(c) list
   * ``torchvision`` stub (``transforms`` is only used for dataset construction),
   * ``torch.solve`` (removed in torch 2.x; used at elbo_functions.py:75,129),
   * ``np.Inf`` (training.py:82),
+  * ``Sampler.__init__`` accepting the data_source argument utils.py:46 passes (torch 2.x),
   * kernel adapter: GP_model.py kernels left-align their ``[L]`` parameters while gpytorch
     (the path LVAE.py really runs, kernel_gen.py:199-310) right-aligns ``batch_shape=[L]``;
     for 4-D inputs the adapter evaluates ``k(a.T01, b.T01).T01`` which is the gpytorch
@@ -35,6 +36,8 @@ def _install_shims():
     sys.modules.setdefault("torchvision", tv)
     sys.modules.setdefault("torchvision.transforms", tv.transforms)
     torch.solve = lambda B, A: (torch.linalg.solve(A, B), None)  # present-but-raising in torch 2.x
+    # utils.py:46 passes data_source to Sampler.__init__, which torch 2.x rejects
+    torch.utils.data.sampler.Sampler.__init__ = lambda self, data_source=None: None
     if not hasattr(np, "Inf"):
         np.Inf = np.inf
     sys.dont_write_bytecode = True
@@ -118,6 +121,29 @@ CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
            bin_int_kernel=[], covariate_missing_val=[], id_covariate=2)
 
 
+# a config exercising every builder branch the sample config leaves out (GP_model.py:146-236):
+# bin_kernel, bin_int_kernel and covariate_missing_val mask products on a Cat, an Rbf (also inside
+# the interaction kernels) and the Cat of an id-free Cat x Rbf.  Columns 6 / 7 are the masks of
+# time_age / gender (covariates_missing below).
+VAR_CFG = dict(cat_kernel=[2, 3], bin_kernel=[5], sqexp_kernel=[0],
+               cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                               {'cont_covariate': 1, 'cat_covariate': 4}],
+               bin_int_kernel=[{'cont_covariate': 0, 'bin_covariate': 4}],
+               covariate_missing_val=[{'covariate': 0, 'mask': 6}, {'covariate': 3, 'mask': 7}], id_covariate=2)
+
+
+def covariates_missing(P, T, seed):
+    """covariates() plus mask columns 6 (time_age observed, per row) and 7 (gender observed, per
+    subject); a missing value is stored as 0 (dataset_def.py:213 fills NaN with 0)."""
+    rng = np.random.default_rng(seed + 1000)
+    X = covariates(P, T, seed)
+    m_age = rng.binomial(1, 0.8, size=P * T).astype(np.float64)
+    m_gen = np.repeat(rng.binomial(1, 0.85, size=P).astype(np.float64), T)
+    X[:, 0] *= m_age
+    X[:, 3] *= m_gen
+    return np.concatenate([X, m_age[:, None], m_gen[:, None]], 1)
+
+
 def full_kernel_ref(L):
     """The non-split additive kernel in kernel_gen.generate_kernel order (kernel_gen.py:28-92),
     built from the reference's own gpytorch-free GP_model classes."""
@@ -166,16 +192,23 @@ def save(name, **arrs):
 # ----------------------------------------------------------------------------------------------
 # 1. KL_closed (elbo_functions.py:8-34), per latent dim, value + autograd grads
 # ----------------------------------------------------------------------------------------------
-def gen_kl_closed(P, T, L, seed, noise, store_gram):
+def gen_kl_closed(P, T, L, seed, noise, store_gram, variants=False):
     rng = np.random.default_rng(seed)
-    X = covariates(P, T, seed)
+    X = covariates_missing(P, T, seed) if variants else covariates(P, T, seed)
     N = P * T
     mu = rng.standard_normal((N, L))
     logv = 0.1 * rng.standard_normal((N, L))
     out = dict(X=X, mu=mu, logv=logv, noise=np.full(L, noise), P=P, T=T, L=L)
     kls, dmus, dlogvs, draws, grams, rawvals = [], [], [], [], [], []
     for l in range(L):
-        k = full_kernel_ref(1)
+        if variants:  # the per-dim kernel as (non-id components, id components) of the builder
+            c = dict(VAR_CFG)
+            k0, k1 = R.generate_kernel_batched(1, c['cat_kernel'], c['bin_kernel'], c['sqexp_kernel'],
+                                               c['cat_int_kernel'], c['bin_int_kernel'],
+                                               c['covariate_missing_val'], c['id_covariate'])
+            k = R.AdditiveKernel(list(k0.kernels) + list(k1.kernels))
+        else:
+            k = full_kernel_ref(1)
         randomise(k, rng)
         names, vals = raw_params(k)
         rawvals.append(np.concatenate(vals))
@@ -202,17 +235,18 @@ def gen_kl_closed(P, T, L, seed, noise, store_gram):
 # ----------------------------------------------------------------------------------------------
 # 2. minibatch_KLD_upper_bound (elbo_functions.py:144-216) + _iter (219-307)
 # ----------------------------------------------------------------------------------------------
-def batched_kernels(L):
-    return R.generate_kernel_batched(L, CFG['cat_kernel'], CFG['bin_kernel'], CFG['sqexp_kernel'],
-                                     CFG['cat_int_kernel'], CFG['bin_int_kernel'],
-                                     CFG['covariate_missing_val'], CFG['id_covariate'])
+def batched_kernels(L, cfg=None):
+    c = cfg or CFG
+    return R.generate_kernel_batched(L, c['cat_kernel'], c['bin_kernel'], c['sqexp_kernel'],
+                                     c['cat_int_kernel'], c['bin_int_kernel'],
+                                     c['covariate_missing_val'], c['id_covariate'])
 
 
-def gen_hensman(P_tot, T, L, M, P_b, seed, natural_gradient, benign=False, noise=1.0):
+def gen_hensman(P_tot, T, L, M, P_b, seed, natural_gradient, benign=False, noise=1.0, variants=False):
     rng = np.random.default_rng(seed)
-    X = covariates(P_tot, T, seed)
+    X = covariates_missing(P_tot, T, seed) if variants else covariates(P_tot, T, seed)
     N = P_tot * T
-    k0, k1 = batched_kernels(L)
+    k0, k1 = batched_kernels(L, VAR_CFG if variants else None)
     randomise(k0, rng)
     randomise(k1, rng)
     perm = rng.permutation(P_tot)[:P_b]
@@ -236,6 +270,12 @@ def gen_hensman(P_tot, T, L, M, P_b, seed, natural_gradient, benign=False, noise
     noise_v = np.full((L, 1), noise)
     out = dict(X_all=X, idx=idx, Z=Z, mu=mu, logv=logv, m=m, H=H, noise=noise_v, P_tot=P_tot,
                P_b=P_b, T=T, L=L, M=M, natural_gradient=int(natural_gradient), eps=1e-6)
+    if variants:  # the Grams of the call convention elbo_functions.py:171-174 (right-aligned batch)
+        with torch.no_grad():
+            xs = torch.tensor(xb).reshape(P_b, 1, T, -1).expand(P_b, L, T, xb.shape[1])
+            out.update(K0xz=KernelAdapter(k0)(torch.tensor(xb), torch.tensor(Z)).evaluate().numpy().copy(),
+                       K0zz=KernelAdapter(k0)(torch.tensor(Z), torch.tensor(Z)).evaluate().numpy().copy(),
+                       K1_st=KernelAdapter(k1)(xs, xs).evaluate().numpy().copy())
     n0, v0 = raw_params(k0)
     n1, v1 = raw_params(k1)
     out.update(raw0=np.stack(v0, 0), raw1=np.stack(v1, 0), names0=np.array(n0), names1=np.array(n1))
@@ -472,7 +512,153 @@ def gen_hmnist_tiny(seed):
                 n=len(ds))
 
 
-def main():
+# ----------------------------------------------------------------------------------------------
+# 6. samplers (utils.py:40-113) under np.random.seed: the row orders the reference draws
+# ----------------------------------------------------------------------------------------------
+class _ListDS:
+    def __init__(self, labels):
+        self.labels = labels
+
+    def __len__(self):
+        return len(self.labels)
+
+    def __getitem__(self, i):
+        return {"label": torch.tensor(self.labels[i])}
+
+
+def gen_samplers(seed):
+    import utils as RU  # noqa: E402  (reference)
+    from torch.utils.data.sampler import BatchSampler
+    P, T, P_b = 11, 4, 3
+    ds = _ListDS(np.zeros((P * T, 6)))
+    np.random.seed(seed)
+    ss = RU.SubjectSampler(ds, P, T)
+    epochs = [np.array(list(iter(ss))) for _ in range(3)]
+    batches = [np.array(b) for b in BatchSampler(ss, P_b * T, drop_last=False)]
+    # varying length: subject ids in contiguous runs of lengths 1..5 (plus one id reappearing
+    # later, which the reference indexes by first occurrence)
+    lengths = [3, 1, 5, 2, 4, 3, 2]
+    ids = np.concatenate([np.full(n, 10 + i) for i, n in enumerate(lengths)]).astype(np.float64)
+    lab = np.zeros((len(ids), 6))
+    lab[:, 2] = ids
+    vds = _ListDS(lab)
+    np.random.seed(seed + 1)
+    vs = RU.VaryingLengthSubjectSampler(vds, 2)
+    v_pairs = [np.array(list(iter(vs))) for _ in range(2)]
+    v_batches = [np.array(b) for b in RU.VaryingLengthBatchSampler(vs, 3)]
+    return dict(P=P, T=T, P_b=P_b, seed=seed, epochs=np.stack(epochs), batch_lens=np.array([len(b) for b in batches]),
+                batches=np.concatenate(batches), v_ids=ids, v_pairs=np.stack(v_pairs),
+                v_batch_lens=np.array([len(b) for b in v_batches]), v_batches=np.concatenate(v_batches))
+
+
+# ----------------------------------------------------------------------------------------------
+# 7. two epochs of training.hensman_training (training.py:15-237), natural gradient, loss 'mse',
+#    driven with an injected subject order (np.random.seed before the call: SubjectSampler's
+#    np.random.shuffle is the only consumer of that state) and injected reparametrisation noise
+#    (a ConvVAE subclass whose sample_latent reads a fixed eps queue instead of torch.randn_like).
+#    Per step the harness records the batch's subject ids and the KL bound (a recording wrapper
+#    around training.minibatch_KLD_upper_bound) and the recon / nll sums (loss_function wrapper).
+# ----------------------------------------------------------------------------------------------
+def gen_hensman_training(P, T, L, M, P_b, seed, epochs=2):
+    import training as RT  # noqa: E402  (reference)
+    rng = np.random.default_rng(seed)
+    X = covariates(P, T, seed)
+    N = P * T
+    pix = rng.integers(0, 256, size=(N, 1, 36, 36)).astype(np.uint8)
+    msk = rng.binomial(1, 0.75, size=(N, 1, 36, 36)).astype(np.uint8)
+    n_batches = (N + P_b * T - 1) // (P_b * T)
+    EPS = rng.standard_normal((epochs * n_batches, P_b * T, L))
+
+    class DS(torch.utils.data.Dataset):
+        def __len__(self):
+            return N
+
+        def __getitem__(self, i):
+            return {"idx": i, "digit": torch.tensor(pix[i] / 255.0), "label": torch.tensor(X[i]),
+                    "mask": torch.tensor(msk[i].astype(np.float64))}
+
+    rec = {"ids": [], "kld": [], "recon": [], "nll": []}
+
+    class VAE(RV.ConvVAE):
+        step = 0
+
+        def sample_latent(self, mu, log_var):
+            e = torch.tensor(EPS[VAE.step][:mu.shape[0]])
+            VAE.step += 1
+            return mu + e * torch.exp(0.5 * log_var)
+
+        def loss_function(self, recon_x, x, mask):
+            out = super().loss_function(recon_x, x, mask)
+            rec["recon"].append(out[0].sum().item())
+            rec["nll"].append(out[1].sum().item())
+            return out
+
+    model = VAE(L, 1296, vy_init=1.0, p_input=0.0, p=0.0).double()
+    model.load_state_dict(vae_weights(model, seed))
+    k0, k1 = batched_kernels(L)
+    randomise(k0, rng)
+    randomise(k1, rng)
+    half = M // 2
+    zrows = np.concatenate([np.arange(0, half), np.arange(N // 2, N // 2 + half)])
+    Z = np.stack([X[zrows]] * L)
+    m0 = rng.standard_normal((L, M, 1))
+    Hr = rng.standard_normal((L, M, M)) / 10
+    H0 = Hr @ np.transpose(Hr, (0, 2, 1))
+    n0, v0 = raw_params(k0)
+    n1, v1 = raw_params(k1)
+    vae0 = {k: v.numpy().copy() for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam([{"params": k0.parameters()}, {"params": k1.parameters()},
+                            {"params": model.parameters()}], lr=1e-3)
+    orig = RT.minibatch_KLD_upper_bound
+
+    def recording(*a, **kw):
+        out = orig(*a, **kw)
+        rec["ids"].append(a[6][:, 2].numpy().copy())
+        rec["kld"].append(out[0].item())
+        return out
+
+    RT.minibatch_KLD_upper_bound = recording
+    try:
+        np.random.seed(seed)
+        res = RT.hensman_training(model, "conv", epochs, DS(), opt, "GPapprox_closed", 1, L, KernelAdapter(k0),
+                                  KernelAdapter(k1), LikStub(torch.ones(L, 1)), torch.tensor(m0), torch.tensor(H0),
+                                  torch.tensor(Z), P, T, False, 6, 0.15, 2, "mse", natural_gradient=True,
+                                  natural_gradient_lr=0.01, subjects_per_batch=P_b, eps=1e-6)
+    finally:
+        RT.minibatch_KLD_upper_bound = orig
+    _, net_arr, nll_arr, recon_arr, kld_arr, m_fin, H_fin, _ = res
+    np.random.seed(seed)
+    perms = []
+    for _ in range(epochs):
+        r = np.arange(P)
+        np.random.shuffle(r)
+        perms.append(r)
+    ids = np.concatenate(rec["ids"])
+    assert np.array_equal(ids[::T].astype(np.int64), np.concatenate(perms)), "subject order != seeded shuffles"
+    fin = {("vae_" + k): v.detach().numpy().copy() for k, v in model.named_parameters()
+           if k in ("conv1.weight", "fc211.bias", "deconv2.weight", "_log_vy")}
+    fin["vae_fc1_rowsum"] = model.fc1.weight.detach().sum(1).numpy().copy()
+    return dict(P=P, T=T, L=L, M=M, P_b=P_b, seed=seed, epochs=epochs, X=X, pix=pix, msk=msk, eps=EPS, Z=Z,
+                m0=m0, H0=H0, raw0=np.stack(v0, 0), raw1=np.stack(v1, 0), perms=np.stack(perms),
+                step_kld=np.array(rec["kld"]), step_recon=np.array(rec["recon"]), step_nll=np.array(rec["nll"]),
+                epoch_net=net_arr, epoch_recon=recon_arr, epoch_nll=nll_arr, epoch_kld=kld_arr,
+                m_final=m_fin.numpy().copy(), H_final=H_fin.numpy().copy(),
+                raw0_final=np.stack(raw_params(k0)[1], 0), raw1_final=np.stack(raw_params(k1)[1], 0), **fin)
+
+
+def main(only=None):
+    jobs = {
+        "kernel_variants_kl.npz": lambda: gen_kl_closed(P=5, T=16, L=2, seed=12, noise=0.9, store_gram=True,
+                                                        variants=True),
+        "kernel_variants_hensman.npz": lambda: gen_hensman(P_tot=24, T=16, L=3, M=40, P_b=4, seed=13,
+                                                           natural_gradient=True, variants=True),
+        "samplers.npz": lambda: gen_samplers(seed=14),
+        "hensman_training_2ep.npz": lambda: gen_hensman_training(P=8, T=16, L=2, M=20, P_b=3, seed=15),
+    }
+    if only:
+        for name in only:
+            save(name, **jobs[name]())
+        return
     save("kl_closed_n64.npz", **gen_kl_closed(P=4, T=16, L=2, seed=0, noise=1.0, store_gram=True))
     save("kl_closed_n256.npz", **gen_kl_closed(P=16, T=16, L=2, seed=1, noise=1.0, store_gram=False))
     save("kl_closed_n96_noise.npz", **gen_kl_closed(P=6, T=16, L=1, seed=2, noise=0.7, store_gram=False))
@@ -493,5 +679,9 @@ def main():
                                               test_subjects=[3, 0, 7, 10], test_lengths=[6, 4, 10, 3]))
 
 
+    for name, job in jobs.items():
+        save(name, **job())
+
+
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

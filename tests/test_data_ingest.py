@@ -5,6 +5,7 @@ the samplers' index order.  Bit-exact: uint8 pixels / masks, fp32 labels."""
 import os
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import GOLDEN, golden
@@ -54,3 +55,24 @@ def test_loader_follows_subject_batches():
         subj = b["label"][:, 2].to(torch.int64)
         # each batch holds whole subjects, rows contiguous per subject, in the permutation order
         assert torch.equal(subj, torch.as_tensor(np.repeat(perm[:P_b] if b is out[0] else perm[P_b:], T)))
+
+
+@pytest.mark.gpu
+def test_device_resident_ingest_on_gpu():
+    """The point of the device-preloaded dataset: CSVs parsed once into HBM,
+    batches are device gathers in the sampler's order -- bit-exact vs the reference's items."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lvae_amd.data import DeviceBatchLoader
+    from lvae_amd.samplers import SubjectSampler, hensman_batches
+    g, ds = _ds(device="cuda")
+    assert ds.pixels.is_cuda and ds.masks.is_cuda and ds.labels.is_cuda
+    perm = SubjectSampler(3, 4, seed=1).permutation()
+    batches = hensman_batches(perm, 2, 4)
+    for b, idx in zip(DeviceBatchLoader(ds, batches), batches):
+        assert b["digit"].is_cuda and b["label"].is_cuda and b["mask"].is_cuda
+        i = idx.numpy()
+        ref = torch.tensor(g["digit"][i]).permute(0, 3, 1, 2).to(torch.float32) / 255.0
+        assert torch.equal(b["digit"].cpu(), ref)
+        assert torch.equal(b["label"].cpu(), torch.tensor(g["label"][i]))
+        assert torch.equal(b["mask"].cpu(), torch.tensor(g["mask"][i]))

@@ -533,3 +533,117 @@ def test_graphed_hensman_step_matches_eager(hip):
     assert rel(graph_step.m, eager.m) < 1e-6 and rel(graph_step.H, eager.H) < 1e-6
     for (n, p), (_, q) in zip(k0_g.named_parameters(), k0_e.named_parameters()):
         assert rel(p, q) < 1e-9, n
+
+
+VAR_CFG = dict(cat_kernel=[2, 3], bin_kernel=[5], sqexp_kernel=[0],
+               cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                               {'cont_covariate': 1, 'cat_covariate': 4}],
+               bin_int_kernel=[{'cont_covariate': 0, 'bin_covariate': 4}],
+               covariate_missing_val=[{'covariate': 0, 'mask': 6}, {'covariate': 3, 'mask': 7}])
+
+
+def test_hensman_kernel_variants_golden(hip):
+    """The Hensman bound with bin / bin x RBF / masked kernels (kernel_variants_hensman.npz): the
+    three Grams of the call convention (elbo_functions.py:171-174) and the bound + gradients."""
+    import lvae_amd as la
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    g = golden("kernel_variants_hensman.npz")
+    L, P_b, T = int(g["L"]), int(g["P_b"]), int(g["T"])
+    k0, k1 = la.generate_kernel_batched(L, **VAR_CFG, id_covariate=2)
+    set_raw(k0, g["raw0"].T)
+    set_raw(k1, g["raw1"].T)
+    k0, k1 = k0.to(DEV), k1.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    lik.noise = torch.tensor(g["noise"][:, 0], device=DEV)
+    X = torch.tensor(g["X_all"][g["idx"]], device=DEV)
+    Z = torch.tensor(g["Z"], device=DEV)
+    with torch.no_grad():
+        xs = X.reshape(P_b, 1, T, -1).expand(P_b, L, T, X.shape[1])
+        assert rel(k0(X, Z).evaluate(), g["K0xz"]) < 1e-13
+        assert rel(k0(Z, Z).evaluate(), g["K0zz"]) < 1e-13
+        assert rel(k1(xs, xs).evaluate(), g["K1_st"]) < 1e-13
+    mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+    lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+    kld, gm, gH = minibatch_KLD_upper_bound(k0, k1, lik, L, torch.tensor(g["m"], device=DEV),
+                                            torch.tensor(g["H"], device=DEV), X, mu, lv, Z, int(g["P_tot"]), P_b, T,
+                                            True, float(g["eps"]))
+    kld.backward()
+    assert rel(kld, g["kld"]) < 1e-8
+    assert rel(mu.grad, g["dmu"]) < 1e-6
+    assert rel(lv.grad, g["dlogv"]) < 1e-6
+    assert rel(torch.stack([p.grad for _, p in k0.named_parameters()]), g["draw0"]) < 1e-6
+    assert rel(torch.stack([p.grad for _, p in k1.named_parameters()]), g["draw1"]) < 1e-4
+    assert rel(gm, g["grad_m"]) < 1e-6
+
+
+class _FixtureImages:
+    """A device-resident dataset over the fixture's arrays with the HealthMNISTDatasetConv batch()
+    interface (digit = uint8 / 255, label, mask), in fp64 as the reference's training casts them."""
+
+    def __init__(self, g):
+        self.pix = torch.tensor(g["pix"], device=DEV)
+        self.msk = torch.tensor(g["msk"], device=DEV)
+        self.lab = torch.tensor(g["X"], device=DEV)
+
+    def __len__(self):
+        return self.lab.shape[0]
+
+    def batch(self, idx):
+        idx = torch.as_tensor(idx, dtype=torch.int64, device=DEV)
+        return {"idx": idx, "digit": self.pix.index_select(0, idx).to(torch.float64) / 255.0,
+                "label": self.lab.index_select(0, idx), "mask": self.msk.index_select(0, idx).to(torch.float64)}
+
+
+def test_hensman_training_two_epochs_vs_reference(hip):
+    """Two epochs of the reference's training.hensman_training (hensman_training_2ep.npz) replayed
+    through the product stack: the drop-in SubjectSampler under the same np.random.seed, torch's
+    BatchSampler, the drop-in HensmanDataLoader (device batches), lvae_amd.HensmanStep (HIP bound,
+    natural-gradient update) and Adam over the same parameter set.  The ConvVAE runs in fp64 here
+    (the reference's dtype) so the comparison is at fp64 tolerances: per-step KL bound and recon
+    sums, and the final (m, H), kernel and network parameters."""
+    import lvae_amd as la
+    from torch.utils.data.sampler import BatchSampler
+    from dropin.utils import HensmanDataLoader, SubjectSampler
+    from lvae_amd.steps import HensmanStep
+    from lvae_amd.vae import ConvVAE
+    g = golden("hensman_training_2ep.npz")
+    P, T, L, P_b = int(g["P"]), int(g["T"]), int(g["L"]), int(g["P_b"])
+    ds = _FixtureImages(g)
+    ref_vae = O.ConvVAE(L).double()
+    ref_vae.load_state_dict(O.vae_weights(ref_vae, int(g["seed"])))
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).double()
+    vae.load_state_dict(ref_vae.state_dict())
+    vae = vae.to(DEV)
+    k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+    set_raw(k0, g["raw0"].T)
+    set_raw(k1, g["raw1"].T)
+    k0, k1 = k0.to(DEV), k1.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+    opt = torch.optim.Adam([{"params": k0.parameters()}, {"params": k1.parameters()},
+                            {"params": vae.parameters()}], lr=1e-3)
+    step = HensmanStep(vae, k0, k1, lik, opt, torch.tensor(g["m0"], device=DEV), torch.tensor(g["H0"], device=DEV),
+                       torch.tensor(g["Z"], device=DEV), P, T, weight=0.15)
+    np.random.seed(int(g["seed"]))
+    loader = HensmanDataLoader(ds, BatchSampler(SubjectSampler(ds, P, T), P_b * T, drop_last=False))
+    s = 0
+    for e in range(int(g["epochs"])):
+        for j, b in enumerate(loader):
+            rows = b["idx"]
+            pb = len(rows) // T
+            # the reference's subject order, bit-exact (np.random.shuffle under the same seed)
+            assert np.array_equal(rows[::T].cpu().numpy() // T, g["perms"][e][j * P_b:j * P_b + pb])
+            eps = torch.tensor(g["eps"][s][:len(rows)], device=DEV)
+            net, recon, nll, kld = step(b["digit"], b["mask"], b["label"], eps)
+            assert rel(kld * L, g["step_kld"][s]) < 1e-7, s
+            assert rel(recon * pb / P, g["step_recon"][s]) < 1e-9, s
+            assert rel(nll * pb / P, g["step_nll"][s]) < 1e-9, s
+            s += 1
+    assert s == len(g["step_kld"])
+    assert rel(step.m, g["m_final"]) < 1e-6
+    assert rel(step.H, g["H_final"]) < 1e-6
+    assert rel(torch.stack([p for _, p in k0.named_parameters()]), g["raw0_final"]) < 1e-8
+    assert rel(torch.stack([p for _, p in k1.named_parameters()]), g["raw1_final"]) < 1e-8
+    sd = dict(vae.named_parameters())
+    for k in ("conv1.weight", "fc211.bias", "deconv2.weight", "_log_vy"):
+        assert rel(sd[k], g["vae_" + k]) < 1e-8, k
+    assert rel(sd["fc1.weight"].sum(1), g["vae_fc1_rowsum"]) < 1e-8

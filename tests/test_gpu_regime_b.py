@@ -472,3 +472,36 @@ def test_closed_step_vs_oracle(hip):
     for (name, p), (_, q) in zip(vae.named_parameters(), ref_vae.named_parameters()):
         if q.grad is not None:  # (_log_vy has no gradient under loss='mse')
             assert rel(p.grad, q.grad) < 1e-3, name
+
+
+VAR_CFG = dict(cat_kernel=[2, 3], bin_kernel=[5], sqexp_kernel=[0],
+               cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                               {'cont_covariate': 1, 'cat_covariate': 4}],
+               bin_int_kernel=[{'cont_covariate': 0, 'bin_covariate': 4}],
+               covariate_missing_val=[{'covariate': 0, 'mask': 6}, {'covariate': 3, 'mask': 7}])
+
+
+def test_kl_closed_kernel_variants_golden(hip):
+    """Bin, bin x RBF and missing-value mask products (GP_model.py:146-236) through the HIP Gram,
+    sweep and adjoint, against the reference's KL_closed (kernel_variants_kl.npz, N = 80)."""
+    import lvae_amd as la
+    g = golden("kernel_variants_kl.npz")
+    L = int(g["L"])
+    k0, k1 = la.generate_kernel_batched(L, **VAR_CFG, id_covariate=2)
+    k = k0 + k1
+    set_raw(k, g["raw"])
+    k = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=float(g["noise"][0])).to(DEV)
+    X = torch.tensor(g["X"], device=DEV)
+    with torch.no_grad():
+        K = k(X, X).evaluate()
+    assert rel(K, g["gram"]) < 1e-13
+    mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+    lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+    kl = la.KL_closed_batched(k, X, lik, mu, lv)
+    kl.sum().backward()
+    assert rel(kl, g["kl"]) < 1e-4
+    assert rel(mu.grad, g["dmu"]) < 1e-4
+    assert rel(lv.grad, g["dlogv"]) < 1e-4
+    draw = torch.stack([p.grad for _, p in k.named_parameters()], 1)
+    assert rel(draw, g["draw"]) < 1e-4
