@@ -535,8 +535,7 @@ def gen_samplers(seed):
     ss = RU.SubjectSampler(ds, P, T)
     epochs = [np.array(list(iter(ss))) for _ in range(3)]
     batches = [np.array(b) for b in BatchSampler(ss, P_b * T, drop_last=False)]
-    # varying length: subject ids in contiguous runs of lengths 1..5 (plus one id reappearing
-    # later, which the reference indexes by first occurrence)
+    # varying length: subject ids in contiguous runs of lengths 1..5
     lengths = [3, 1, 5, 2, 4, 3, 2]
     ids = np.concatenate([np.full(n, 10 + i) for i, n in enumerate(lengths)]).astype(np.float64)
     lab = np.zeros((len(ids), 6))
@@ -646,6 +645,59 @@ def gen_hensman_training(P, T, L, M, P_b, seed, epochs=2):
                 raw0_final=np.stack(raw_params(k0)[1], 0), raw1_final=np.stack(raw_params(k1)[1], 0), **fin)
 
 
+# ----------------------------------------------------------------------------------------------
+# 8. epochs of training.standard_training with type_KL='closed' (training.py:431-592): full batch,
+#    per-dim kernels and likelihoods, constrain_scales.  The reference samples the latent twice
+#    per step (the forward's draw feeds the decoder; the num_samples loop's draw is unused for
+#    'closed'), so the eps queue holds two entries per step and the decoder uses the first.
+# ----------------------------------------------------------------------------------------------
+def gen_standard_training(P, T, L, seed, epochs=3):
+    import training as RT  # noqa: E402  (reference)
+    rng = np.random.default_rng(seed)
+    X = covariates(P, T, seed)
+    N = P * T
+    pix = rng.integers(0, 256, size=(N, 1, 36, 36)).astype(np.uint8)
+    msk = rng.binomial(1, 0.75, size=(N, 1, 36, 36)).astype(np.uint8)
+    EPS = rng.standard_normal((2 * epochs, N, L))
+
+    class DS(torch.utils.data.Dataset):
+        def __len__(self):
+            return N
+
+        def __getitem__(self, i):
+            return {"idx": i, "digit": torch.tensor(pix[i] / 255.0), "label": torch.tensor(X[i]),
+                    "mask": torch.tensor(msk[i].astype(np.float64))}
+
+    class VAE(RV.ConvVAE):
+        calls = 0
+
+        def sample_latent(self, mu, log_var):
+            e = torch.tensor(EPS[VAE.calls])
+            VAE.calls += 1
+            return mu + e * torch.exp(0.5 * log_var)
+
+    model = VAE(L, 1296, vy_init=1.0, p_input=0.0, p=0.0).double()
+    model.load_state_dict(vae_weights(model, seed))
+    kernels = []
+    for _ in range(L):
+        k = full_kernel_ref(1)
+        randomise(k, rng)
+        kernels.append(k)
+    raw_init = np.stack([np.concatenate(raw_params(k)[1]) for k in kernels])
+    liks = [LikStub(torch.tensor([1.0])) for _ in range(L)]
+    groups = [{"params": k.parameters()} for k in kernels] + [{"params": model.parameters()}]
+    opt = torch.optim.Adam(groups, lr=1e-3)
+    res = RT.standard_training(model, "conv", epochs, DS(), opt, "closed", 1, L,
+                               [[KernelAdapter(k) for k in kernels]], liks, None, 2, P, T, 6, 0.15, True, "mse")
+    _, net_arr, nll_arr, recon_arr, gp_arr = res
+    fin = {("vae_" + k): v.detach().numpy().copy() for k, v in model.named_parameters()
+           if k in ("conv1.weight", "fc211.bias", "deconv2.weight", "_log_vy")}
+    fin["vae_fc1_rowsum"] = model.fc1.weight.detach().sum(1).numpy().copy()
+    return dict(P=P, T=T, L=L, seed=seed, epochs=epochs, X=X, pix=pix, msk=msk, eps=EPS, raw=raw_init,
+                step_net=net_arr, step_recon=recon_arr, step_nll=nll_arr, step_gp=gp_arr,
+                raw_final=np.stack([np.concatenate(raw_params(k)[1]) for k in kernels]), **fin)
+
+
 def main(only=None):
     jobs = {
         "kernel_variants_kl.npz": lambda: gen_kl_closed(P=5, T=16, L=2, seed=12, noise=0.9, store_gram=True,
@@ -654,6 +706,7 @@ def main(only=None):
                                                            natural_gradient=True, variants=True),
         "samplers.npz": lambda: gen_samplers(seed=14),
         "hensman_training_2ep.npz": lambda: gen_hensman_training(P=8, T=16, L=2, M=20, P_b=3, seed=15),
+        "standard_training_closed.npz": lambda: gen_standard_training(P=4, T=16, L=2, seed=16),
     }
     if only:
         for name in only:

@@ -6,7 +6,9 @@
   (utils.py:40-113): bit-exact;
 * hensman_training_2ep.npz -- two epochs of the reference's training.hensman_training
   (training.py:15-140) with an injected subject order and reparametrisation noise: per-step KL
-  bound / recon sums, per-epoch averages and the final (m, H), kernel and network parameters.
+  bound / recon sums, per-epoch averages and the final (m, H), kernel and network parameters;
+* standard_training_closed.npz -- three full-batch epochs of training.standard_training with
+  type_KL='closed' (training.py:431-592): per-step net / recon / GP loss, final parameters.
 """
 import numpy as np
 import pytest
@@ -197,6 +199,30 @@ def test_hensman_training_two_epochs_oracle():
     assert rel(H, g["H_final"]) < 1e-7
     assert rel(raw0.T, g["raw0_final"]) < 1e-9
     assert rel(raw1.T, g["raw1_final"]) < 1e-9
+    sd = dict(vae.named_parameters())
+    for k in ("conv1.weight", "fc211.bias", "deconv2.weight", "_log_vy"):
+        assert rel(sd[k], g["vae_" + k]) < 1e-9, k
+    assert rel(sd["fc1.weight"].sum(1), g["vae_fc1_rowsum"]) < 1e-9
+
+
+# ------------------------------------------------------------------------------------------
+# three epochs of standard_training, type_KL='closed' (training.py:431-592): oracle closed step
+# ------------------------------------------------------------------------------------------
+def test_standard_training_closed_oracle():
+    g = golden("standard_training_closed.npz")
+    P, T, L, img, mask, X = training_inputs(g)
+    spec = O.spec_full(**CFG)
+    vae = O.ConvVAE(L).double()
+    vae.load_state_dict(O.vae_weights(vae, int(g["seed"])))
+    raw = torch.tensor(g["raw"], requires_grad=True)
+    opt = torch.optim.Adam([raw] + list(vae.parameters()), lr=1e-3)
+    for s in range(int(g["epochs"])):
+        eps = torch.tensor(g["eps"][2 * s])   # the forward's draw (see gen_standard_training)
+        net, recon, gp = O.closed_step(vae, spec, raw, torch.ones(L), img, mask, X, eps, 0.15, opt=opt)
+        assert rel(net, g["step_net"][s]) < 1e-10, s
+        assert rel(recon, g["step_recon"][s]) < 1e-10, s
+        assert rel(gp, g["step_gp"][s]) < 1e-10, s
+    assert rel(raw, g["raw_final"]) < 1e-9
     sd = dict(vae.named_parameters())
     for k in ("conv1.weight", "fc211.bias", "deconv2.weight", "_log_vy"):
         assert rel(sd[k], g["vae_" + k]) < 1e-9, k
