@@ -33,7 +33,7 @@
 //   W_i = A_ik P^-1       bound c_k ||P^-1||_1        (pivot(k), pnorm[l][k][1]: max column sum)
 //
 // Scratch (spd_sweep_scratch_bytes): Wbuf 2 x [L, np, 256] fp32, planes Wh Wl Ch Cl [L, np, 256]
-// fp16, Pinv [L, 256, 256] fp32, cmax [L, nt] u32, pnorm [L, nt, 2] fp32.  A [L, np, np]: lower
+// fp16, cmax [L, nt] u32, pnorm [L, nt, 2] fp32.  A [L, np, np]: lower
 // 256-block tiles read, overwritten.  Kinv [L, np, np]: out, full symmetric.  np % 256 == 0.
 #include "mfma_x3.hpp"
 #include "prof.hpp"
@@ -53,7 +53,6 @@ constexpr int kSwBB = kSwB * kSwB;
 struct SwScratch {
   float* W[2];                  // [L][np][256]
   _Float16 *Wh, *Wl, *Ch, *Cl;  // [L][np][256]
-  float* Pinv;                  // [L][256][256]
   uint32_t* cmax;               // [L][nt]   fp32 bits of max |column k| (atomicMax)
   float* pnorm;                 // [L][nt][2] max |P_k^-1|, max column abs-sum of P_k^-1
   int nt;
@@ -72,7 +71,6 @@ struct SwScratch {
     Wl = (_Float16*)take(col * 2);
     Ch = (_Float16*)take(col * 2);
     Cl = (_Float16*)take(col * 2);
-    Pinv = (float*)take((size_t)L * kSwBB * 4);
     nt = np_ / kSwB;
     cmax = (uint32_t*)take((size_t)L * nt * 4);
     pnorm = (float*)take((size_t)L * nt * 2 * 4);
@@ -111,137 +109,303 @@ __global__ __launch_bounds__(256) void sw_colmax_kernel(const float* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
-// pivot: T = A_kk (lower triangle read, symmetrised) -> T = -P^-1 (full), Pinv = P^-1.
-// 1024 threads; thread (tr, tc) = (tid >> 5, tid & 31) holds rows 8 tr + r (r < 8) of columns
-// tc + 32 b (b < 8) in a[b][r] (row pairs adjacent: v_pk_fma_f32 with the column value
-// broadcast).  The block is first scaled to unit diagonal (P' = S P S, s_i = P_ii^-1/2), so every
-// sweep pivot d lies in (0, 1] and the whole step is ONE rank-1 update
-//   a_ij -= u_i v_j,  u = c (u_p = d - 1),  v = c / d (v_p = 1 - 1/d),  c = column p,
-// which leaves row / column p at c / d and a_pp at 2 - 1/d (the constant 2 is removed from the
-// diagonal at the end; no later pivot reads a_pp).  With d <= 1 none of these cancels.  Column p + 1
-// is published in a double-buffered LDS vector by its 32 owner threads: one barrier per pivot.
+// pivot: T = A_kk (lower triangle read) -> T = -P^-1 (full), Pinv = P^-1, log|P|, info, split bounds.
+// One 1024-thread workgroup per dim; the 36 lower 32 x 32 blocks of P live in LDS (pitch 33, 152 KB)
+// for the whole kernel and every block operation is a chain of 16 v_mfma_f32_32x32x2f32 reading its
+// operands straight from LDS (fp32 products and sums: the accuracy of LAPACK spotrf + spotri):
+//   1. blocked right-looking Cholesky P = L L^T, 8 panels q:
+//        diagonal block: one wave factors it in registers and inverts its factor (pv_diag), the
+//                        diagonal slot then holds L_qq^-1;
+//        panel:          L_iq = A_iq L_qq^-T                        (waves 0 .. 6-q)
+//        trailing:       A_ij -= L_iq L_jq^T, q < j <= i             (all waves; wave 0 takes
+//                        (q+1, q+1) first and factors it right away: the next diagonal factor
+//                        overlaps the rest of the trailing update)
+//   2. L^-1 in place, block row by block row: (L^-1)_ij = -L_ii^-1 sum_{k=j}^{i-1} L_ik (L^-1)_kj
+//      (the outer product by L_ii^-1 takes the inner sum straight from the accumulator registers as
+//      the B operand, with the K index permuted to the accumulator layout)
+//   3. P^-1 = L^-T L^-1, all 36 lower blocks at once (sum_{k >= i} (L^-1)_ki^T (L^-1)_kj), written
+//      back after one barrier, then streamed out (both triangles, coalesced) with the split bounds.
+// The Cholesky form (rather than an explicit-inverse block sweep) keeps the block updates backward
+// stable: a 32-wide explicit-inverse update loses cond(P_qq) digits (measured 20x larger K^-1 error).
 // ------------------------------------------------------------------------------------------
-template <int B0>
-__device__ __attribute__((always_inline)) inline void sw_pivot_cols(float (&a)[8][8], float (*colbuf)[kSwB],
-                                                                    float* dpiv, int tid, int tr, int tc) {
-  for (int q = 0; q < 32; ++q) {
-    const int p = 32 * B0 + q;
-    const float* cb = colbuf[p & 1];
-    const float d = cb[p];
-    if (tid == 0) dpiv[p] = d;
-    const float id = __builtin_amdgcn_rcpf(d);
-    float u[8];
-    {
-      const float4 u0 = *reinterpret_cast<const float4*>(cb + 8 * tr);
-      const float4 u1 = *reinterpret_cast<const float4*>(cb + 8 * tr + 4);
-      u[0] = u0.x, u[1] = u0.y, u[2] = u0.z, u[3] = u0.w;
-      u[4] = u1.x, u[5] = u1.y, u[6] = u1.z, u[7] = u1.w;
-    }
-    const int rp = p - 8 * tr;
+constexpr int kPvL = 33;                 // LDS pitch (floats) of a 32 x 32 block
+constexpr int kPvBlk = 32 * kPvL;        // floats per block
+constexpr int kPvBlocks = 36;            // lower blocks of 8 x 8
+__device__ inline float* pv_blk(float* lf, int R, int C) { return lf + (R * (R + 1) / 2 + C) * kPvBlk; }
+
+typedef float pv_f32x16 __attribute__((ext_vector_type(16)));
+
+#ifdef LVAE_PV_TIMING
+__device__ unsigned long long g_pv_t[64];
+#define PV_T(i) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_pv_t[i] = wall_clock64(); } while (0)
+#else
+#define PV_T(i) do { } while (0)
+#endif
+
+__device__ inline float pv_rl(float v, int lane) {  // v of lane `lane` (uniform lane index)
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// accumulator element e of a 32x32x2 MFMA block in lane (rl, hh): row (e&3) + 8 (e>>2) + 4 hh, col rl
+__device__ inline int pv_row(int e, int hh) { return (e & 3) + 8 * (e >> 2) + 4 * hh; }
+
+__device__ inline void pv_load(pv_f32x16& acc, const float* B, int rl, int hh) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) u[r] = (r == rp) ? d - 1.0f : u[r];
+  for (int e = 0; e < 16; ++e) acc[e] = B[pv_row(e, hh) * kPvL + rl];
+}
+__device__ inline void pv_store(const pv_f32x16& acc, float* B, int rl, int hh, float sgn = 1.f) {
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      float v = cb[tc + 32 * b] * id;
-      if (b == B0) v = (tc == q) ? 1.0f - id : v;
+  for (int e = 0; e < 16; ++e) B[pv_row(e, hh) * kPvL + rl] = sgn * acc[e];
+}
+// acc += op(X) op(Y)^T with X, Y 32 x 32 LDS blocks: TX / TY select the transposed operand
+//   A[r][k] = TX ? X[k][r] : X[r][k],   B[k][c] = TY ? Y[k][c] : Y[c][k]   (c, r = rl)
+// Two interleaved accumulation chains (even / odd k-steps) so consecutive MFMAs do not wait on
+// each other's results.
+template <bool TX, bool TY>
+__device__ inline void pv_mma(pv_f32x16& acc, const float* X, const float* Y, int rl, int hh, float sx = 1.f) {
+  pv_f32x16 t = {};
 #pragma unroll
-      for (int r = 0; r < 8; ++r) a[b][r] = fmaf(-u[r], v, a[b][r]);
-    }
-    // publish column p + 1 (owner: tc == (p + 1) & 31, register column (p + 1) >> 5)
-    float* nb = colbuf[(p + 1) & 1] + 8 * tr;
-    if (q < 31) {
-      if (tc == q + 1) {
-        *reinterpret_cast<float4*>(nb) = make_float4(a[B0][0], a[B0][1], a[B0][2], a[B0][3]);
-        *reinterpret_cast<float4*>(nb + 4) = make_float4(a[B0][4], a[B0][5], a[B0][6], a[B0][7]);
-      }
-    } else if constexpr (B0 < 7) {
-      if (tc == 0) {
-        *reinterpret_cast<float4*>(nb) = make_float4(a[B0 + 1][0], a[B0 + 1][1], a[B0 + 1][2], a[B0 + 1][3]);
-        *reinterpret_cast<float4*>(nb + 4) = make_float4(a[B0 + 1][4], a[B0 + 1][5], a[B0 + 1][6], a[B0 + 1][7]);
-      }
-    }
-    __syncthreads();
+  for (int s = 0; s < 16; ++s) {
+    const int k = 2 * s + hh;
+    const float a = TX ? X[k * kPvL + rl] : X[rl * kPvL + k];
+    const float b = TY ? Y[k * kPvL + rl] : Y[rl * kPvL + k];
+    if (s & 1)
+      t = __builtin_amdgcn_mfma_f32_32x32x2f32(sx * a, b, t, 0, 0, 0);
+    else
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sx * a, b, acc, 0, 0, 0);
   }
-  if constexpr (B0 < 7) sw_pivot_cols<B0 + 1>(a, colbuf, dpiv, tid, tr, tc);
+  acc += t;
+}
+
+// Rank-1 elimination steps inside MFMA accumulators.  A 32 x 32 block held as one accumulator
+// (lane (c, hh), element e: row (e&3) + 8 (e>>2) + 4 hh, column c) keeps row p in element e(p) of the
+// lanes of half h(p).  An outer product u v^T is then ONE v_mfma_f32_32x32x2f32 whose k-slot h(p)
+// carries u (A operand, lanes of half h(p)) and v (B operand, same lanes) and whose other k-slot is
+// zero: no value crosses lanes, only the pivot itself (one readlane).
+__device__ inline int pv_hh(int r) { return (r >> 2) & 1; }            // half holding row r
+__device__ inline int pv_e(int r) { return (r & 3) | ((r >> 3) << 2); }  // its element
+
+// The Cholesky panel q, by waves 0 .. 7-q (wave w: row block i = q + w):
+//   every wave factors the diagonal block X = A_qq in its own accumulator, X -= u u^T / d_p (u = row
+//   p of X: the Schur complement step; L_qq[:, p] = u / sqrt d_p), and wave w > 0 applies the same
+//   steps to Bt = A_iq^T (Bt -= u b^T / d_p, b = row p of Bt = A'_iq[:, p]; L_iq[:, p] = b / sqrt d_p)
+// so the panel needs no L_qq^-1 and the whole panel is 32 steps deep.  Wave 0 writes L_qq (zero
+// upper part), waves > 0 their L_iq, into LDS; wave 0 also returns sum log d_p and the first
+// non-positive pivot.
+__device__ inline void pv_panel(float* lf, int q, int w, int lane, double& ld, int& bad) {
+  const int rl = lane & 31, hh = lane >> 5, i = q + w;
+  float* Dq = pv_blk(lf, q, q);
+  float* Bi = pv_blk(lf, i, q);
+  pv_f32x16 X, Bt;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = pv_row(e, hh);
+    X[e] = r >= rl ? Dq[r * kPvL + rl] : Dq[rl * kPvL + r];
+    Bt[e] = (w > 0) ? Bi[rl * kPvL + r] : 0.0f;
+  }
+  float dp = 0.f;  // lane p: pivot d_p
+  __syncthreads();  // every panel wave has its copy of A_qq before wave 0 overwrites it with L_qq
+#pragma unroll
+  for (int p = 0; p < 32; ++p) {
+    const int ep = pv_e(p), hp = pv_hh(p);
+    const float d = pv_rl(X[ep], p + 32 * hp);
+    const float id = __builtin_amdgcn_rcpf(d), is = __builtin_amdgcn_rsqf(d);
+    const bool mine = (hh == hp);
+    const float u = (mine && rl >= p) ? X[ep] : 0.0f;
+    if (w > 0) {
+      const float bp = mine ? Bt[ep] : 0.0f;
+      if (mine) Bi[rl * kPvL + p] = bp * is;
+      Bt = __builtin_amdgcn_mfma_f32_32x32x2f32(-u, bp * id, Bt, 0, 0, 0);
+    } else {
+      if (mine) Dq[rl * kPvL + p] = u * is;
+      if (lane == p) dp = d;
+    }
+    X = __builtin_amdgcn_mfma_f32_32x32x2f32(-u, u * id, X, 0, 0, 0);
+  }
+  if (w == 0) {
+    const double lv = (lane < 32) ? log((double)dp) : 0.0;
+    ld += wave_sum(lv);
+    const unsigned long long nb = __ballot(lane < 32 && !(dp > 0.0f && isfinite(dp)));
+    if (nb) bad = min(bad, 32 * q + (int)__builtin_ctzll(nb));
+  }
+}
+
+// one wave: the lower-triangular factor L in block D -> L^-1 (forward substitution as rank-1 steps:
+// Y = I; Y -= a b^T with a = column p of L (a_p = L_pp - 1), b = row p of Y / L_pp: the pivot row
+// is rescaled in the same update)
+__device__ inline void pv_trinv(float* D, int lane) {
+  const int rl = lane & 31, hh = lane >> 5;
+  pv_f32x16 y;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) y[e] = (pv_row(e, hh) == rl) ? 1.0f : 0.0f;
+  const float lrr = D[rl * kPvL + rl];
+  const float ilr = 1.0f / lrr;  // lane rl: 1 / L_rr
+#pragma unroll
+  for (int p = 0; p < 32; ++p) {
+    const int ep = pv_e(p), hp = pv_hh(p);
+    const bool mine = (hh == hp);
+    const float Lrp = D[rl * kPvL + p];
+    const float a = mine ? ((rl == p) ? Lrp - 1.0f : Lrp) : 0.0f;
+    const float b = mine ? y[ep] * pv_rl(ilr, p) : 0.0f;
+    y = __builtin_amdgcn_mfma_f32_32x32x2f32(-a, b, y, 0, 0, 0);
+  }
+  pv_store(y, D, rl, hh);
 }
 
 __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall, int np_, int kb, SwScratch S,
                                                         double* __restrict__ logdet, int32_t* __restrict__ info) {
-  __shared__ __attribute__((aligned(16))) float colbuf[2][kSwB];
-  __shared__ float dg[kSwB];
-  __shared__ float dpiv[kSwB];
-  __shared__ float csum[kSwB];
-  __shared__ double red[16];
-  __shared__ int bad_s;
+  __shared__ float lf[kPvBlocks * kPvBlk];
+  __shared__ float colsum[kSwB];
   __shared__ uint32_t pmax_s, pn1_s;
-  float* __restrict__ Pinv = S.Pinv;
-  const int l = blockIdx.x, tid = threadIdx.x, tr = tid >> 5, tc = tid & 31;
+  __shared__ int bad_s;
+  const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
-  float a[8][8];
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int row = 8 * tr + r, col = tc + 32 * b;
-      const int hi = row >= col ? row : col, lo = row >= col ? col : row;
-      a[b][r] = T[hi * np_ + lo];
-      if (row == col) dg[row] = a[b][r];
-    }
   if (tid == 0) {
     bad_s = INT_MAX;
     pmax_s = 0u;
     pn1_s = 0u;
   }
-  if (tid < kSwB) csum[tid] = 0.f;
-  __syncthreads();
+  if (tid < kSwB) colsum[tid] = 0.f;
+  PV_T(0);
+  // lower blocks -> LDS (row r = tid >> 5 of a block, 32 consecutive columns per 32 threads); all 36
+  // loads in flight before the first LDS write
+  {
+    const int r = tid >> 5, c = tid & 31;
+    float v[kPvBlocks];
 #pragma unroll
-  for (int b = 0; b < 8; ++b)
+    for (int R = 0, b = 0; R < 8; ++R)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) a[b][r] *= rsqrtf(dg[8 * tr + r]) * rsqrtf(dg[tc + 32 * b]);
-  if (tc == 0) {
-    *reinterpret_cast<float4*>(&colbuf[0][8 * tr]) = make_float4(a[0][0], a[0][1], a[0][2], a[0][3]);
-    *reinterpret_cast<float4*>(&colbuf[0][8 * tr + 4]) = make_float4(a[0][4], a[0][5], a[0][6], a[0][7]);
+      for (int C = 0; C <= R; ++C, ++b) v[b] = T[(int64_t)(32 * R + r) * np_ + 32 * C + c];
+#pragma unroll
+    for (int b = 0; b < kPvBlocks; ++b) lf[b * kPvBlk + r * kPvL + c] = v[b];
   }
   __syncthreads();
+  double ld = 0.0;  // wave 0: sum of log pivots
+  int bad = INT_MAX;
+  PV_T(1);
 
-  sw_pivot_cols<0>(a, colbuf, dpiv, tid, tr, tc);
-
-  // a = -(S P S)^-1 + 2 I  ->  -P^-1 = S a' S; max |P^-1| and its column abs-sums (split bounds)
-  float* Pl = Pinv + (int64_t)l * kSwBB;
-  float pm = 0.f;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    float cs = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int row = 8 * tr + r, col = tc + 32 * b;
-      const float x = (a[b][r] - (row == col ? 2.0f : 0.0f)) * rsqrtf(dg[row]) * rsqrtf(dg[col]);
-      T[row * np_ + col] = x;
-      Pl[row * kSwB + col] = -x;
-      cs += fabsf(x);
-      pm = fmaxf(pm, fabsf(x));
+  // 1. Cholesky P = L L^T, panel by panel (pv_panel), then the trailing update A_ij -= L_iq L_jq^T
+  for (int q = 0; q < 8; ++q) {
+    if (w <= 7 - q) {
+      pv_panel(lf, q, w, lane, ld, bad);
+    } else {
+      __syncthreads();  // pv_panel's barrier
     }
-    atomicAdd(&csum[tc + 32 * b], cs);
+    __syncthreads();
+    PV_T(2 + 2 * q);
+    const int m = 7 - q, nb = m * (m + 1) / 2;
+    for (int t = w; t < nb; t += 16) {  // trailing block t, column-major from the diagonal
+      int jj = 0, u = t;
+      while (u >= m - jj) {
+        u -= m - jj;
+        ++jj;
+      }
+      const int j = q + 1 + jj, i = j + u;
+      pv_f32x16 acc;
+      float* Bij = pv_blk(lf, i, j);
+      pv_load(acc, Bij, rl, hh);
+      pv_mma<false, false>(acc, pv_blk(lf, i, q), pv_blk(lf, j, q), rl, hh, -1.f);
+      pv_store(acc, Bij, rl, hh);
+    }
+    __syncthreads();
+    PV_T(3 + 2 * q);
   }
+  // the diagonal factors -> L_ii^-1 (eight waves in parallel)
+  if (w < 8) pv_trinv(pv_blk(lf, w, w), lane);
+  __syncthreads();
+  PV_T(20);
+
+  // 2. L^-1 in place by recursive doubling (the diagonal slots already hold L_ii^-1): at each level,
+  //    for the lower-triangular [A 0; B C] of two inverted halves, B <- -C^-1 B A^-1 (X = B A^-1 to
+  //    LDS, then -C^-1 X); levels of 64, 128, 256 rows: a chain of 2 + 4 + 8 block products
+  if (w < 4) {  // 64: B = L_{2a+1, 2a}
+    const int a = 2 * w;
+    pv_f32x16 X = {}, Y = {};
+    pv_mma<false, true>(X, pv_blk(lf, a + 1, a), pv_blk(lf, a, a), rl, hh);
+    const float* Ci = pv_blk(lf, a + 1, a + 1);
+#pragma unroll
+    for (int s = 0; s < 16; ++s)  // Y = C^-1 X, X straight from the accumulator (K permuted to its rows)
+      Y = __builtin_amdgcn_mfma_f32_32x32x2f32(Ci[rl * kPvL + pv_row(s, hh)], X[s], Y, 0, 0, 0);
+    pv_store(Y, pv_blk(lf, a + 1, a), rl, hh, -1.f);
+  }
+  __syncthreads();
+  PV_T(24);
+#pragma unroll 1
+  for (int lv = 1; lv <= 2; ++lv) {
+    const int h = 1 << lv;                 // half width in blocks (2, 4)
+    const int per = h * h;                 // blocks of B per instance
+    const int inst = w / per, t = w % per;
+    const bool act = inst < 4 / h;         // 2 instances of 128, 1 of 256
+    const int o = 2 * h * inst;            // first block row / column of the instance
+    const int i = o + h + t / h, j = o + t % h;
+    pv_f32x16 acc = {};
+    if (act)  // X_ij = sum_{k=j}^{o+h-1} L_ik (A^-1)_kj
+      for (int k = j; k < o + h; ++k) pv_mma<false, true>(acc, pv_blk(lf, i, k), pv_blk(lf, k, j), rl, hh);
+    __syncthreads();
+    if (act) pv_store(acc, pv_blk(lf, i, j), rl, hh);
+    __syncthreads();
+    acc = pv_f32x16{};
+    if (act)  // Y_ij = sum_{k=o+h}^{i} (C^-1)_ik X_kj
+      for (int k = o + h; k <= i; ++k) pv_mma<false, true>(acc, pv_blk(lf, i, k), pv_blk(lf, k, j), rl, hh);
+    __syncthreads();
+    if (act) pv_store(acc, pv_blk(lf, i, j), rl, hh, -1.f);
+    __syncthreads();
+  }
+  PV_T(21);
+
+  // 3. P^-1 = L^-T L^-1: block n = i (i + 1) / 2 + j costs 8 - i products; longest-processing-time
+  //    assignment, 7-8 products per wave, 30 per SIMD
+  constexpr signed char kLauum[16][3] = {{0, -1, -1},  {1, 31, -1},  {2, 32, -1},  {3, 26, -1},
+                                         {4, 27, -1},  {5, 28, 33},  {6, 22, 34},  {7, 23, 35},
+                                         {8, 24, -1},  {9, 25, -1},  {10, 17, -1}, {11, 18, -1},
+                                         {12, 19, -1}, {13, 20, -1}, {14, 21, 29}, {15, 16, 30}};
+  pv_f32x16 res[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n >= 0) {
+      int i = 0;
+      while ((i + 1) * (i + 2) / 2 <= n) ++i;
+      const int j = n - i * (i + 1) / 2;
+      res[h] = pv_f32x16{};
+      for (int k = i; k < 8; ++k) pv_mma<true, true>(res[h], pv_blk(lf, k, i), pv_blk(lf, k, j), rl, hh);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n >= 0) pv_store(res[h], lf + n * kPvBlk, rl, hh);
+  }
+  __syncthreads();
+  PV_T(22);
+
+  // 4. out: T = -P^-1, both triangles (a wave writes 256 consecutive floats of one row; the LDS reads
+  //    are consecutive (lower part) or pitch-33 strided (mirror): conflict-free); split bounds: max
+  //    |P^-1| and the column abs-sums
+  const int c = tid & 255;
+  float cs = 0.f, pm = 0.f;
+  for (int r = tid >> 8; r < kSwB; r += 4) {
+    const float v = r >= c ? pv_blk(lf, r >> 5, c >> 5)[(r & 31) * kPvL + (c & 31)]
+                           : pv_blk(lf, c >> 5, r >> 5)[(c & 31) * kPvL + (r & 31)];
+    T[(int64_t)r * np_ + c] = -v;
+    cs += fabsf(v);
+    pm = fmaxf(pm, fabsf(v));
+  }
+  atomicAdd(&colsum[c], cs);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) pm = fmaxf(pm, __shfl_xor(pm, o, 64));
-  if ((tid & 63) == 0) atomicMax(&pmax_s, __float_as_uint(pm));
+  if (lane == 0) atomicMax(&pmax_s, __float_as_uint(pm));
+  if (w == 0 && lane == 0) bad_s = bad;
   __syncthreads();
-  if (tid < kSwB) atomicMax(&pn1_s, __float_as_uint(csum[tid]));
-  // log|P| = sum log d_p - 2 sum log s_i with the s_i the scaling actually applied (rsqrtf): the
-  // pivots d_p are those of S P S, so this is exact to the rounding of the d_p; first bad pivot
-  double lv = 0.0;
-  if (tid < kSwB) {
-    const float d = dpiv[tid];
-    if (!(d > 0.0f) || !isfinite(d)) atomicMin(&bad_s, tid);
-    lv = log((double)d) - 2.0 * log((double)rsqrtf(dg[tid]));
-  }
-  lv = block_sum<1024>(lv, red);  // (its barriers also order the pmax_s / pn1_s atomics)
+  if (tid < kSwB) atomicMax(&pn1_s, __float_as_uint(colsum[tid]));
+  __syncthreads();
+  PV_T(23);
   if (tid == 0) {
     float* pn = S.pnorm + ((int64_t)l * S.nt + kb) * 2;
     pn[0] = __uint_as_float(pmax_s);
     pn[1] = __uint_as_float(pn1_s);
-    logdet[l] += lv;
+    logdet[l] += ld;
     if (bad_s != INT_MAX && info[l] == 0) info[l] = kb * kSwB + bad_s + 1;
   }
 }
@@ -317,17 +481,17 @@ __global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, 
   if (role == 0) {
     if (i == k) return;
     const SwScales sc = sw_scales(S, l, k);
-    const float* P = S.Pinv + (int64_t)l * kSwBB;
+    const float* P = A + (int64_t)k * kSwB * np_ + k * kSwB;  // -P^-1 (the pivot's output, both triangles)
     Frag f;
     f.zero();
     if (i > k) {
-      tile_gemm_x3<true, true>(A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB, np_, P + sn * kSwT * kSwB, kSwB,
+      tile_gemm_x3<true, true, true>(A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB, np_, P + sn * kSwT * np_, np_,
                                0, kSwB, f, (_Float16*)lds, sc.c, sc.p);
     } else {
       // A_ik(m, t) = tile (k, i)[t][m]; tile (k, k-1) is Wprev[k] ([rows of k][cols of k-1])
       const float* src = (i == k - 1) ? Wp + (int64_t)k * kSwBB : A + (int64_t)k * kSwB * np_ + i * kSwB;
       const int64_t ls = (i == k - 1) ? kSwB : np_;
-      tile_gemm_x3<false, true>(src + sm * kSwT, ls, P + sn * kSwT * kSwB, kSwB, 0, kSwB, f, (_Float16*)lds, sc.c,
+      tile_gemm_x3<false, true, true>(src + sm * kSwT, ls, P + sn * kSwT * np_, np_, 0, kSwB, f, (_Float16*)lds, sc.c,
                                 sc.p);
     }
     float* C = Wc + sub;
@@ -650,6 +814,14 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
 }  // namespace lvae
 
 extern "C" {
+#ifdef LVAE_PV_TIMING
+int lvae_pv_timing(float* A, int np_, int L, void* scratch, double* logdet, int32_t* info, unsigned long long* out) {
+  lvae::SwScratch S((char*)scratch, np_, L);
+  lvae::sw_pivot_kernel<<<L, 1024>>>(A, np_, 0, S, logdet, info);
+  (void)hipDeviceSynchronize();
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lvae::g_pv_t), sizeof(unsigned long long) * 64);
+}
+#endif
 size_t lvae_spd_sweep_scratch_size(int np_, int L) { return lvae::spd_sweep_scratch_bytes(np_, L); }
 int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
                        void* stream) {
