@@ -52,7 +52,7 @@ constexpr int kSwBB = kSwB * kSwB;
 
 struct SwScratch {
   float* W[2];                  // [L][np][256]
-  _Float16 *Wh, *Wl, *Ch, *Cl;  // [L][np][256]
+  _Float16 *Wh[2], *Wl[2], *Ch[2], *Cl[2];  // [L][np][256], by pass parity (prep(k+1) runs beside U2(k))
   uint32_t* cmax;               // [L][nt]   fp32 bits of max |column k| (atomicMax)
   float* pnorm;                 // [L][nt][2] max |P_k^-1|, max column abs-sum of P_k^-1
   int nt;
@@ -67,10 +67,12 @@ struct SwScratch {
     const size_t col = (size_t)L * np_ * kSwB;
     W[0] = (float*)take(col * 4);
     W[1] = (float*)take(col * 4);
-    Wh = (_Float16*)take(col * 2);
-    Wl = (_Float16*)take(col * 2);
-    Ch = (_Float16*)take(col * 2);
-    Cl = (_Float16*)take(col * 2);
+    for (int b = 0; b < 2; ++b) {
+      Wh[b] = (_Float16*)take(col * 2);
+      Wl[b] = (_Float16*)take(col * 2);
+      Ch[b] = (_Float16*)take(col * 2);
+      Cl[b] = (_Float16*)take(col * 2);
+    }
     nt = np_ / kSwB;
     cmax = (uint32_t*)take((size_t)L * nt * 4);
     pnorm = (float*)take((size_t)L * nt * 2 * 4);
@@ -495,8 +497,8 @@ __global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, 
                                 sc.p);
     }
     float* C = Wc + sub;
-    _Float16* h = S.Wh + l * col + sub;
-    _Float16* lo = S.Wl + l * col + sub;
+    _Float16* h = S.Wh[k & 1] + l * col + sub;
+    _Float16* lo = S.Wl[k & 1] + l * col + sub;
     float wm = 0.f;
     frag_foreach(f, [&](int r, int c, float v) {
       C[r * kSwB + c] = v;
@@ -523,8 +525,8 @@ __global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, 
       src = A + ((int64_t)k * kSwB + sn * kSwT) * np_ + i * kSwB + sm * kSwT;
       ls = np_;
     }
-    _Float16* h = S.Ch + l * col + sub;
-    _Float16* lo = S.Cl + l * col + sub;
+    _Float16* h = S.Ch[k & 1] + l * col + sub;
+    _Float16* lo = S.Cl[k & 1] + l * col + sub;
     const float scc = sw_scales(S, l, k).c;
     blk128_visit(src, ls, i < k, (float*)lds,
                  [&](int r, int c, f32x4 v) { sw_split4(v, scc, h + r * kSwB + c, lo + r * kSwB + c); });
@@ -547,49 +549,41 @@ __global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, 
 }
 
 // ------------------------------------------------------------------------------------------
-// U1(k): A_{k+1,k+1} -= W_{k+1} C_{k+1}^T on its three lower 128-blocks: x3 tile GEMMs on the fp32
-// operands (W from Wbuf, C = the still unswept tile (k+1, k)), 3 L workgroups -- short, so the side
-// stream (U1 + the next pivot) stays within U2's time.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sw_u1_kernel(float* __restrict__ Aall, SwScratch S, int np_, int k) {
-  __shared__ __attribute__((aligned(16))) char lds[x3_lds_bytes()];
-  const int l = blockIdx.y, sm = blockIdx.x == 0 ? 0 : 1, sn = blockIdx.x == 2 ? 1 : 0, kp = k + 1;
-  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
-  float* A = Aall + l * np2;
-  float* T = A + ((int64_t)kp * kSwB + sm * kSwT) * np_ + kp * kSwB + sn * kSwT;
-  const float* Wr = S.W[k & 1] + l * col + (int64_t)kp * kSwBB + sm * kSwT * kSwB;
-  const float* Cr = A + ((int64_t)kp * kSwB + sn * kSwT) * np_ + k * kSwB;
-  const SwScales sc = sw_scales(S, l, k);
-  Frag f;
-  frag_load(f, T, np_);
-  tile_gemm_x3<true, true, true>(Wr, kSwB, Cr, np_, 0, kSwB, f, (_Float16*)lds, sc.w, sc.c);
-  frag_foreach(f, [&](int r, int c, float v) { T[(int64_t)r * np_ + c] = v; });
-}
-
-// ------------------------------------------------------------------------------------------
 // update(k): A_IJ += (-W_I) C_J^T on lower 256-tiles (I >= J, I, J != k), K = 256: one 512-thread
 // workgroup per 256 x 256 tile on the pre-split fp16 planes (x3_dma.hpp layout and DMA staging,
 // double-buffered K chunks of 32).  C enters in 8 chunks of 16 accumulator elements INSIDE the K
 // loop (chunk j loaded in step j, added in step j + 1), read and written non-temporally (CAUX = slc:
 // the C stream does not evict the planes from L2).  Measured at np = 4096, L = 16: C streaming alone
 // ~200 us, the GEMM alone ~200 us, together 293 us per launch (a 256 x 128 half-tile form with two
-// workgroups per CU moved 1.5x the plane bytes and took 350-410 us).
-//   the tile (k+1, k+1) is U1's (sw_u1_kernel), except in the last pass
-//   LAST:   -result to Kinv (I, J) and its mirror instead of in place
+// workgroups per CU moved 1.5x the plane bytes and took 350-410 us).  Three tile sets (MODE):
+//   kSwU2    the interior: I, J not in {k, k+1} -- on the caller's stream, beside
+//   kSwU1    row / column k+1 (incl. the next pivot block) -- on the side stream, ahead of the next
+//            pivot and prep (lookahead: those do not wait for the interior update)
+//   kSwLast  every tile of the last pass (I, J != k): -result to Kinv (I, J) and its mirror
 // ------------------------------------------------------------------------------------------
-template <bool LAST, int CAUX = LAST ? 0 : 2>
+constexpr int kSwU2 = 0, kSwU1 = 1, kSwLast = 2;
+template <int MODE, int CAUX = MODE == kSwLast ? 0 : 2>
 __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S,
                                                            float* __restrict__ Kinv, int np_, int k,
                                                            int ntl, int nwg) {
+  constexpr bool LAST = MODE == kSwLast;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int l = wgid / ntl;
+  const int l = wgid / ntl, t = wgid % ntl, nt = np_ / kSwB;
   int I, J;
-  sx_tri_blocked(wgid % ntl, np_ / kSwB - 1, I, J);
-  I += I >= k;
-  J += J >= k;
-  if (!LAST && I == k + 1 && J == k + 1) return;  // U1's tile
+  if constexpr (MODE == kSwU1) {  // t < k: (k+1, t); t == k: (k+1, k+1); t > k: (t+1, k+1)
+    I = t > k ? t + 1 : k + 1;
+    J = t > k ? k + 1 : (t < k ? t : k + 1);
+  } else if constexpr (MODE == kSwU2) {
+    sx_tri_blocked(t, nt - 2, I, J);
+    I += I >= k ? 2 : 0;
+    J += J >= k ? 2 : 0;
+  } else {
+    sx_tri_blocked(t, nt - 1, I, J);
+    I += I >= k;
+    J += J >= k;
+  }
   const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
   float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
@@ -598,10 +592,10 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   const int64_t oa = l * col + (int64_t)I * kSwBB, ob = l * col + (int64_t)J * kSwBB;
   const SwScales sc = sw_scales(S, l, k);
   const float cs = sc.w * sc.c, inv = 1.0f / cs;  // accumulate in sW sC units (exact powers of two)
-  const _Float16* ah = S.Wh + oa;
-  const _Float16* al = S.Wl + oa;
-  const _Float16* bh = S.Ch + ob;
-  const _Float16* bl = S.Cl + ob;
+  const _Float16* ah = S.Wh[k & 1] + oa;
+  const _Float16* al = S.Wl[k & 1] + oa;
+  const _Float16* bh = S.Ch[k & 1] + ob;
+  const _Float16* bl = S.Cl[k & 1] + ob;
   sx_f32x16 acc[4][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -653,8 +647,8 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, vo,
                                                 ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
         }
-    // tiles of row / column k+1: the C operand of the next pass
-    if (I == k + 1 || J == k + 1) sw_fold_max(mx, S.cmax + l * S.nt + k + 1);
+    // tiles of row / column k+1 (not the next pivot block): the C operand of the next pass
+    if (MODE == kSwU1 && I != J) sw_fold_max(mx, S.cmax + l * S.nt + k + 1);
   } else {
     // -result to Kinv (I, J) (diagonal tiles: lower elements only) and, transposed through LDS, to
     // (J, I): per 128-row half of the tile, U[c][r ^ 4 (c & 31)] = value (r, c), read back as float4
@@ -744,15 +738,22 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------
 // host sequencing
 // ------------------------------------------------------------------------------------------
-// The pivot's stream (highest priority, so its workgroups are dispatched ahead of U2's as CUs free)
-// and its fork / join events: one set per (device, caller stream), created on first use.  The map
-// and every enqueue sequence that records / waits on a set's events hold g_side_mu, so host threads
-// sharing a caller stream cannot interleave their fork / join records, and callers on different
-// streams never share a side stream.  (Disjoint CU masks for the two streams were measured 2.6 ms
-// per step slower: every masked queue slowed the rest of the step.)
+// Lookahead schedule.  Per pass the caller's stream updates row / column k+1 first (U1(k), one
+// short launch) and then the interior (U2(k)); the side stream (highest priority, so its workgroups
+// are dispatched ahead of U2's as CUs free) runs the next pass's critical chain beside U2(k):
+//     main:  wait ev_prep (prep(k));  U1(k); record ev_u1;  U2(k)
+//     side:  wait ev_u1;  pivot(k+1); prep(k+1); record ev_prep
+// (prep(k+1) writes the other plane buffer, whose readers U1 / U2(k-1) precede U1(k) on the main
+// stream; it copies the swept column k into tiles U2(k) does not touch).  A pass costs
+// U1 + max(U2, pivot + prep) instead of prep + max(U2, U1 + pivot).  (Running U1 on the side stream
+// instead measured slower: its 240 tiles then queue behind U2's for CU slots.)
+// One stream + event set per (device, caller stream), created on first use; the map and every
+// enqueue sequence hold g_side_mu, so host threads sharing a caller stream cannot interleave their
+// records / waits, and callers on different streams never share a side stream.  (Disjoint CU masks
+// for the two streams were measured 2.6 ms per step slower: every masked queue slowed the rest.)
 struct SwSide {
   hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, prep = nullptr, u1 = nullptr;
 };
 
 static std::mutex g_side_mu;
@@ -766,8 +767,8 @@ static int sw_side(hipStream_t caller, SwSide*& out) {  // g_side_mu held by the
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (hipStreamCreateWithPriority(&sd.s, hipStreamNonBlocking, greatest) != hipSuccess) return LVAE_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
-    if (hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
+    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.u1})
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
   }
   out = &sd;
   return 0;
@@ -783,30 +784,32 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   SwSide* sd = nullptr;
   LVAE_TRY(sw_side(st, sd));
   SwScratch S((char*)scratch, np_, L);
-  const int nt = np_ / kSwB, ntl = (nt - 1) * nt / 2, nwg = ntl * L;
+  const int nt = np_ / kSwB;
+  const int ntl2 = (nt - 2) * (nt - 1) / 2, ntl1 = nt - 1, ntll = (nt - 1) * nt / 2;
+  auto ok = [](hipError_t e) { return e == hipSuccess; };
   (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
   (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
   (void)hipMemsetAsync(S.cmax, 0, sizeof(uint32_t) * L * nt, st);
-  if (nt > 1) sw_colmax_kernel<<<dim3(nt - 1, L), 256, 0, st>>>(A, np_, S);
-  sw_pivot_kernel<<<L, 1024, 0, st>>>(A, np_, 0, S, logdet, info);
-  for (int k = 0; k < nt; ++k) {
-    if (nt > 1) sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, st>>>(A, S, np_, nt, k);
-    if (k + 1 < nt) {
-      if (hipEventRecord(sd->fork, st) != hipSuccess) return LVAE_ERR_LAUNCH;
-      if (hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
-      sw_u1_kernel<<<dim3(3, L), 256, 0, sd->s>>>(A, S, np_, k);
-      sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info);
-      if (hipEventRecord(sd->join, sd->s) != hipSuccess) return LVAE_ERR_LAUNCH;
-      if (ntl > 1) {
-        ProfScope ps(LVAE_PH_SWEEP_UPD, st);
-        sw_update_kernel<false><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, ntl, nwg);
-      }
-      if (hipStreamWaitEvent(st, sd->join, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
-    } else {
-      if (ntl > 0) sw_update_kernel<true><<<nwg, 512, 0, st>>>(A, S, Kinv, np_, k, ntl, nwg);
-      sw_finish_kernel<<<dim3(4 * (2 * (nt - 1) + 1), L), 256, 0, st>>>(A, S, Kinv, np_, nt);
+  if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
+  if (nt > 1) sw_colmax_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
+  sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info);
+  if (nt > 1) sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, sd->s>>>(A, S, np_, nt, 0);
+  if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+  for (int k = 0; k + 1 < nt; ++k) {
+    if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prep(k)
+    sw_update_kernel<kSwU1><<<ntl1 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl1, ntl1 * L);
+    if (!ok(hipEventRecord(sd->u1, st)) || !ok(hipStreamWaitEvent(sd->s, sd->u1, 0))) return LVAE_ERR_LAUNCH;
+    sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info);
+    sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, sd->s>>>(A, S, np_, nt, k + 1);
+    if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+    if (ntl2 > 0) {
+      ProfScope ps(LVAE_PH_SWEEP_UPD, st);
+      sw_update_kernel<kSwU2><<<ntl2 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl2, ntl2 * L);
     }
   }
+  if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // the whole side chain
+  if (ntll > 0) sw_update_kernel<kSwLast><<<ntll * L, 512, 0, st>>>(A, S, Kinv, np_, nt - 1, ntll, ntll * L);
+  sw_finish_kernel<<<dim3(4 * (2 * (nt - 1) + 1), L), 256, 0, st>>>(A, S, Kinv, np_, nt);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
