@@ -112,7 +112,8 @@ size_t lvae_kl_closed_workspace_size(int n, int L);
  * x: [n, ldx] fp64 covariates; mu, logv: element (i, l) at mu[i*ld_mu + l] (fp64);
  * params [L, n_params] fp64; noise [L] fp64; kl [L] fp64; info [L] int32.
  * workspace: lvae_kl_closed_workspace_size(n, L) bytes, 256-B aligned.
- * need_bwd = 0 skips the K^-1 assembly the backward needs.                                  */
+ * need_bwd != 0 also writes the backward's S-GEMM operand (fp16 planes of K^-1 diag(sqrt v),
+ * per-row scales) into the workspace; lvae_kl_closed_bwd_f32 requires a need_bwd forward.      */
 int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
                            const double* params, const double* noise, const double* mu, const double* logv,
                            int ld_mu, double* kl, int32_t* info, void* workspace, int need_bwd,

@@ -3,8 +3,10 @@
 //
 //   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
 //   K^-1, log|K|                                   (spd_sweep_f32: block symmetric sweep, f16 x3 MFMA)
-//   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation; also the
-//                                                   split bound max |K^-1_ij| sqrt(v_j) of the S GEMM)
+//   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation; when a backward
+//                                                   follows, the same pass writes the S GEMM operand
+//                                                   B = K^-1 diag(sqrt v) as fp16 hi / lo planes with
+//                                                   a per-row power-of-two scale)
 //   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
 // backward (dL/dkl_l = g_l):
 //   S = K^-1 V K^-1                                (syrk_x3_f32, f16 x3 MFMA, lower tiles)
@@ -22,8 +24,7 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L);
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
                 double* part, double* dparams, double* dnoise, hipStream_t st);
-int syrk_x3_f32(int np_, int L, const float* Kinv, const float* sv, const uint32_t* bmax, _Float16* planes, float* S,
-                hipStream_t st);
+int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, hipStream_t st);
 int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
                   hipStream_t st);
 size_t spd_sweep_scratch_bytes(int np_, int L);
@@ -31,8 +32,8 @@ size_t spd_sweep_scratch_bytes(int np_, int L);
 struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
   _Float16* planes;  // fp16 hi / lo planes of the S GEMM operand: 2 L np^2 halves
-  uint32_t* bmax;    // [L] fp32 bits of max |K^-1_ij| sqrt(v_j)
-  float* rmax;       // [L, np] per-row maxima of the same
+  float* rsc;        // [L, np] their per-row split scales
+  float* gb;         // [L] max_j sqrt(Kinv_jj v_j) (kl_bdiag_kernel)
   char* sweep;
   double *mu, *alpha, *kdiag, *logdet, *part;
   size_t bytes;
@@ -49,8 +50,8 @@ struct KLWorkspace {
     Kinv = (float*)take(mat);
     v = (float*)take((size_t)L * np_ * sizeof(float));
     sv = (float*)take((size_t)L * np_ * sizeof(float));
-    bmax = (uint32_t*)take((size_t)L * sizeof(uint32_t));
-    rmax = (float*)take((size_t)L * np_ * sizeof(float));
+    rsc = (float*)take((size_t)L * np_ * sizeof(float));
+    gb = (float*)take((size_t)L * sizeof(float));
     mu = (double*)take((size_t)L * np_ * sizeof(double));
     alpha = (double*)take((size_t)L * np_ * sizeof(double));
     kdiag = (double*)take((size_t)L * np_ * sizeof(double));
@@ -73,66 +74,86 @@ __global__ void kl_prep_kernel(const double* __restrict__ mu, const double* __re
   sv[(int64_t)l * np_ + i] = (float)sqrt(vv);
 }
 
-// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]; rmax[l][i] =
-// max_j |Kinv[i][j]| sqrt(v_j) (reduced to the split bound of the S GEMM operand by kl_finalize)
+// g[l] = max_j sqrt(Kinv_jj) sqrt(v_j): with |Kinv_ij| <= sqrt(Kinv_ii Kinv_jj) (K^-1 SPD), row i of
+// B = K^-1 diag(sqrt v) is bounded by sqrt(Kinv_ii) g[l] -- the split bound kl_alpha_kernel needs
+// BEFORE it streams the row (one pass over K^-1 instead of two)
+__global__ __launch_bounds__(256) void kl_bdiag_kernel(const float* __restrict__ Kinv, const float* __restrict__ sv,
+                                                       int np_, float* __restrict__ g) {
+  __shared__ float red[4];
+  const int l = blockIdx.x, tid = threadIdx.x;
+  float m = 0.f;
+  for (int j = tid; j < np_; j += 256)
+    m = fmaxf(m, sqrtf(fabsf(Kinv[(int64_t)l * np_ * np_ + (int64_t)j * np_ + j])) * sv[(int64_t)l * np_ + j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) g[l] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]; with PLANES also
+// row i of the S GEMM operand B = K^-1 diag(sqrt v) as fp16 planes B_ij sc_i = hi + lo, sc_i =
+// x3_scale(sqrt(Kinv_ii) g[l]) (a bound on max_j |B_ij|, kl_bdiag_kernel): the backward's GEMM
+// reads its operand pre-split and nothing re-reads K^-1 for it.
+template <bool PLANES>
 __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ muc,
                                                        const float* __restrict__ sv, int np_,
-                                                       double* __restrict__ alpha, double* __restrict__ kdiag,
-                                                       float* __restrict__ rmax) {
+                                                       const float* __restrict__ g, double* __restrict__ alpha,
+                                                       double* __restrict__ kdiag, float* __restrict__ rsc,
+                                                       _Float16* __restrict__ Bh, _Float16* __restrict__ Bl) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
   const int l = blockIdx.y, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= np_) return;
-  const float* row = Kinv + (int64_t)l * np_ * np_ + (int64_t)i * np_;
+  const int64_t ro = (int64_t)l * np_ * np_ + (int64_t)i * np_;
+  const float* row = Kinv + ro;
   const double* m = muc + (int64_t)l * np_;
   const float* s = sv + (int64_t)l * np_;
+  const float dii = row[i];
+  const float sc = PLANES ? x3_scale(sqrtf(fabsf(dii)) * g[l]) : 0.f;
   double acc = 0.0;
-  float bm = 0.f;
   for (int j = lane * 4; j < np_; j += 256) {
     const float4 k4 = *reinterpret_cast<const float4*>(row + j);
-    const float4 s4 = *reinterpret_cast<const float4*>(s + j);
     acc += (double)k4.x * m[j] + (double)k4.y * m[j + 1] + (double)k4.z * m[j + 2] + (double)k4.w * m[j + 3];
-    bm = fmaxf(fmaxf(bm, fmaxf(fabsf(k4.x) * s4.x, fabsf(k4.y) * s4.y)),
-               fmaxf(fabsf(k4.z) * s4.z, fabsf(k4.w) * s4.w));
+    if constexpr (PLANES) {
+      const float4 s4 = *reinterpret_cast<const float4*>(s + j);
+      const float y[4] = {k4.x * s4.x * sc, k4.y * s4.y * sc, k4.z * s4.z * sc, k4.w * s4.w * sc};
+      half4 h, lo;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        h[q] = (_Float16)y[q];
+        lo[q] = (_Float16)(y[q] - (float)h[q]);
+      }
+      *reinterpret_cast<half4*>(Bh + ro + j) = h;
+      *reinterpret_cast<half4*>(Bl + ro + j) = lo;
+    }
   }
   acc = wave_sum(acc);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
   if (lane == 0) {
     alpha[(int64_t)l * np_ + i] = acc;
-    kdiag[(int64_t)l * np_ + i] = (double)row[i];
-    rmax[(int64_t)l * np_ + i] = bm;
+    kdiag[(int64_t)l * np_ + i] = (double)dii;
+    if (PLANES) rsc[(int64_t)l * np_ + i] = sc;
   }
 }
 
 __global__ __launch_bounds__(256) void kl_finalize_kernel(const double* __restrict__ muc, const double* __restrict__ logv,
                                                           int ld, const double* __restrict__ alpha,
                                                           const double* __restrict__ kdiag,
-                                                          const double* __restrict__ logdet,
-                                                          const float* __restrict__ rmax, int n, int np_,
-                                                          double* __restrict__ kl, uint32_t* __restrict__ bmax) {
+                                                          const double* __restrict__ logdet, int n, int np_,
+                                                          double* __restrict__ kl) {
   __shared__ double red[4];
-  __shared__ float fred[4];
   const int l = blockIdx.x, tid = threadIdx.x;
   double quad = 0.0, tr = 0.0, slv = 0.0;
-  float bm = 0.f;
   for (int i = tid; i < n; i += 256) {
     const double lv = logv[(int64_t)i * ld + l];
     quad += muc[(int64_t)l * np_ + i] * alpha[(int64_t)l * np_ + i];
     tr += exp(lv) * kdiag[(int64_t)l * np_ + i];
     slv += lv;
   }
-  for (int i = tid; i < np_; i += 256) bm = fmaxf(bm, rmax[(int64_t)l * np_ + i]);
   quad = block_sum<256>(quad, red);
   tr = block_sum<256>(tr, red);
   slv = block_sum<256>(slv, red);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
-  if ((tid & 63) == 0) fred[tid >> 6] = bm;
-  __syncthreads();
-  if (tid == 0) {
-    kl[l] = 0.5 * (tr + quad - (double)n + logdet[l] - slv);
-    bmax[l] = __float_as_uint(fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3])));
-  }
+  if (tid == 0) kl[l] = 0.5 * (tr + quad - (double)n + logdet[l] - slv);
 }
 
 __global__ void kl_bwd_elem_kernel(const double* __restrict__ logv, int ld, int n, int np_, int L,
@@ -163,7 +184,6 @@ size_t lvae_kl_closed_workspace_size(int n, int L) {
 int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,
                            const double* noise, const double* mu, const double* logv, int ld_mu, double* kl,
                            int32_t* info, void* workspace, int need_bwd, void* stream) {
-  (void)need_bwd;
   if (!spec) return -1;
   if (!x) return -2;
   if (n <= 0) return -4;
@@ -188,9 +208,16 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   }
   {
     ProfScope ps(LVAE_PH_KL_REDUCE, st);
-    kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.alpha, ws.kdiag, ws.rmax);
-    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, ws.rmax, n, np_, kl,
-                                          ws.bmax);
+    const int64_t per = (int64_t)L * np_ * np_;
+    if (need_bwd) {
+      kl_bdiag_kernel<<<L, 256, 0, st>>>(ws.Kinv, ws.sv, np_, ws.gb);
+      kl_alpha_kernel<true><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.gb, ws.alpha, ws.kdiag,
+                                                               ws.rsc, ws.planes, ws.planes + per);
+    } else {
+      kl_alpha_kernel<false><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, nullptr, ws.alpha,
+                                                                ws.kdiag, nullptr, nullptr, nullptr);
+    }
+    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   }
   LVAE_CHECK_LAUNCH();
   return 0;
@@ -205,11 +232,11 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
-  // S = K^-1 V K^-1 into the (no longer needed) Gram buffer, through the fp16 hi / lo planes of
-  // K^-1 diag(sqrt v) (np is a multiple of 256: lvae_kl_closed_padded_n)
+  // S = K^-1 V K^-1 into the (no longer needed) Gram buffer, from the fp16 hi / lo planes of
+  // K^-1 diag(sqrt v) the forward wrote (need_bwd; np is a multiple of 256: lvae_kl_closed_padded_n)
   {
     ProfScope ps(LVAE_PH_SYRK, st);
-    LVAE_TRY(syrk_x3_f32(np_, L, ws.Kinv, ws.sv, ws.bmax, ws.planes, ws.A, st));
+    LVAE_TRY(syrk_x3_f32(np_, L, ws.rsc, ws.planes, ws.A, st));
   }
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);

@@ -2,9 +2,10 @@
 // on the f16 matrix cores with the fp32-accurate 3-product split (see mfma_x3.hpp for the error
 // argument), specialised for throughput:
 //
-//   split : B sc = K^-1 diag(sqrt v) sc is split ONCE into fp16 hi / lo planes (sc = x3_scale of
-//           max |B|, found by kl_alpha_kernel in the forward; B sc = hi + lo; the
-//           generic x3 tile GEMM re-splits every operand chunk for every output tile);
+//   split : row i of B = K^-1 diag(sqrt v), times sc_i = x3_scale(bound on max_j |B_ij|), is split
+//           ONCE into fp16 hi / lo planes by the forward's kl_alpha_kernel (which reads K^-1 anyway); the
+//           epilogue divides by sc_i sc_j (the generic x3 tile GEMM would re-split every operand
+//           chunk for every output tile);
 //   syrk  : 256 x 256 output tiles, 512 threads = 8 waves (2 along M x 4 along N, 128 x 64 each,
 //           4 x 2 blocks of v_mfma_f32_32x32x16_f16, three products per block and k-step);
 //           operands staged global -> LDS directly (global_load_lds_dwordx4, no VGPR round trip)
@@ -23,33 +24,8 @@
 
 namespace lvae {
 
-__global__ __launch_bounds__(256) void syrk_split_kernel(const float* __restrict__ Kinv, const float* __restrict__ sv,
-                                                         const uint32_t* __restrict__ bmax,
-                                                         _Float16* __restrict__ Bh, _Float16* __restrict__ Bl,
-                                                         int np_, int64_t n4) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n4) return;
-  const int64_t i0 = e * 4;
-  const int64_t per = (int64_t)np_ * np_;
-  const int l = (int)(i0 / per);
-  const int k = (int)(i0 % np_);
-  const sx_f32x4 x = *reinterpret_cast<const sx_f32x4*>(Kinv + i0);
-  const sx_f32x4 s = *reinterpret_cast<const sx_f32x4*>(sv + (int64_t)l * np_ + k);
-  const float sc = x3_scale(__uint_as_float(bmax[l]));
-  sx_half4 h, lo;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float y = x[q] * s[q] * sc;
-    const _Float16 hh = (_Float16)y;
-    h[q] = hh;
-    lo[q] = (_Float16)(y - (float)hh);
-  }
-  *reinterpret_cast<sx_half4*>(Bh + i0) = h;
-  *reinterpret_cast<sx_half4*>(Bl + i0) = lo;
-}
-
 __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
-                                                      const uint32_t* __restrict__ bmax, float* __restrict__ S,
+                                                      const float* __restrict__ rsc, float* __restrict__ S,
                                                       int np_, int ntl, int nwg) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];  // 128 KB, the only LDS object
   // XCD-contiguous remap (bijective): blocks sharing blockIdx % 8 take a contiguous wgid range
@@ -77,30 +53,32 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   sx_gemm(ah, al, bh, bl, ld, np_, lds, acc);
   // epilogue: C layout of 32x32 blocks -- row (e&3) + 8(e>>2) + 4(lane>>5), col lane&31
-  const float sc = x3_scale(__uint_as_float(bmax[l])), inv = 1.0f / (sc * sc);
+  // per-row split scales of B: S_ij = (B sc)_i (B sc)_j^T / (sc_i sc_j) (exact: powers of two)
+  const float* rs = rsc + (int64_t)l * np_;
   float* C = S + base + (int64_t)(I * kSxT + wm) * ld + J * kSxT + wn;
+  float icol[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) icol[b] = 1.0f / rs[J * kSxT + wn + 32 * b + r32];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int e = 0; e < 16; ++e) {
+      const int row = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * kh;
+      const float irow = 1.0f / rs[I * kSxT + wm + row];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * kh, col = 32 * b + r32;
-        C[(int64_t)row * ld + col] = acc[a][b][e] * inv;
-      }
+      for (int b = 0; b < 2; ++b) C[(int64_t)row * ld + 32 * b + r32] = acc[a][b][e] * (irow * icol[b]);
+    }
 }
 
-// S (lower 256-tiles of [L, np, np] fp32) = K^-1 diag(v) K^-1; planes: 2 L np^2 halves of scratch.
-// sv = sqrt(v) [L, np]; bmax[l] = fp32 bits of max_ij |K^-1_ij| sv_j (the split bound of B).
-int syrk_x3_f32(int np_, int L, const float* Kinv, const float* sv, const uint32_t* bmax, _Float16* planes, float* S,
-                hipStream_t st) {
+// S (lower 256-tiles of [L, np, np] fp32) = K^-1 diag(v) K^-1 from the fp16 hi / lo planes of
+// B = K^-1 diag(sqrt v) (2 L np^2 halves: hi then lo), row i scaled by rsc[l][i] (kl_alpha_kernel).
+int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, hipStream_t st) {
   if (np_ % kSxT) return -1;
-  const int64_t per = (int64_t)np_ * np_, n4 = (int64_t)L * per / 4;
-  _Float16* Bh = planes;
-  _Float16* Bl = planes + (int64_t)L * per;
-  syrk_split_kernel<<<cdiv(n4, 256), 256, 0, st>>>(Kinv, sv, bmax, Bh, Bl, np_, n4);
+  const int64_t per = (int64_t)np_ * np_;
+  const _Float16* Bh = planes;
+  const _Float16* Bl = planes + (int64_t)L * per;
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L;
-  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, bmax, S, np_, ntl, nwg);
+  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, rsc, S, np_, ntl, nwg);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -65,9 +65,11 @@ class _KLClosedFn(torch.autograd.Function):
         ws = torch.empty(int(lib.lvae_kl_closed_workspace_size(n, L)), dtype=torch.uint8, device=dev)
         kl = torch.empty(L, dtype=torch.float64, device=dev)
         info = torch.empty(L, dtype=torch.int32, device=dev)
+        # the backward's S GEMM operand is written by the forward only when a backward can follow
+        need_bwd = int(any(t.requires_grad for t in (params, noise, mu, logv)))
         rc = lib.lvae_kl_closed_fwd_f32(spec, _lib.ptr(x64), x64.shape[1], n, L, _lib.ptr(p), _lib.ptr(nz),
                                         _lib.ptr(mu64), _lib.ptr(lv64), L, _lib.ptr(kl), _lib.ptr(info),
-                                        _lib.ptr(ws), 1, _lib.stream_ptr())
+                                        _lib.ptr(ws), need_bwd, _lib.stream_ptr())
         _lib.check(rc, "kl_closed_fwd")
         _check_info(info, "KL_closed cholesky")
         ctx.save_for_backward(p, mu64, lv64, x64, ws)
