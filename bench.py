@@ -45,7 +45,7 @@ DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2_pmc_summary.json")
-U2_NAME = "sw_update_kernel<false,"      # the sweep's rank-256 update U2 (spd_sweep.hip)
+U2_NAME = "sw_update_kernel<0,2>"       # the sweep's interior rank-256 update U2 (spd_sweep.hip, MODE kSwU2)
 
 
 def log(*a):
@@ -278,17 +278,18 @@ def run_closed(args, world, rank, dev):
         res["gp_cholesky_gflops_basis"] = (f"L*N^3/3 (the LAPACK potrf count, SURVEY.md §8(d)) / time of the whole "
                                            f"inverse phase (block-sweep K^-1 + log|K|, {inv_ms:.2f} ms/step on rank 0)")
         res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
-        # dominant kernel: the sweep's rank-256 update U2 (nt - 1 launches per step).  Algorithmic
-        # bytes per launch: every updated lower 256-tile read and written once in fp32 -> 2 x 4 B x
-        # 256^2 per tile, ((nt-1) nt / 2 - 1) tiles per dim, x the dims of this rank.
+        # dominant kernel: the sweep's interior rank-256 update U2 (nt - 1 launches per step; row /
+        # column k+1 go to the short U1 launch ahead of it).  Algorithmic bytes per launch: every
+        # updated lower 256-tile read and written once in fp32 -> 2 x 4 B x 256^2 per tile,
+        # (nt-2) (nt-1) / 2 tiles per dim (I, J not in {k, k+1}), x the dims of this rank.
         nt = np_ // 256
         upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
-        tiles = ((nt - 1) * nt // 2 - 1) * Lr
+        tiles = (nt - 2) * (nt - 1) // 2 * Lr
         upd_bytes = 2 * 4 * 256 * 256 * tiles
         if upd_n:
             avg_s = upd_ms / upd_n * 1e-3
             ach = upd_bytes / avg_s / 1e9
-            res["roofline"] = {"kernel": "sw_update_kernel<false, 2> (sweep rank-256 update U2, spd_sweep.hip)",
+            res["roofline"] = {"kernel": "sw_update_kernel<0, 2> (sweep interior rank-256 update U2, spd_sweep.hip)",
                                "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic((U2_NAME,)) if world == 1 else None,
                                "algorithmic_bytes_per_launch": upd_bytes, "avg_launch_us": avg_s * 1e6,
