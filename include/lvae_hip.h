@@ -5,10 +5,10 @@
  * device memory inside, all work enqueued asynchronously on the caller's hipStream_t (passed as
  * void*), safe to call from several host threads.  Process-wide state is limited to (1) the
  * opt-in phase timer (lvae_prof_*) and (2) the sweep's side stream (lvae_spd_sweep_f32,
- * lvae_kl_closed_fwd_f32): one high-priority stream + fork / join event pair per (device, caller
- * stream), created on first use, kept for the process lifetime, and guarded by a mutex held for
- * each call's whole enqueue sequence.  The calls are graph-capturable (the side stream joins the
- * capture through the fork event).  Return value: 0 = ok, <0 = -(index of the bad argument),
+ * lvae_kl_closed_fwd_f32): one high-priority stream + three events (fork, prep, u1) per (device,
+ * caller stream), created on first use, kept for the process lifetime, and guarded by a mutex held
+ * for each call's whole enqueue sequence.  The calls are graph-capturable (the side stream joins
+ * the capture through the fork event and is joined back before the call returns).  Return value: 0 = ok, <0 = -(index of the bad argument),
  * LVAE_ERR_LAUNCH on a HIP launch error.  Numerical failure (a non-positive-definite pivot) is
  * NOT a return code (the call is asynchronous): it is written to the device `info` array,
  * LAPACK-style (first failing column + 1, 0 = ok), and the Python layer raises
@@ -134,8 +134,10 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
  * A_kk <- -P^-1, A_ik <- A_ik P^-1, A_ij <- A_ij - A_ik P^-1 A_kj (P = A_kk); after the last block
  * A = -K^-1.  np % 256 == 0.  A [L, np, np] (lower 256-block tiles read, overwritten);
  * scratch: lvae_spd_sweep_scratch_size(np, L) bytes, 256-B aligned; Ainv [L, np, np] full
- * symmetric out; logdet [L]; info [L] LAPACK-style (first bad column + 1).  The pivot inverses run
- * on a second (internal, per caller stream) stream joined back to `stream`.
+ * symmetric out; logdet [L]; info [L] LAPACK-style (first bad column + 1).  Pivot blocks are
+ * inverted by a blocked Cholesky in LDS (fp32 MFMA); with lookahead, the next pivot and its
+ * prep run on a second (internal, per caller stream) stream beside each interior update and are
+ * joined back to `stream`.
  * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
 size_t lvae_spd_sweep_scratch_size(int np_, int L);
 int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
