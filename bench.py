@@ -222,7 +222,7 @@ def run_closed(args, world, rank, dev):
     vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(dev)
     kernel = la.generate_kernel(**CFG, latent_dim=L).to(dev)
     lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(dev)
-    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3)
+    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3, fused=True)
     img, mask, X = health_mnist_batch(P, T, seed=100, device=dev)   # the same data set on every rank
     gen = torch.Generator(device=dev).manual_seed(7)
     eps = torch.randn(N, L, device=dev, generator=gen)
@@ -331,7 +331,7 @@ def run_hensman(args, world, rank, dev):
         H = k0(z, z).evaluate() + 1e-6 * torch.eye(M, dtype=torch.float64, device=dev)
     m = torch.zeros(L, M, 1, dtype=torch.float64, device=dev)
     opt = torch.optim.Adam([{"params": k0.parameters()}, {"params": k1.parameters()},
-                            {"params": vae.parameters()}], lr=1e-3, capturable=True)
+                            {"params": vae.parameters()}], lr=1e-3, capturable=True, fused=True)
     hook = ngr = None
     if world > 1:
         from lvae_amd.distributed import GradAllReduce, allreduce_tensors

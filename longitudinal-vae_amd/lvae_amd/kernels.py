@@ -41,6 +41,10 @@ class _Factor(nn.Module):
     def factor_params(self):
         return []
 
+    def factor_raw(self):
+        """[(raw parameter, min_log buffer)] in factor_params order"""
+        return []
+
     def forward(self, x1, x2):
         return Gram(_Scaled(self, None), x1, x2)
 
@@ -88,6 +92,9 @@ class RbfKernel(_Factor):
     def factor_params(self):
         return [self.lengthscale]
 
+    def factor_raw(self):
+        return [(self._log_lengthscale, self.min_log_lengthscale)]
+
 
 class PeriodicKernel(_Factor):
     """exp(-2 sin^2(pi |x1_d - x2_d| / p) / l^2).  EXTENSION (BASELINE config 5): not in the
@@ -112,6 +119,9 @@ class PeriodicKernel(_Factor):
 
     def factor_params(self):
         return [self.lengthscale, self.period]
+
+    def factor_raw(self):
+        return [(self._log_lengthscale, self.min_log_lengthscale), (self._log_period, self.min_log_lengthscale)]
 
 
 class LinearKernel(_Factor):
@@ -166,6 +176,14 @@ class ScaleKernel(nn.Module):
             params += mod.factor_params()
         return [([(k, d) for k, d, _ in facs], params)]
 
+    def raw_components(self):
+        """[(factors, [(raw, min_log)])]: the same parameters, unconstrained"""
+        facs = self.kernel.factors()
+        refs = [(self._log_scale, self.min_log_scale)]
+        for _, _, mod in facs:
+            refs += mod.factor_raw()
+        return [([(k, d) for k, d, _ in facs], refs)]
+
     def forward(self, x1, x2):
         return Gram(AdditiveKernel([self]), x1, x2)
 
@@ -186,6 +204,12 @@ class _Scaled:
         dev = params[0].device if params else None
         one = torch.ones(ld, dtype=torch.float64, device=dev)
         return [([(k, d) for k, d, _ in facs], [one] + params)]
+
+    def raw_components(self):
+        refs = [None]  # the unit scale
+        for _, _, m in self.mod.factors():
+            refs += m.factor_raw()
+        return [([(k, d) for k, d, _ in self.mod.factors()], refs)]
 
     @property
     def latent_dim(self):
@@ -209,6 +233,12 @@ class AdditiveKernel(nn.Module):
             out += k.components()
         return out
 
+    def raw_components(self):
+        out = []
+        for k in self.kernels:
+            out += k.raw_components()
+        return out
+
     def spec(self):
         comps = self.components()
         return _lib.make_spec([c for c, _ in comps])
@@ -228,13 +258,32 @@ class AdditiveKernel(nn.Module):
 
 
 def kernel_spec_and_params(kernel):
-    """(KernelSpec, [L, P] parameter matrix) of an AdditiveKernel / ScaleKernel / factor."""
-    comps = kernel.components()
+    """(KernelSpec, [L, P] parameter matrix) of an AdditiveKernel / ScaleKernel.
+
+    The positivity transform exp(m + softplus(raw - m)) runs ONCE on the stacked raw parameters
+    (a handful of kernels forward and backward) instead of once per parameter tensor: the step is
+    launch-bound at the Hensman sizes, where the per-parameter form cost ~40 launches."""
+    comps = kernel.raw_components()
     spec = _lib.make_spec([c for c, _ in comps])
-    cols = []
-    for _, ps in comps:
-        cols += ps
-    return spec, torch.stack([c.to(torch.float64) for c in cols], dim=-1)
+    refs = [r for _, rs in comps for r in rs]
+    raws = [r for r in refs if r is not None]
+    if not raws:
+        return spec, torch.ones(1, len(refs), dtype=torch.float64)
+    L = raws[0][0].shape[0]
+    R = torch.stack([r[0] for r in raws], 0).to(torch.float64)          # [P', L]
+    m = torch.cat([r[1] for r in raws]).to(torch.float64).unsqueeze(1)  # [P', 1]
+    C = torch.exp(m + F.softplus(R - m))
+    if len(raws) == len(refs):
+        return spec, C.t()
+    one = torch.ones(L, dtype=torch.float64, device=R.device)
+    cols, j = [], 0
+    for r in refs:
+        if r is None:
+            cols.append(one)
+        else:
+            cols.append(C[j])
+            j += 1
+    return spec, torch.stack(cols, dim=-1)
 
 
 # ------------------------------------------------------------------------------------------

@@ -5,7 +5,9 @@ HensmanStep  : hensman_training batch body incl. the natural-gradient update (tr
 GraphedStep  : either step replayed as HIP graphs (torch.cuda.CUDAGraph is a hipGraph on ROCm)
 
 Both steps return detached device scalars; callers read them when they choose (the reference's
-per-step ``.item()`` calls, training.py:137-140, are the sync points this removes).  Each step is
+per-step ``.item()`` calls, training.py:137-140, are the sync points this removes).  Gradients are
+reset to None (``optimiser.zero_grad()``'s default, as training.py:93 calls it): backward then
+assigns each gradient instead of filling it with zeros and adding, two kernels less per parameter.  Each step is
 split into ``forward_backward`` (everything up to the gradients) and ``apply`` (optimiser + state
 updates) so that a data-parallel all-reduce can sit between two captured graphs.
 """
@@ -22,7 +24,7 @@ class ClosedStep:
         self.grad_hook = grad_hook  # e.g. the data-parallel all-reduce
 
     def forward_backward(self, img, mask, X, eps=None):
-        self.opt.zero_grad(set_to_none=False)
+        self.opt.zero_grad(set_to_none=True)
         recon, mu, log_var = self.vae(img, eps)
         mse, nll = self.vae.loss_function(recon, img, mask)
         recon_loss, nll_loss = mse.sum(), nll.sum()
@@ -75,7 +77,7 @@ class HensmanStep:
         self._gm = self._gH = None
 
     def forward_backward(self, img, mask, X, eps=None):
-        self.opt.zero_grad(set_to_none=False)
+        self.opt.zero_grad(set_to_none=True)
         recon, mu, log_var = self.vae(img, eps)
         mse, nll = self.vae.loss_function(recon, img, mask)
         recon_loss, nll_loss = mse.sum(), nll.sum()
