@@ -10,18 +10,17 @@
 // updates), so factor, triangular inverse and product collapse into one HBM-streaming kernel per pass.
 //
 // Per pass k (all L latent dims in every launch):
-//   prep(k)   (one launch, three workgroup roles)
-//             W_i = A_ik P^-1 for i != k (x3 tile GEMM) -> fp32 Wbuf[k & 1][i] ([rows of i][cols of k])
-//                 and the fp16 planes of -256 W_i;
-//             C_j = A_jk for j != k (the unswept column, transposed from row k where j < k) -> the
-//                 fp16 planes of 256 C_j;
-//             the previous pass's swept column Wbuf[(k-1) & 1] copied into its in-place tiles
-//   U1(k)     on a second, highest-priority stream: A_{k+1,k+1} -= W_{k+1} C_{k+1}^T, then
-//   pivot(k+1)  -P^-1 by an in-register Gauss-Jordan sweep of the 256 x 256 block (one 1024-thread
-//             workgroup per dim), log|P|, info -- overlapped with
-//   U2(k)     A_ij += (-W_i) C_j^T for every other lower 256-tile (pre-split planes, DMA-staged, C
-//             streamed non-temporally under the MFMAs); the last pass writes -A to Kinv (both triangles)
+//   pivot(k)  P = A_kk -> -P^-1 into A_kk and the fp16 planes of P^-1 (blocked Cholesky in LDS on
+//             fp32 MFMA, one 1024-thread workgroup per dim), log|P|, info, split bounds
+//   prepC(k)  C_i = A_ik for i != k (the unswept column; tile (k, i)^T where i < k) -> its planes
+//   prepW(k)  W_i = C_i P^-1 from the planes (one 256 x 256 x3 tile GEMM per block), written IN
+//             PLACE into the column's tiles (transposed into tile (k, i) for i < k) and as the
+//             planes of -W_i
+//   U1(k)     row / column k+1 (incl. the next pivot block): A_ij += (-W_i) C_j^T
+//   U2(k)     the interior tiles (I, J not in {k, k+1}), pre-split planes DMA-staged, C streamed
+//             non-temporally under the MFMAs; the last pass writes -A to Kinv (both triangles)
 //   finish    the last swept column and pivot block to Kinv
+// with lookahead: pivot(k+1), prepC(k+1) and prepW(k+1) run on a side stream beside U2(k).
 //
 // Split scales.  Every GEMM operand is split x sc = hi + lo into fp16 planes with a per-(dim, pass)
 // power of two sc = x3_scale(bound), bound >= max |x|, so nothing overflows fp16 whatever the scale
@@ -32,8 +31,8 @@
 //   P^-1                  bound max |P^-1|            (pivot(k), pnorm[l][k][0])
 //   W_i = A_ik P^-1       bound c_k ||P^-1||_1        (pivot(k), pnorm[l][k][1]: max column sum)
 //
-// Scratch (spd_sweep_scratch_bytes): Wbuf 2 x [L, np, 256] fp32, planes Wh Wl Ch Cl [L, np, 256]
-// fp16, cmax [L, nt] u32, pnorm [L, nt, 2] fp32.  A [L, np, np]: lower
+// Scratch (spd_sweep_scratch_bytes): planes Wh Wl Ch Cl 2 x [L, np, 256] fp16 (by pass parity),
+// Ph Pl [L, 256, 256] fp16, cmax [L, nt] u32, pnorm [L, nt, 2] fp32.  A [L, np, np]: lower
 // 256-block tiles read, overwritten.  Kinv [L, np, np]: out, full symmetric.  np % 256 == 0.
 #include "mfma_x3.hpp"
 #include "prof.hpp"
@@ -47,12 +46,12 @@
 namespace lvae {
 
 constexpr int kSwB = 256;  // pivot block
-constexpr int kSwT = 128;  // output tile of tile_gemm_x3 (prep)
+constexpr int kSwT = 128;  // sub-tile of the prepC / finish copies
 constexpr int kSwBB = kSwB * kSwB;
 
 struct SwScratch {
-  float* W[2];                  // [L][np][256]
   _Float16 *Wh[2], *Wl[2], *Ch[2], *Cl[2];  // [L][np][256], by pass parity (prep(k+1) runs beside U2(k))
+  _Float16 *Ph, *Pl;                         // [L][256][256] planes of P^-1 sP
   uint32_t* cmax;               // [L][nt]   fp32 bits of max |column k| (atomicMax)
   float* pnorm;                 // [L][nt][2] max |P_k^-1|, max column abs-sum of P_k^-1
   int nt;
@@ -65,14 +64,14 @@ struct SwScratch {
       return p;
     };
     const size_t col = (size_t)L * np_ * kSwB;
-    W[0] = (float*)take(col * 4);
-    W[1] = (float*)take(col * 4);
     for (int b = 0; b < 2; ++b) {
       Wh[b] = (_Float16*)take(col * 2);
       Wl[b] = (_Float16*)take(col * 2);
       Ch[b] = (_Float16*)take(col * 2);
       Cl[b] = (_Float16*)take(col * 2);
     }
+    Ph = (_Float16*)take((size_t)L * kSwBB * 2);
+    Pl = (_Float16*)take((size_t)L * kSwBB * 2);
     nt = np_ / kSwB;
     cmax = (uint32_t*)take((size_t)L * nt * 4);
     pnorm = (float*)take((size_t)L * nt * 2 * 4);
@@ -373,6 +372,17 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
       for (int k = i; k < 8; ++k) pv_mma<true, true>(res[h], pv_blk(lf, k, i), pv_blk(lf, k, j), rl, hh);
     }
   }
+  {  // max |P^-1| before the planes are written (their split scale)
+    float pm = 0.f;
+#pragma unroll
+    for (int h = 0; h < 3; ++h)
+      if (kLauum[w][h] >= 0)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pm = fmaxf(pm, fabsf(res[h][e]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pm = fmaxf(pm, __shfl_xor(pm, o, 64));
+    if (lane == 0) atomicMax(&pmax_s, __float_as_uint(pm));
+  }
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
@@ -382,22 +392,25 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   __syncthreads();
   PV_T(22);
 
-  // 4. out: T = -P^-1, both triangles (a wave writes 256 consecutive floats of one row; the LDS reads
-  //    are consecutive (lower part) or pitch-33 strided (mirror): conflict-free); split bounds: max
-  //    |P^-1| and the column abs-sums
+  // 4. out: T = -P^-1 (both triangles) and the planes of P^-1 sP for prepW (a wave writes 256
+  //    consecutive elements of one row; the LDS reads are consecutive (lower part) or pitch-33
+  //    strided (mirror): conflict-free); the column abs-sums (split bound of W)
   const int c = tid & 255;
-  float cs = 0.f, pm = 0.f;
+  const float sP = x3_scale(__uint_as_float(pmax_s));
+  _Float16* ph = S.Ph + (int64_t)l * kSwBB;
+  _Float16* pl = S.Pl + (int64_t)l * kSwBB;
+  float cs = 0.f;
   for (int r = tid >> 8; r < kSwB; r += 4) {
     const float v = r >= c ? pv_blk(lf, r >> 5, c >> 5)[(r & 31) * kPvL + (c & 31)]
                            : pv_blk(lf, c >> 5, r >> 5)[(c & 31) * kPvL + (r & 31)];
     T[(int64_t)r * np_ + c] = -v;
+    const float y = v * sP;
+    const _Float16 yh = (_Float16)y;
+    ph[r * kSwB + c] = yh;
+    pl[r * kSwB + c] = (_Float16)(y - (float)yh);
     cs += fabsf(v);
-    pm = fmaxf(pm, fabsf(v));
   }
   atomicAdd(&colsum[c], cs);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) pm = fmaxf(pm, __shfl_xor(pm, o, 64));
-  if (lane == 0) atomicMax(&pmax_s, __float_as_uint(pm));
   if (w == 0 && lane == 0) bad_s = bad;
   __syncthreads();
   if (tid < kSwB) atomicMax(&pn1_s, __float_as_uint(colsum[tid]));
@@ -419,8 +432,8 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
 // ------------------------------------------------------------------------------------------
 template <typename Fn>
 __device__ inline void blk128_visit(const float* __restrict__ src, int64_t ld, bool trans, float* __restrict__ lds,
-                                    Fn fn) {
-  const int t = threadIdx.x, c4 = t & 15, r0 = t >> 4;
+                                    Fn fn, int t = threadIdx.x) {
+  const int c4 = t & 15, r0 = t >> 4;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (trans) {
@@ -462,90 +475,97 @@ __device__ inline void sw_split4(f32x4 v, float s, _Float16* __restrict__ hi, _F
   *reinterpret_cast<x3_half4*>(lo) = l;
 }
 
-constexpr int cmaxi(int a, int b) { return a > b ? a : b; }
+// ------------------------------------------------------------------------------------------
+// prepC(k): the planes of C_i = A_ik (i != k; tile (i, k), or tile (k, i)^T for i < k, which for
+// i = k-1 already holds the previous pass's swept W^{k-1}_k^T in place), scale sC.  grid (4 nt, L):
+// (block i, 128 x 128 sub-tile (sm, sn)), 256 threads -- a wide launch of its own: folded into the
+// GEMM's workgroups (one per block) the same work measured slower (126 vs 55 + 79 us per pass).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sw_prepc_kernel(const float* __restrict__ Aall, SwScratch S, int np_, int k) {
+  __shared__ float lds[64 * 129];
+  const int l = blockIdx.y, w = blockIdx.x, i = w >> 2, sm = (w >> 1) & 1, sn = w & 1;
+  if (i == k) return;
+  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
+  const float* A = Aall + l * np2;
+  const int64_t sub = (int64_t)i * kSwBB + sm * kSwT * kSwB + sn * kSwT;
+  const float* src = i > k ? A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB + sn * kSwT
+                           : A + ((int64_t)k * kSwB + sn * kSwT) * np_ + i * kSwB + sm * kSwT;
+  _Float16* h = S.Ch[k & 1] + l * col + sub;
+  _Float16* lo = S.Cl[k & 1] + l * col + sub;
+  const float scc = sw_scales(S, l, k).c;
+  blk128_visit(src, np_, i < k, lds,
+               [&](int r, int c, f32x4 v) { sw_split4(v, scc, h + r * kSwB + c, lo + r * kSwB + c); });
+}
 
 // ------------------------------------------------------------------------------------------
-// prep(k): grid.x = 3 * 4 nt (role = blockIdx.x / 4 nt), grid.y = L; (block i, sub-tile sm, sn)
-//   role 0: W_i (i != k) = A_ik P^-1  (x3 tile GEMM; A_ik = tile (i, k) or tile (k, i)^T)
-//   role 1: C planes of block i (i != k) = split(256 A_ik)
-//   role 2: (k >= 1) copy of the previous pass's W_i into its in-place tile (i != k-1)
-// Tile (k, k-1) is still being copied in this launch: its readers take it from Wprev[k] instead.
+// prepW(k): W_i = A_ik P^-1 = (C_i sC)(P^-1 sP) / (sC sP) for i != k: one 512-thread workgroup per
+// 256 x 256 block on the pre-split planes (sx_gemm, K = 256), grid (nt - 1, L).  W_i goes IN PLACE
+// into the swept column -- tile (i, k), or transposed (through LDS) into tile (k, i) for i < k: the
+// column's readers are done (prepC read it, U1 / U2 read only planes) -- and as the planes of -W_i sW.
+// W_{k+1} is part of column k+1, so its max |W| folds into cmax[k+1].
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sw_prep_kernel(float* __restrict__ Aall, SwScratch S, int np_, int nt, int k) {
-  __shared__ __attribute__((aligned(16))) char lds[cmaxi(x3_lds_bytes(), 64 * 129 * 4)];
-  const int l = blockIdx.y, role = blockIdx.x / (4 * nt), w = blockIdx.x % (4 * nt);
-  const int i = w >> 2, sm = (w >> 1) & 1, sn = w & 1;
+__global__ __launch_bounds__(512) void sw_prepw_kernel(float* __restrict__ Aall, SwScratch S, int np_, int k) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  const int l = blockIdx.y, i = blockIdx.x < k ? blockIdx.x : blockIdx.x + 1;
   const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
+  const int64_t oc = l * col + (int64_t)i * kSwBB, op = (int64_t)l * kSwBB;
+  const SwScales sc = sw_scales(S, l, k);
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  sx_gemm(S.Ch[k & 1] + oc, S.Cl[k & 1] + oc, S.Ph + op, S.Pl + op, kSwB, kSwB, lds, acc);
+  const float inv = 1.0f / (sc.c * sc.p);
+  _Float16* wh = S.Wh[k & 1] + oc;
+  _Float16* wl = S.Wl[k & 1] + oc;
   float* A = Aall + l * np2;
-  float* Wc = S.W[k & 1] + l * col;
-  const float* Wp = S.W[(k + 1) & 1] + l * col;
-  const int64_t sub = (int64_t)i * kSwBB + sm * kSwT * kSwB + sn * kSwT;  // sub-tile (sm, sn) of block row i
-  if (role == 0) {
-    if (i == k) return;
-    const SwScales sc = sw_scales(S, l, k);
-    const float* P = A + (int64_t)k * kSwB * np_ + k * kSwB;  // -P^-1 (the pivot's output, both triangles)
-    Frag f;
-    f.zero();
-    if (i > k) {
-      tile_gemm_x3<true, true, true>(A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB, np_, P + sn * kSwT * np_, np_,
-                               0, kSwB, f, (_Float16*)lds, sc.c, sc.p);
-    } else {
-      // A_ik(m, t) = tile (k, i)[t][m]; tile (k, k-1) is Wprev[k] ([rows of k][cols of k-1])
-      const float* src = (i == k - 1) ? Wp + (int64_t)k * kSwBB : A + (int64_t)k * kSwB * np_ + i * kSwB;
-      const int64_t ls = (i == k - 1) ? kSwB : np_;
-      tile_gemm_x3<false, true, true>(src + sm * kSwT, ls, P + sn * kSwT * np_, np_, 0, kSwB, f, (_Float16*)lds, sc.c,
-                                sc.p);
+  float wm = 0.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = sx_row(a, e), c = sx_col(b);
+        const float v = acc[a][b][e] * inv;
+        acc[a][b][e] = v;
+        wm = fmaxf(wm, fabsf(v));
+        const float y = -v * sc.w;
+        const _Float16 yh = (_Float16)y;
+        wh[r * kSwB + c] = yh;
+        wl[r * kSwB + c] = (_Float16)(y - (float)yh);
+        if (i > k) A[(int64_t)(i * kSwB + r) * np_ + k * kSwB + c] = v;
+      }
+  if (i < k) {  // tile (k, i) = W_i^T, per 128-row half of W through LDS (coalesced 512-B rows)
+    float* U = reinterpret_cast<float*>(lds);
+    const int tid = threadIdx.x, w = tid >> 6;
+    float* Ot = A + (int64_t)k * kSwB * np_ + i * kSwB;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      __syncthreads();  // hh = 0: the GEMM's last LDS reads; hh = 1: the half-0 readers
+      if ((w >> 2) == hh) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              const int rl = sx_row(a, e) - 128 * hh, c = sx_col(b);
+              U[c * 128 + (rl ^ ((c & 31) << 2))] = acc[a][b][e];
+            }
+      }
+      __syncthreads();
+      const int t4 = tid & 31;
+#pragma unroll 4
+      for (int cc = 0; cc < kSwB; cc += 16) {
+        const int c = cc + (tid >> 5), rl = 4 * t4;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(&U[c * 128 + (rl ^ ((c & 31) << 2))]);
+        *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + 128 * hh + rl) = v;
+      }
     }
-    float* C = Wc + sub;
-    _Float16* h = S.Wh[k & 1] + l * col + sub;
-    _Float16* lo = S.Wl[k & 1] + l * col + sub;
-    float wm = 0.f;
-    frag_foreach(f, [&](int r, int c, float v) {
-      C[r * kSwB + c] = v;
-      wm = fmaxf(wm, fabsf(v));
-      const float y = -v * sc.w;
-      const _Float16 hh = (_Float16)y;
-      h[r * kSwB + c] = hh;
-      lo[r * kSwB + c] = (_Float16)(y - (float)hh);
-    });
-    // W_{k+1} (this pass's swept column, block k+1) becomes part of the C operand of pass k+1
-    if (i == k + 1) sw_fold_max(wm, S.cmax + l * S.nt + k + 1);
-  } else if (role == 1) {
-    if (i == k) return;
-    // C_i(m, t) = A_ik: tile (i, k) for i > k; tile (k, i)^T for i < k (Wprev[k]^T for i = k-1)
-    const float* src;
-    int64_t ls;
-    if (i > k) {
-      src = A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB + sn * kSwT;
-      ls = np_;
-    } else if (i == k - 1) {
-      src = Wp + (int64_t)k * kSwBB + sn * kSwT * kSwB + sm * kSwT;
-      ls = kSwB;
-    } else {
-      src = A + ((int64_t)k * kSwB + sn * kSwT) * np_ + i * kSwB + sm * kSwT;
-      ls = np_;
-    }
-    _Float16* h = S.Ch[k & 1] + l * col + sub;
-    _Float16* lo = S.Cl[k & 1] + l * col + sub;
-    const float scc = sw_scales(S, l, k).c;
-    blk128_visit(src, ls, i < k, (float*)lds,
-                 [&](int r, int c, f32x4 v) { sw_split4(v, scc, h + r * kSwB + c, lo + r * kSwB + c); });
-  } else {
-    const int c = k - 1;
-    if (k == 0 || i == c) return;
-    // tile (i, c) = W_i for i > c; tile (c, i) = W_i^T for i < c
-    float* dst;
-    const float* src;
-    if (i > c) {
-      dst = A + ((int64_t)i * kSwB + sm * kSwT) * np_ + c * kSwB + sn * kSwT;
-      src = Wp + sub;
-    } else {
-      dst = A + ((int64_t)c * kSwB + sm * kSwT) * np_ + i * kSwB + sn * kSwT;
-      src = Wp + (int64_t)i * kSwBB + sn * kSwT * kSwB + sm * kSwT;
-    }
-    blk128_visit(src, kSwB, i < c, (float*)lds,
-                 [&](int r, int cc, f32x4 v) { *reinterpret_cast<f32x4*>(dst + (int64_t)r * np_ + cc) = v; });
   }
+  if (i == k + 1) sw_fold_max(wm, S.cmax + l * S.nt + k + 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -707,26 +727,25 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
                                                         float* __restrict__ Kinv, int np_, int nt) {
   __shared__ float lds[64 * 129];
   const int l = blockIdx.y, w = blockIdx.x, blk = w >> 2, sm = (w >> 1) & 1, sn = w & 1, c = nt - 1;
-  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
-  const float* Wc = S.W[c & 1] + l * col;
+  const int64_t np2 = (int64_t)np_ * np_;
+  const float* A = Aall + l * np2;
+  // the last swept column is in place: tile (c, i) = A_ci = W_i^T (i < c)
   const float* src;
-  int64_t ls, r0, c0;
+  const int64_t ls = np_;
+  int64_t r0, c0;
   bool tr = false;
-  if (blk < c) {
-    src = Wc + (int64_t)blk * kSwBB + sm * kSwT * kSwB + sn * kSwT;
-    ls = kSwB;
+  if (blk < c) {  // Kinv (i, c) = -tile (c, i)^T
+    src = A + (int64_t)(c * kSwB + sn * kSwT) * np_ + blk * kSwB + sm * kSwT;
+    tr = true;
     r0 = blk * kSwB + sm * kSwT;
     c0 = c * kSwB + sn * kSwT;
-  } else if (blk < 2 * c) {
+  } else if (blk < 2 * c) {  // Kinv (c, i) = -tile (c, i)
     const int i = blk - c;
-    src = Wc + (int64_t)i * kSwBB + sn * kSwT * kSwB + sm * kSwT;
-    ls = kSwB;
-    tr = true;
+    src = A + (int64_t)(c * kSwB + sm * kSwT) * np_ + i * kSwB + sn * kSwT;
     r0 = c * kSwB + sm * kSwT;
     c0 = i * kSwB + sn * kSwT;
   } else {
-    src = Aall + l * np2 + (int64_t)(c * kSwB + sm * kSwT) * np_ + c * kSwB + sn * kSwT;
-    ls = np_;
+    src = A + (int64_t)(c * kSwB + sm * kSwT) * np_ + c * kSwB + sn * kSwT;
     r0 = c * kSwB + sm * kSwT;
     c0 = c * kSwB + sn * kSwT;
   }
@@ -793,14 +812,18 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
   if (nt > 1) sw_colmax_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
   sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info);
-  if (nt > 1) sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, sd->s>>>(A, S, np_, nt, 0);
+  if (nt > 1) {
+    sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, 0);
+    sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, 0);
+  }
   if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
   for (int k = 0; k + 1 < nt; ++k) {
     if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prep(k)
     sw_update_kernel<kSwU1><<<ntl1 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl1, ntl1 * L);
     if (!ok(hipEventRecord(sd->u1, st)) || !ok(hipStreamWaitEvent(sd->s, sd->u1, 0))) return LVAE_ERR_LAUNCH;
     sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info);
-    sw_prep_kernel<<<dim3(3 * 4 * nt, L), 256, 0, sd->s>>>(A, S, np_, nt, k + 1);
+    sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, k + 1);
+    sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, k + 1);
     if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
     if (ntl2 > 0) {
       ProfScope ps(LVAE_PH_SWEEP_UPD, st);
