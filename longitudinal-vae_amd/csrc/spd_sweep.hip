@@ -139,7 +139,11 @@ typedef float pv_f32x16 __attribute__((ext_vector_type(16)));
 #ifdef LVAE_PV_TIMING
 __device__ unsigned long long g_pv_t[64];
 #define PV_T(i) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_pv_t[i] = wall_clock64(); } while (0)
+// U2 probes (pass k == 4): per workgroup {start, first chunk staged, loop end, end, summed chunk waits, smid}
+__device__ unsigned long long g_u2_t[4096 * 6];
+#define U2_T(j, v) do { if (MODE == kSwU2 && k == 4 && threadIdx.x == 0) g_u2_t[wgid * 6 + (j)] = (v); } while (0)
 #else
+#define U2_T(j, v) do { } while (0)
 #define PV_T(i) do { } while (0)
 #endif
 
@@ -572,7 +576,7 @@ __global__ __launch_bounds__(512) void sw_prepw_kernel(float* __restrict__ Aall,
 // update(k): A_IJ += (-W_I) C_J^T on lower 256-tiles (I >= J, I, J != k), K = 256: one 512-thread
 // workgroup per 256 x 256 tile on the pre-split fp16 planes (x3_dma.hpp layout and DMA staging,
 // double-buffered K chunks of 32).  C enters in 8 chunks of 16 accumulator elements INSIDE the K
-// loop (chunk j loaded in step j, added in step j + 1), read and written non-temporally (CAUX = slc:
+// loop (chunk j loaded in step j, added in step j + 2), read and written non-temporally (CAUX = slc:
 // the C stream does not evict the planes from L2).  Measured at np = 4096, L = 16: C streaming alone
 // ~200 us, the GEMM alone ~200 us, together 293 us per launch (a 256 x 128 half-tile form with two
 // workgroups per CU moved 1.5x the plane bytes and took 350-410 us).  Three tile sets (MODE):
@@ -621,28 +625,43 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
-  // chunk j = accumulator elements 16 j .. 16 j + 15 (a = i >> 5, e = (i >> 1) & 15, b = i & 1)
-  float cv[16];
+  // chunk j = accumulator elements 16 j .. 16 j + 15 (a = i >> 5, e = (i >> 1) & 15, b = i & 1),
+  // loaded in step j AFTER that step's plane DMA and added in step j + 2: the counted wait of step
+  // j + 1 (vmcnt(16)) retires DMA j + 1 and leaves C chunk j in flight
+  float cv[2][16];
   constexpr int nk = kSwB / kSxBK;
   static_assert(nk * 16 == 128, "one C chunk per K step");
+#ifdef LVAE_PV_TIMING
+  unsigned long long t_wait = 0, t_w0 = wall_clock64();
+  U2_T(0, t_w0);
+  U2_T(5, (unsigned long long)__smid());
+#endif
   sx_issue(ah, al, bh, bl, kSwB, 0, lds);
 #pragma unroll
   for (int s = 0; s < nk; ++s) {
-    SX_WAIT_VM(0);  // chunk s staged, C chunk s - 1 landed
+#ifdef LVAE_PV_TIMING
+    t_w0 = wall_clock64();
+#endif
+    if (s == 0) SX_WAIT_VM(0);
+    else __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): DMA s and C chunk s - 2 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+#ifdef LVAE_PV_TIMING
+    if (s == 0) U2_T(1, wall_clock64());
+    else t_wait += wall_clock64() - t_w0;
+#endif
     if (s + 1 < nk) sx_issue(ah, al, bh, bl, kSwB, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
-    if (s >= 1) {
+    if (s >= 2) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int i = 16 * (s - 1) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
-        acc[a][b][e] += cv[q] * cs;
+        const int i = 16 * (s - 2) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+        acc[a][b][e] += cv[s & 1][q] * cs;
       }
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int i = 16 * s + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
-      cv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+      cv[s & 1][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
           rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX));
     }
     __builtin_amdgcn_s_setprio(1);
@@ -650,10 +669,16 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
     __builtin_amdgcn_s_setprio(0);
   }
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int i = 16 * (nk - 1) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
-    acc[a][b][e] += cv[q] * cs;
-  }
+  for (int j = nk - 2; j < nk; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = 16 * j + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      acc[a][b][e] += cv[j & 1][q] * cs;
+    }
+#ifdef LVAE_PV_TIMING
+  U2_T(2, wall_clock64());
+  U2_T(4, t_wait);
+#endif
   if constexpr (!LAST) {
     float mx = 0.f;
 #pragma unroll
@@ -669,6 +694,10 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
         }
     // tiles of row / column k+1 (not the next pivot block): the C operand of the next pass
     if (MODE == kSwU1 && I != J) sw_fold_max(mx, S.cmax + l * S.nt + k + 1);
+#ifdef LVAE_PV_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    U2_T(3, wall_clock64());
+#endif
   } else {
     // -result to Kinv (I, J) (diagonal tiles: lower elements only) and, transposed through LDS, to
     // (J, I): per 128-row half of the tile, U[c][r ^ 4 (c & 31)] = value (r, c), read back as float4
@@ -846,6 +875,12 @@ int lvae_pv_timing(float* A, int np_, int L, void* scratch, double* logdet, int3
   lvae::sw_pivot_kernel<<<L, 1024>>>(A, np_, 0, S, logdet, info);
   (void)hipDeviceSynchronize();
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lvae::g_pv_t), sizeof(unsigned long long) * 64);
+}
+int lvae_u2_timing(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
+                   unsigned long long* out) {
+  const int rc = lvae::spd_sweep_f32(np_, L, A, scratch, Kinv, logdet, info, nullptr);
+  (void)hipDeviceSynchronize();
+  return rc ? rc : (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lvae::g_u2_t), sizeof(unsigned long long) * 4096 * 6);
 }
 #endif
 size_t lvae_spd_sweep_scratch_size(int np_, int L) { return lvae::spd_sweep_scratch_bytes(np_, L); }

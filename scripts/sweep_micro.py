@@ -26,7 +26,7 @@ info = torch.zeros(L, dtype=torch.int32, device=dev)
 A = A0.clone()
 VARIANTS = {"base": {}}  # add env overrides here to time variants side by side
 for var in os.environ.get("LVAE_MICRO_VARIANTS", "base").split(","):
-        os.environ.update(VARIANTS[var])
+    os.environ.update(VARIANTS[var])
     ts = []
     for r in range(reps):
         A.copy_(A0)
