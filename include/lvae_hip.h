@@ -215,6 +215,15 @@ int lvae_relu_maxpool2_fwd_f32(const float* x, int64_t planes, int H, int W, flo
                                void* stream);
 int lvae_relu_maxpool2_bwd_f32(const float* gy, const float* y, const uint8_t* idx, int64_t planes, int H,
                                int W, float* gx, void* stream);
+/* The same with the conv's per-channel bias folded in (the conv then runs without one): x is the
+ * bias-free conv output [N, C, H, W], y = max_pool2d(relu(x + bias)); the backward also writes
+ * db [C] = the conv's bias gradient (deterministic; workspace: lvae_relu_maxpool2_bias_workspace_size
+ * bytes).  Replaces nn.Conv2d's bias add and its bias-gradient sum (VAE.py:44-50).             */
+size_t lvae_relu_maxpool2_bias_workspace_size(int N, int C);
+int lvae_relu_maxpool2_bias_fwd_f32(const float* x, const float* bias, int N, int C, int H, int W, float* y,
+                                    uint8_t* idx, void* stream);
+int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8_t* idx, int N, int C, int H, int W,
+                                    float* gx, float* db, void* workspace, void* stream);
 
 /* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
  * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject

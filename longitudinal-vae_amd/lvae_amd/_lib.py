@@ -100,6 +100,9 @@ SIGNATURES = {
     "lvae_hensman_iH_offset": (_SZ, [_DIMS]),
     "lvae_relu_maxpool2_fwd_f32": (_I32, [_VP, _I64, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _I32, _I32, _VP, _VP]),
+    "lvae_relu_maxpool2_bias_workspace_size": (_SZ, [_I32, _I32]),
+    "lvae_relu_maxpool2_bias_fwd_f32": (_I32, [_VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
+    "lvae_relu_maxpool2_bias_bwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),

@@ -43,6 +43,57 @@ class _ReluMaxPool2(torch.autograd.Function):
         return gx
 
 
+class _ConvReluMaxPool2(torch.autograd.Function):
+    """max_pool2d(relu(conv2d(x, w, b, padding=1)), 2, 2) (VAE.py:44-50): the 3x3 conv runs without
+    its bias on MIOpen; bias add, relu and pool are one HIP pass (lvae_relu_maxpool2_bias_fwd_f32), and
+    the backward's routing pass also returns the bias gradient (lvae_relu_maxpool2_bias_bwd_f32), so
+    neither the full-resolution bias add nor torch's strided bias-gradient sum runs."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from . import _lib
+        lib = _lib.lib()
+        y0 = F.conv2d(x, weight, None, 1, 1).contiguous()
+        N, C, H, W = y0.shape
+        b = bias.contiguous()
+        y = torch.empty(N, C, H // 2, W // 2, dtype=y0.dtype, device=y0.device)
+        idx = torch.empty(N, C, H // 2, W // 2, dtype=torch.uint8, device=y0.device)
+        _lib.check(lib.lvae_relu_maxpool2_bias_fwd_f32(_lib.ptr(y0), _lib.ptr(b), N, C, H, W, _lib.ptr(y),
+                                                        _lib.ptr(idx), _lib.stream_ptr()), "relu_maxpool2_bias_fwd")
+        ctx.save_for_backward(x, weight, y, idx)
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import _lib
+        lib = _lib.lib()
+        x, weight, y, idx = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        gy = gy.contiguous()
+        g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
+        db = torch.empty(C, dtype=gy.dtype, device=gy.device)
+        ws = torch.empty(lib.lvae_relu_maxpool2_bias_workspace_size(N, C) // 4 + 1, dtype=torch.float32,
+                         device=gy.device)
+        _lib.check(lib.lvae_relu_maxpool2_bias_bwd_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), N, C, H, W,
+                                                        _lib.ptr(g0), _lib.ptr(db), _lib.ptr(ws), _lib.stream_ptr()),
+                   "relu_maxpool2_bias_bwd")
+        gx = gw = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            gx, gw, _ = torch.ops.aten.convolution_backward(
+                g0, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return gx, gw, db if ctx.needs_input_grad[2] else None
+
+
+def conv_relu_maxpool2(conv, x):
+    """pool(relu(conv(x))) for the encoder's 3x3 / padding-1 convs: fused bias path for CUDA fp32."""
+    if (x.is_cuda and x.dtype == torch.float32 and conv.bias is not None and conv.weight.dtype == torch.float32
+            and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0):
+        return _ConvReluMaxPool2.apply(x, conv.weight, conv.bias)
+    return relu_maxpool2(conv(x))
+
+
 def relu_maxpool2(x):
     """pool(relu(x)) of the encoder (VAE.py:44-50): fused HIP kernel for CUDA fp32 activations."""
     if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0:
@@ -91,8 +142,8 @@ class ConvVAE(nn.Module):
         return torch.exp(self.min_log_vy + F.softplus(self._log_vy - self.min_log_vy))
 
     def encode(self, x):
-        z = self.dropout2d_1(relu_maxpool2(self.conv1(x)))   # pool1(relu(conv1))
-        z = self.dropout2d_2(relu_maxpool2(self.conv2(z)))   # pool2(relu(conv2))
+        z = self.dropout2d_1(conv_relu_maxpool2(self.conv1, x))   # pool1(relu(conv1))
+        z = self.dropout2d_2(conv_relu_maxpool2(self.conv2, z))   # pool2(relu(conv2))
         h1 = self.dropout1(F.relu(self.fc1(z.reshape(-1, 32 * 9 * 9))))
         h2 = self.dropout2(F.relu(self.fc21(h1)))
         return self.fc211(h2), self.fc221(h2)

@@ -243,6 +243,59 @@ def test_relu_maxpool2_matches_torch(hip):
     assert torch.equal(xa.grad, xb.grad)
 
 
+@pytest.mark.parametrize("n,c,hw", [(5, 16, 36), (37, 32, 18)])
+def test_relu_maxpool2_bias_kernels_match_torch(hip, n, c, hw):
+    """The bias-folded relu + pool kernels on a given conv output y0 vs torch's y0 + b -> relu ->
+    max_pool2d: pooled values and the routed gradient bit-exact, the bias gradient to fp32
+    summation order."""
+    import torch.nn.functional as F
+    from lvae_amd import _lib
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    y0 = torch.randn(n, c, hw, hw, device=DEV, generator=gen)
+    y0[0, 0, :4, :4] = -5.0      # all-negative windows
+    y0[1, 1, 2:4, 2:4] = 0.25    # ties
+    b = torch.randn(c, device=DEV, generator=gen)
+    y = torch.empty(n, c, hw // 2, hw // 2, device=DEV)
+    idx = torch.empty(n, c, hw // 2, hw // 2, dtype=torch.uint8, device=DEV)
+    _lib.check(hip.lvae_relu_maxpool2_bias_fwd_f32(_lib.ptr(y0), _lib.ptr(b), n, c, hw, hw, _lib.ptr(y), _lib.ptr(idx),
+                                                    _lib.stream_ptr()), "fwd")
+    yr = y0.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    ref = F.max_pool2d(F.relu(yr + br.view(1, -1, 1, 1)), 2, 2)
+    assert torch.equal(y, ref)
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    ref.backward(g)
+    gx = torch.empty_like(y0)
+    db = torch.empty(c, device=DEV)
+    ws = torch.empty(hip.lvae_relu_maxpool2_bias_workspace_size(n, c) // 4 + 1, device=DEV)
+    _lib.check(hip.lvae_relu_maxpool2_bias_bwd_f32(_lib.ptr(g), _lib.ptr(y), _lib.ptr(idx), n, c, hw, hw, _lib.ptr(gx),
+                                                    _lib.ptr(db), _lib.ptr(ws), _lib.stream_ptr()), "bwd")
+    assert torch.equal(gx, yr.grad)
+    assert float((db - br.grad).abs().max() / br.grad.abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("n,cin,cout,hw", [(5, 1, 16, 36), (37, 16, 32, 18)])
+def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw):
+    """Encoder conv with its bias folded into the fused relu + pool pass (bias gradient from its
+    backward, weight / input gradients from aten.convolution_backward) vs nn.Conv2d -> relu ->
+    max_pool2d, to fp32 rounding (MIOpen may pick different conv solvers for the two calls)."""
+    from lvae_amd.vae import conv_relu_maxpool2
+    import torch.nn.functional as F
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(DEV)
+    x = torch.randn(n, cin, hw, hw, device=DEV, generator=gen)
+    g = None
+    outs = []
+    for fused in (True, False):
+        xr = x.clone().requires_grad_()
+        y = conv_relu_maxpool2(conv, xr) if fused else F.max_pool2d(F.relu(conv(xr)), 2, 2)
+        if g is None:
+            g = torch.randn(y.shape, device=DEV, generator=gen)
+        outs.append([y] + list(torch.autograd.grad(y, [xr, conv.weight, conv.bias], g)))
+    for a, b in zip(*outs):
+        assert float((a - b).abs().max() / b.abs().max()) < 1e-5
+
+
 def _random_hypers(k, L, rng, scale=(0.3, 1.5), ell=(1.0, 4.0)):
     """[L, P] raw parameters: per-dim random scales and lengthscales (named_parameters order)."""
     return np.stack([np.log(rng.uniform(*scale, L)) if "scale" in n else np.log(rng.uniform(*ell, L))
