@@ -224,6 +224,14 @@ int lvae_relu_maxpool2_bias_fwd_f32(const float* x, const float* bias, int N, in
                                     uint8_t* idx, void* stream);
 int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8_t* idx, int N, int C, int H, int W,
                                     float* gx, float* db, void* workspace, void* stream);
+/* The whole backward of the first encoder conv (1 input channel, 3x3, padding 1; its input, the
+ * image, needs no gradient) from the pooled gradient: dw [C, 1, 3, 3] and db [C] as sums over the
+ * pooled outputs of g * (the 3x3 image patch at the window's argmax), no full-resolution gradient
+ * and no conv kernel.  x: the conv input [N, 1, H, W]; y, idx: that layer's forward outputs.
+ * Deterministic (workspace: lvae_conv1_relu_maxpool2_wgrad_workspace_size bytes).              */
+size_t lvae_conv1_relu_maxpool2_wgrad_workspace_size(int N, int C);
+int lvae_conv1_relu_maxpool2_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N,
+                                       int C, int H, int W, float* dw, float* db, void* workspace, void* stream);
 
 /* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
  * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject

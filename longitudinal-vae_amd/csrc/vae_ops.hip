@@ -138,6 +138,76 @@ __global__ __launch_bounds__(256) void bias_partial_sum_kernel(const float* __re
 
 constexpr int kPoolBiasPer = 16;  // images per backward block (x C channels in the grid)
 
+// The first encoder conv (1 input channel, 3 x 3, padding 1) needs no input gradient, so its whole
+// backward reduces to dW[c][ky][kx] = sum g * x[r + ky - 1][s + kx - 1] and db[c] = sum g over the
+// pooled outputs, (r, s) = the argmax position of each window (the only nonzero of the routed
+// gradient): the full-resolution gradient is never written and no conv kernel runs.  Grid (nb, C);
+// partials part[c][bx][10] (9 taps + bias), reduced in a fixed order by conv1_wgrad_sum_kernel.
+__global__ __launch_bounds__(256) void relu_maxpool2_conv1_wgrad_kernel(const float* __restrict__ gy,
+                                                                        const float* __restrict__ y,
+                                                                        const uint8_t* __restrict__ idx,
+                                                                        const float* __restrict__ x, int N, int C,
+                                                                        int Ho, int Wo, int per,
+                                                                        float* __restrict__ part) {
+  __shared__ float red[10][256];
+  const int c = blockIdx.y, n0 = blockIdx.x * per, n1 = min(N, n0 + per);
+  const int P = Ho * Wo, H = 2 * Ho, W = 2 * Wo;
+  const int total = (n1 - n0) * P;
+  float acc[10];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) acc[q] = 0.f;
+  for (int t = threadIdx.x; t < total; t += 256) {
+    const int n = n0 + t / P, r = t % P, i = r / Wo, j = r % Wo;
+    const int64_t e = ((int64_t)n * C + c) * P + r;
+    const float g = y[e] > 0.f ? gy[e] : 0.f;
+    acc[9] += g;
+    const int k = idx[e], rr = 2 * i + (k >> 1), ss = 2 * j + (k & 1);
+    const float* xp = x + (int64_t)n * H * W;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int yy = rr + ky - 1, xx = ss + kx - 1;
+        const float v = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? xp[yy * W + xx] : 0.f;
+        acc[3 * ky + kx] += g * v;
+      }
+  }
+#pragma unroll
+  for (int q = 0; q < 10; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+#pragma unroll
+      for (int q = 0; q < 10; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 10) part[((int64_t)c * gridDim.x + blockIdx.x) * 10 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// dw[c][q] = sum_b part[c][b][q] (q < 9), db[c] = sum_b part[c][b][9]; one block per channel
+__global__ __launch_bounds__(256) void conv1_wgrad_sum_kernel(const float* __restrict__ part, int nb,
+                                                              float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[10][256];
+  const int c = blockIdx.x;
+  float s[10];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) s[q] = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 256)
+#pragma unroll
+    for (int q = 0; q < 10; ++q) s[q] += part[((int64_t)c * nb + b) * 10 + q];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) red[q][threadIdx.x] = s[q];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+#pragma unroll
+      for (int q = 0; q < 10; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 9) dw[c * 9 + threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x == 9) db[c] = red[9][0];
+}
+
 }  // namespace lvae
 
 using namespace lvae;
@@ -180,6 +250,29 @@ int lvae_relu_maxpool2_bias_fwd_f32(const float* x, const float* bias, int N, in
   if (total == 0) return 0;
   relu_maxpool2_bias_fwd_kernel<<<cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(x, bias, C, total, Ho, Wo, y,
                                                                                     idx);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t lvae_conv1_relu_maxpool2_wgrad_workspace_size(int N, int C) {
+  return N <= 0 || C <= 0 ? 0 : sizeof(float) * 10 * (size_t)C * (size_t)cdiv(N, kPoolBiasPer);
+}
+
+int lvae_conv1_relu_maxpool2_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N,
+                                       int C, int H, int W, float* dw, float* db, void* workspace, void* stream) {
+  if (!gy || !y || !idx || !x || !dw || !db || !workspace) return -1;
+  if (N < 0 || C <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) {
+    (void)hipMemsetAsync(dw, 0, sizeof(float) * 9 * C, st);
+    (void)hipMemsetAsync(db, 0, sizeof(float) * C, st);
+    return 0;
+  }
+  const int nb = (int)cdiv(N, kPoolBiasPer);
+  float* part = (float*)workspace;
+  relu_maxpool2_conv1_wgrad_kernel<<<dim3(nb, C), 256, 0, st>>>(gy, y, idx, x, N, C, H / 2, W / 2, kPoolBiasPer,
+                                                                 part);
+  conv1_wgrad_sum_kernel<<<C, 256, 0, st>>>(part, nb, dw, db);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -71,6 +71,17 @@ class _ConvReluMaxPool2(torch.autograd.Function):
         x, weight, y, idx = ctx.saved_tensors
         N, C, H, W = ctx.shape
         gy = gy.contiguous()
+        if not ctx.needs_input_grad[0] and x.shape[1] == 1:
+            # first conv: weight and bias gradients straight from the pooled gradient
+            dw = torch.empty(C, 1, 3, 3, dtype=gy.dtype, device=gy.device)
+            db = torch.empty(C, dtype=gy.dtype, device=gy.device)
+            ws = torch.empty(lib.lvae_conv1_relu_maxpool2_wgrad_workspace_size(N, C) // 4 + 1, dtype=torch.float32,
+                             device=gy.device)
+            xc = x.contiguous()
+            _lib.check(lib.lvae_conv1_relu_maxpool2_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N,
+                                                               C, H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                                               _lib.stream_ptr()), "conv1_relu_maxpool2_wgrad")
+            return (None, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None)
         g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
         db = torch.empty(C, dtype=gy.dtype, device=gy.device)
         ws = torch.empty(lib.lvae_relu_maxpool2_bias_workspace_size(N, C) // 4 + 1, dtype=torch.float32,
@@ -89,7 +100,8 @@ class _ConvReluMaxPool2(torch.autograd.Function):
 def conv_relu_maxpool2(conv, x):
     """pool(relu(conv(x))) for the encoder's 3x3 / padding-1 convs: fused bias path for CUDA fp32."""
     if (x.is_cuda and x.dtype == torch.float32 and conv.bias is not None and conv.weight.dtype == torch.float32
-            and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0):
+            and tuple(conv.kernel_size) == (3, 3) and tuple(conv.padding) == (1, 1) and tuple(conv.stride) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and conv.groups == 1 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0):
         return _ConvReluMaxPool2.apply(x, conv.weight, conv.bias)
     return relu_maxpool2(conv(x))
 

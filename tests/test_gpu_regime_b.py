@@ -274,11 +274,13 @@ def test_relu_maxpool2_bias_kernels_match_torch(hip, n, c, hw):
     assert float((db - br.grad).abs().max() / br.grad.abs().max()) < 1e-5
 
 
-@pytest.mark.parametrize("n,cin,cout,hw", [(5, 1, 16, 36), (37, 16, 32, 18)])
-def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw):
+@pytest.mark.parametrize("n,cin,cout,hw,xgrad", [(5, 1, 16, 36, True), (37, 16, 32, 18, True), (37, 1, 16, 36, False),
+                                               (3, 1, 4, 8, False)])
+def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw, xgrad):
     """Encoder conv with its bias folded into the fused relu + pool pass (bias gradient from its
-    backward, weight / input gradients from aten.convolution_backward) vs nn.Conv2d -> relu ->
-    max_pool2d, to fp32 rounding (MIOpen may pick different conv solvers for the two calls)."""
+    backward, weight / input gradients from aten.convolution_backward; for the first conv, whose
+    input needs no gradient, weight and bias gradients straight from the pooled gradient) vs
+    nn.Conv2d -> relu -> max_pool2d, to fp32 rounding (MIOpen may pick different conv solvers)."""
     from lvae_amd.vae import conv_relu_maxpool2
     import torch.nn.functional as F
     gen = torch.Generator(device=DEV).manual_seed(1)
@@ -287,11 +289,12 @@ def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw):
     g = None
     outs = []
     for fused in (True, False):
-        xr = x.clone().requires_grad_()
+        xr = x.clone().requires_grad_(xgrad)
         y = conv_relu_maxpool2(conv, xr) if fused else F.max_pool2d(F.relu(conv(xr)), 2, 2)
         if g is None:
             g = torch.randn(y.shape, device=DEV, generator=gen)
-        outs.append([y] + list(torch.autograd.grad(y, [xr, conv.weight, conv.bias], g)))
+        wrt = ([xr] if xgrad else []) + [conv.weight, conv.bias]
+        outs.append([y] + list(torch.autograd.grad(y, wrt, g)))
     for a, b in zip(*outs):
         assert float((a - b).abs().max() / b.abs().max()) < 1e-5
 
