@@ -138,74 +138,173 @@ __global__ __launch_bounds__(256) void bias_partial_sum_kernel(const float* __re
 
 constexpr int kPoolBiasPer = 16;  // images per backward block (x C channels in the grid)
 
-// The first encoder conv (1 input channel, 3 x 3, padding 1) needs no input gradient, so its whole
-// backward reduces to dW[c][ky][kx] = sum g * x[r + ky - 1][s + kx - 1] and db[c] = sum g over the
-// pooled outputs, (r, s) = the argmax position of each window (the only nonzero of the routed
-// gradient): the full-resolution gradient is never written and no conv kernel runs.  Grid (nb, C);
-// partials part[c][bx][10] (9 taps + bias), reduced in a fixed order by conv1_wgrad_sum_kernel.
-__global__ __launch_bounds__(256) void relu_maxpool2_conv1_wgrad_kernel(const float* __restrict__ gy,
-                                                                        const float* __restrict__ y,
-                                                                        const uint8_t* __restrict__ idx,
-                                                                        const float* __restrict__ x, int N, int C,
-                                                                        int Ho, int Wo, int per,
-                                                                        float* __restrict__ part) {
-  __shared__ float red[10][256];
-  const int c = blockIdx.y, n0 = blockIdx.x * per, n1 = min(N, n0 + per);
+// The first encoder conv end to end: 1 input channel, 3 x 3, padding 1, bias, relu, 2x2 pool, one
+// thread per pooled position (n, i, j) for all C channels.  The 4 x 4 input patch under the window
+// is loaded once; per channel the 2 x 2 conv outputs are sum_ky sum_kx p w (this order) + b, then
+// relu + first-strict-max as in relu_maxpool2_bias_fwd_kernel.  The full-resolution conv output
+// (16 x the image bytes) is never written; MIOpen's Winograd conv for this shape took ~270 us.
+__global__ __launch_bounds__(256) void conv1_relu_maxpool2_fwd_kernel(const float* __restrict__ x,
+                                                                      const float* __restrict__ w,
+                                                                      const float* __restrict__ bias, int N, int C,
+                                                                      int Ho, int Wo, float* __restrict__ y,
+                                                                      uint8_t* __restrict__ idx) {
   const int P = Ho * Wo, H = 2 * Ho, W = 2 * Wo;
-  const int total = (n1 - n0) * P;
-  float acc[10];
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)N * P) return;
+  const int n = (int)(e / P), r = (int)(e % P), i = r / Wo, j = r % Wo;
+  const float* xn = x + (int64_t)n * H * W;
+  float p[4][4];
 #pragma unroll
-  for (int q = 0; q < 10; ++q) acc[q] = 0.f;
-  for (int t = threadIdx.x; t < total; t += 256) {
-    const int n = n0 + t / P, r = t % P, i = r / Wo, j = r % Wo;
-    const int64_t e = ((int64_t)n * C + c) * P + r;
-    const float g = y[e] > 0.f ? gy[e] : 0.f;
-    acc[9] += g;
-    const int k = idx[e], rr = 2 * i + (k >> 1), ss = 2 * j + (k & 1);
-    const float* xp = x + (int64_t)n * H * W;
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int b = 0; b < 4; ++b) {
+      const int yy = 2 * i - 1 + a, xx = 2 * j - 1 + b;
+      p[a][b] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? xn[yy * W + xx] : 0.f;
+    }
+  for (int c = 0; c < C; ++c) {
+    const float* wc = w + 9 * c;
+    const float bc = bias[c];
+    float v[4];
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int yy = rr + ky - 1, xx = ss + kx - 1;
-        const float v = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? xp[yy * W + xx] : 0.f;
-        acc[3 * ky + kx] += g * v;
-      }
+    for (int d = 0; d < 4; ++d) {
+      const int dy = d >> 1, dx = d & 1;
+      float s = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) s = fmaf(p[dy + ky][dx + kx], wc[3 * ky + kx], s);
+      v[d] = s + bc;
+    }
+    float m = v[0];
+    uint8_t k = 0;
+    if (v[1] > m) m = v[1], k = 1;
+    if (v[2] > m) m = v[2], k = 2;
+    if (v[3] > m) m = v[3], k = 3;
+    const int64_t o = ((int64_t)n * C + c) * P + r;
+    y[o] = m > 0.f ? m : 0.f;
+    idx[o] = k;
   }
+}
+constexpr int kWgradPer = 4;      // images per conv3x3_pool_wgrad block
+
+// Weight and bias gradients of a 3 x 3 / stride-1 / padding-1 conv followed by the fused relu + 2x2
+// pool, straight from the pooled gradient: the routed full-resolution gradient has one nonzero per
+// window (at its argmax), so dW[co][ci][ky][kx] = sum g * x[ci][r + ky - 1][s + kx - 1] and
+// db[co] = sum g over the pooled outputs (r, s = the argmax position).  No full-resolution gradient
+// for the weights and no weight-gradient conv (MIOpen's needs two NCHW <-> NHWC transposes).
+// One block per `per` images; per image the Cin input planes (zero border) and the routed gradient
+// g and argmax offset of all C channels are staged in LDS, then thread t owns the (co, ci) pairs
+// t % Q + 256 p... (Q = C Cin pairs; with Q < 256 the S = 256 / Q threads of a pair split its
+// positions and are summed in LDS at the end).  Block partials part[bx][m], m = C Cin 9 + C,
+// summed over blocks in a fixed order by wgrad_sum_kernel: deterministic.
+template <int NP>
+__global__ __launch_bounds__(256) void conv3x3_pool_wgrad_kernel(const float* __restrict__ gy,
+                                                                 const float* __restrict__ y,
+                                                                 const uint8_t* __restrict__ idx,
+                                                                 const float* __restrict__ x, int N, int C, int Cin,
+                                                                 int Ho, int Wo, int per, float* __restrict__ part) {
+  extern __shared__ float sm[];
+  // channel stride of the staged input: odd, so the 16+ ci lanes reading one offset hit distinct banks
+  const int H = 2 * Ho, W = 2 * Wo, Hp = H + 2, Wp = W + 2, P = Ho * Wo, HWp = (Hp * Wp) | 1;
+  const int Q = C * Cin, S = Q >= 256 ? 1 : 256 / Q;
+  float* zl = sm;                                   // [Cin][HWp]
+  float* gl = zl + Cin * HWp;                       // [C][P]
+  int* ol = reinterpret_cast<int*>(gl + C * P);     // [C][P] padded offset of the argmax
+  const int t = threadIdx.x, split = Q >= 256 ? 0 : t / Q;
+  const bool active = Q >= 256 || t < Q * S;
+  const int n0 = blockIdx.x * per, n1 = min(N, n0 + per);
+  for (int e = t; e < Cin * HWp; e += 256) zl[e] = 0.f;
+  float acc[NP][9], bacc[NP];
 #pragma unroll
-  for (int q = 0; q < 10; ++q) red[q][threadIdx.x] = acc[q];
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o)
+  for (int p = 0; p < NP; ++p) {
+    bacc[p] = 0.f;
 #pragma unroll
-      for (int q = 0; q < 10; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    for (int q = 0; q < 9; ++q) acc[p][q] = 0.f;
+  }
+  for (int n = n0; n < n1; ++n) {
+    __syncthreads();  // the previous image's reads are done (and the border is zero)
+    const float* xn = x + (int64_t)n * Cin * H * W;
+#pragma unroll 4
+    for (int e = t; e < Cin * H * W; e += 256) {
+      const int ci = e / (H * W), r = (e / W) % H, c = e % W;
+      zl[ci * HWp + (r + 1) * Wp + c + 1] = xn[e];
+    }
+    const int64_t b0 = (int64_t)n * C * P;
+#pragma unroll 4
+    for (int e = t; e < C * P; e += 256) {  // unconditional loads: no load waits on another
+      const float yv = y[b0 + e], gv = gy[b0 + e];
+      const int k = idx[b0 + e], r = e % P, i = r / Wo, j = r % Wo;
+      gl[e] = yv > 0.f ? gv : 0.f;
+      ol[e] = (2 * i + (k >> 1)) * Wp + 2 * j + (k & 1);  // padded coords of tap (0, 0)
+    }
     __syncthreads();
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int pr = (Q >= 256 ? t : t % Q) + 256 * p;
+      if (active && pr < Q) {
+        const int co = pr / Cin, ci = pr % Cin;
+        const float* zc = zl + ci * HWp;
+        for (int r = split; r < P; r += S) {
+          const float g = gl[co * P + r];
+          if (g == 0.f) continue;
+          const float* z0 = zc + ol[co * P + r];
+          bacc[p] += g;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) acc[p][3 * ky + kx] += g * z0[ky * Wp + kx];
+        }
+      }
+    }
   }
-  if (threadIdx.x < 10) part[((int64_t)c * gridDim.x + blockIdx.x) * 10 + threadIdx.x] = red[threadIdx.x][0];
+  // sum the S position splits of each pair in LDS (reusing the staging area), then write partials
+  __syncthreads();
+  const int m = Q * 9 + C;
+  float* pb = part + (int64_t)blockIdx.x * m;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (S > 1) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) sm[q * 256 + t] = acc[p][q];
+      sm[9 * 256 + t] = bacc[p];
+      __syncthreads();
+      if (t < Q) {
+        for (int sp = 1; sp < S; ++sp) {
+#pragma unroll
+          for (int q = 0; q < 9; ++q) acc[p][q] += sm[q * 256 + sp * Q + t];
+          bacc[p] += sm[9 * 256 + sp * Q + t];
+        }
+      }
+      __syncthreads();
+    }
+    const int pr = t + 256 * p;
+    if (t < Q && pr < Q) {
+      const int co = pr / Cin, ci = pr % Cin;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) pb[pr * 9 + q] = acc[p][q];
+      if (ci == 0) pb[Q * 9 + co] = bacc[p];
+    }
+  }
 }
 
-// dw[c][q] = sum_b part[c][b][q] (q < 9), db[c] = sum_b part[c][b][9]; one block per channel
-__global__ __launch_bounds__(256) void conv1_wgrad_sum_kernel(const float* __restrict__ part, int nb,
-                                                              float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[10][256];
-  const int c = blockIdx.x;
-  float s[10];
-#pragma unroll
-  for (int q = 0; q < 10; ++q) s[q] = 0.f;
-  for (int b = threadIdx.x; b < nb; b += 256)
-#pragma unroll
-    for (int q = 0; q < 10; ++q) s[q] += part[((int64_t)c * nb + b) * 10 + q];
-#pragma unroll
-  for (int q = 0; q < 10; ++q) red[q][threadIdx.x] = s[q];
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o)
-#pragma unroll
-      for (int q = 0; q < 10; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
-    __syncthreads();
+// out[q] = sum_b part[b][q] (fixed order): 64 columns x 4 row slices per block, slices summed in LDS;
+// q < nw -> dw[q], else db[q - nw]
+__global__ __launch_bounds__(256) void wgrad_sum_kernel(const float* __restrict__ part, int nb, int m, int nw,
+                                                        float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6, q = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (q < m) {
+#pragma unroll 8
+    for (int b = sl; b < nb; b += 4) s += part[(int64_t)b * m + q];
   }
-  if (threadIdx.x < 9) dw[c * 9 + threadIdx.x] = red[threadIdx.x][0];
-  if (threadIdx.x == 9) db[c] = red[9][0];
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && q < m) {
+    const float v = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    if (q < nw) dw[q] = v;
+    else db[q - nw] = v;
+  }
 }
 
 }  // namespace lvae
@@ -237,6 +336,18 @@ int lvae_relu_maxpool2_bwd_f32(const float* gy, const float* y, const uint8_t* i
   return 0;
 }
 
+int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float* bias, int N, int C, int H, int W,
+                                     float* y, uint8_t* idx, void* stream) {
+  if (!x || !w || !bias || !y || !idx) return -1;
+  if (N < 0 || C <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return -2;
+  const int64_t total = (int64_t)N * (H / 2) * (W / 2);
+  if (total == 0) return 0;
+  conv1_relu_maxpool2_fwd_kernel<<<cdiv(total, 256), 256, 0, (hipStream_t)stream>>>(x, w, bias, N, C, H / 2, W / 2, y,
+                                                                                     idx);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
 size_t lvae_relu_maxpool2_bias_workspace_size(int N, int C) {
   return N <= 0 || C <= 0 ? 0 : sizeof(float) * (size_t)C * (size_t)cdiv(N, kPoolBiasPer);
 }
@@ -254,25 +365,39 @@ int lvae_relu_maxpool2_bias_fwd_f32(const float* x, const float* bias, int N, in
   return 0;
 }
 
-size_t lvae_conv1_relu_maxpool2_wgrad_workspace_size(int N, int C) {
-  return N <= 0 || C <= 0 ? 0 : sizeof(float) * 10 * (size_t)C * (size_t)cdiv(N, kPoolBiasPer);
+static size_t conv3x3_pool_wgrad_lds(int C, int Cin, int H, int W) {
+  const size_t stage = (size_t)Cin * (((H + 2) * (W + 2)) | 1) + 2 * (size_t)C * (H / 2) * (W / 2);
+  return sizeof(float) * (stage > 2560 ? stage : 2560);
 }
 
-int lvae_conv1_relu_maxpool2_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N,
-                                       int C, int H, int W, float* dw, float* db, void* workspace, void* stream) {
+size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin) {
+  return N <= 0 || C <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)C * Cin * 9 + C) * (size_t)cdiv(N, kWgradPer);
+}
+
+int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
+                                int Cin, int H, int W, float* dw, float* db, void* workspace, void* stream) {
   if (!gy || !y || !idx || !x || !dw || !db || !workspace) return -1;
-  if (N < 0 || C <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return -2;
+  if (N < 0 || C <= 0 || Cin <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return -2;
+  const int Q = C * Cin, NP = (Q + 255) / 256;
+  if (NP > 4) return -3;
+  const size_t lds = conv3x3_pool_wgrad_lds(C, Cin, H, W);
+  if (lds > 64 * 1024) return -4;
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) {
-    (void)hipMemsetAsync(dw, 0, sizeof(float) * 9 * C, st);
+    (void)hipMemsetAsync(dw, 0, sizeof(float) * Q * 9, st);
     (void)hipMemsetAsync(db, 0, sizeof(float) * C, st);
     return 0;
   }
-  const int nb = (int)cdiv(N, kPoolBiasPer);
+  const int nb = (int)cdiv(N, kWgradPer), m = Q * 9 + C;
   float* part = (float*)workspace;
-  relu_maxpool2_conv1_wgrad_kernel<<<dim3(nb, C), 256, 0, st>>>(gy, y, idx, x, N, C, H / 2, W / 2, kPoolBiasPer,
-                                                                 part);
-  conv1_wgrad_sum_kernel<<<C, 256, 0, st>>>(part, nb, dw, db);
+  const int Ho = H / 2, Wo = W / 2;
+  switch (NP) {
+    case 1: conv3x3_pool_wgrad_kernel<1><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
+    case 2: conv3x3_pool_wgrad_kernel<2><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
+    case 3: conv3x3_pool_wgrad_kernel<3><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
+    default: conv3x3_pool_wgrad_kernel<4><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
+  }
+  wgrad_sum_kernel<<<cdiv(m, 64), 256, 0, st>>>(part, nb, m, Q * 9, dw, db);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

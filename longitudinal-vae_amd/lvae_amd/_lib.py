@@ -101,10 +101,11 @@ SIGNATURES = {
     "lvae_relu_maxpool2_fwd_f32": (_I32, [_VP, _I64, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _I32, _I32, _VP, _VP]),
     "lvae_relu_maxpool2_bias_workspace_size": (_SZ, [_I32, _I32]),
+    "lvae_conv1_relu_maxpool2_fwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bias_fwd_f32": (_I32, [_VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bias_bwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
-    "lvae_conv1_relu_maxpool2_wgrad_workspace_size": (_SZ, [_I32, _I32]),
-    "lvae_conv1_relu_maxpool2_wgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
+    "lvae_conv3x3_pool_wgrad_workspace_size": (_SZ, [_I32, _I32, _I32]),
+    "lvae_conv3x3_pool_wgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),

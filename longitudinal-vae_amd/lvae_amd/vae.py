@@ -44,22 +44,33 @@ class _ReluMaxPool2(torch.autograd.Function):
 
 
 class _ConvReluMaxPool2(torch.autograd.Function):
-    """max_pool2d(relu(conv2d(x, w, b, padding=1)), 2, 2) (VAE.py:44-50): the 3x3 conv runs without
-    its bias on MIOpen; bias add, relu and pool are one HIP pass (lvae_relu_maxpool2_bias_fwd_f32), and
-    the backward's routing pass also returns the bias gradient (lvae_relu_maxpool2_bias_bwd_f32), so
-    neither the full-resolution bias add nor torch's strided bias-gradient sum runs."""
+    """max_pool2d(relu(conv2d(x, w, b, padding=1)), 2, 2) (VAE.py:44-50).
+    Forward: a 1-channel input (the first conv) is one direct HIP pass (lvae_conv1_relu_maxpool2_fwd_f32);
+    otherwise the conv runs without its bias on MIOpen and bias add, relu and pool are one HIP pass
+    (lvae_relu_maxpool2_bias_fwd_f32).  Backward: weight and bias gradients straight from the pooled
+    gradient (lvae_conv3x3_pool_wgrad_f32); the routed full-resolution gradient is formed only for the
+    input gradient (MIOpen backward-data), which the first conv does not need."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         from . import _lib
         lib = _lib.lib()
-        y0 = F.conv2d(x, weight, None, 1, 1).contiguous()
-        N, C, H, W = y0.shape
         b = bias.contiguous()
-        y = torch.empty(N, C, H // 2, W // 2, dtype=y0.dtype, device=y0.device)
-        idx = torch.empty(N, C, H // 2, W // 2, dtype=torch.uint8, device=y0.device)
-        _lib.check(lib.lvae_relu_maxpool2_bias_fwd_f32(_lib.ptr(y0), _lib.ptr(b), N, C, H, W, _lib.ptr(y),
-                                                        _lib.ptr(idx), _lib.stream_ptr()), "relu_maxpool2_bias_fwd")
+        if x.shape[1] == 1:  # first conv: one direct HIP pass, no full-resolution output
+            xc, wc = x.contiguous(), weight.contiguous()
+            N, C, H, W = x.shape[0], weight.shape[0], x.shape[2], x.shape[3]
+            y = torch.empty(N, C, H // 2, W // 2, dtype=x.dtype, device=x.device)
+            idx = torch.empty(N, C, H // 2, W // 2, dtype=torch.uint8, device=x.device)
+            _lib.check(lib.lvae_conv1_relu_maxpool2_fwd_f32(_lib.ptr(xc), _lib.ptr(wc), _lib.ptr(b), N, C, H, W,
+                                                             _lib.ptr(y), _lib.ptr(idx), _lib.stream_ptr()),
+                       "conv1_relu_maxpool2_fwd")
+        else:
+            y0 = F.conv2d(x, weight, None, 1, 1).contiguous()
+            N, C, H, W = y0.shape
+            y = torch.empty(N, C, H // 2, W // 2, dtype=y0.dtype, device=y0.device)
+            idx = torch.empty(N, C, H // 2, W // 2, dtype=torch.uint8, device=y0.device)
+            _lib.check(lib.lvae_relu_maxpool2_bias_fwd_f32(_lib.ptr(y0), _lib.ptr(b), N, C, H, W, _lib.ptr(y),
+                                                            _lib.ptr(idx), _lib.stream_ptr()), "relu_maxpool2_bias_fwd")
         ctx.save_for_backward(x, weight, y, idx)
         ctx.shape = (N, C, H, W)
         return y
@@ -71,17 +82,27 @@ class _ConvReluMaxPool2(torch.autograd.Function):
         x, weight, y, idx = ctx.saved_tensors
         N, C, H, W = ctx.shape
         gy = gy.contiguous()
-        if not ctx.needs_input_grad[0] and x.shape[1] == 1:
-            # first conv: weight and bias gradients straight from the pooled gradient
-            dw = torch.empty(C, 1, 3, 3, dtype=gy.dtype, device=gy.device)
+        Cin = x.shape[1]
+        if C * Cin <= 1024 and 4 * (Cin * (((H + 2) * (W + 2)) | 1) + 2 * C * (H // 2) * (W // 2)) <= 65536:
+            # weight and bias gradients from the pooled gradient (lvae_conv3x3_pool_wgrad_f32); the routed
+            # full-resolution gradient only feeds the input gradient (MIOpen backward-data), and the
+            # first conv (image input) needs none
+            dw = torch.empty_like(weight)
             db = torch.empty(C, dtype=gy.dtype, device=gy.device)
-            ws = torch.empty(lib.lvae_conv1_relu_maxpool2_wgrad_workspace_size(N, C) // 4 + 1, dtype=torch.float32,
+            ws = torch.empty(lib.lvae_conv3x3_pool_wgrad_workspace_size(N, C, Cin) // 4 + 1, dtype=torch.float32,
                              device=gy.device)
             xc = x.contiguous()
-            _lib.check(lib.lvae_conv1_relu_maxpool2_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N,
-                                                               C, H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
-                                                               _lib.stream_ptr()), "conv1_relu_maxpool2_wgrad")
-            return (None, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None)
+            _lib.check(lib.lvae_conv3x3_pool_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N, C, Cin,
+                                                        H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                                        _lib.stream_ptr()), "conv3x3_pool_wgrad")
+            gx = None
+            if ctx.needs_input_grad[0]:
+                g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
+                _lib.check(lib.lvae_relu_maxpool2_bwd_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), N * C, H, W,
+                                                           _lib.ptr(g0), _lib.stream_ptr()), "relu_maxpool2_bwd")
+                gx = torch.ops.aten.convolution_backward(g0, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0]
+            return gx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None
         g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
         db = torch.empty(C, dtype=gy.dtype, device=gy.device)
         ws = torch.empty(lib.lvae_relu_maxpool2_bias_workspace_size(N, C) // 4 + 1, dtype=torch.float32,
