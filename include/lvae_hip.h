@@ -220,15 +220,15 @@ int lvae_relu_maxpool2_bwd_f32(const float* gy, const float* y, const uint8_t* i
  * db [C] = the conv's bias gradient (deterministic; workspace: lvae_relu_maxpool2_bias_workspace_size
  * bytes).  Replaces nn.Conv2d's bias add and its bias-gradient sum (VAE.py:44-50).             */
 size_t lvae_relu_maxpool2_bias_workspace_size(int N, int C);
+int lvae_relu_maxpool2_bias_fwd_f32(const float* x, const float* bias, int N, int C, int H, int W, float* y,
+                                    uint8_t* idx, void* stream);
+int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8_t* idx, int N, int C, int H, int W,
+                                    float* gx, float* db, void* workspace, void* stream);
 /* The first encoder conv end to end (VAE.py:44-47): x [N, 1, H, W], w [C, 1, 3, 3], bias [C],
  * padding 1 -> y = max_pool2d(relu(conv(x) + bias), 2, 2), idx as above; the full-resolution conv
  * output is never written.                                                                      */
 int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float* bias, int N, int C, int H, int W,
                                      float* y, uint8_t* idx, void* stream);
-int lvae_relu_maxpool2_bias_fwd_f32(const float* x, const float* bias, int N, int C, int H, int W, float* y,
-                                    uint8_t* idx, void* stream);
-int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8_t* idx, int N, int C, int H, int W,
-                                    float* gx, float* db, void* workspace, void* stream);
 /* Weight and bias gradients of a 3x3 / stride-1 / padding-1 conv followed by the fused relu + pool
  * (the encoder convs), from the pooled gradient: dw [C, Cin, 3, 3] and db [C] as sums over the
  * pooled outputs of g * (the 3x3 input patch at the window's argmax) -- the full-resolution
@@ -239,8 +239,6 @@ int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin);
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
                                 int Cin, int H, int W, float* dw, float* db, void* workspace, void* stream);
-int lvae_conv1_relu_maxpool2_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N,
-                                       int C, int H, int W, float* dw, float* db, void* workspace, void* stream);
 
 /* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
  * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject
