@@ -239,6 +239,15 @@ int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin);
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
                                 int Cin, int H, int W, float* dw, float* db, void* workspace, void* stream);
+/* ConvVAE decoder output (VAE.py:73-75): out = sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)
+ * (z) + bias), z [N, Cin, Hi, Wi] (Cin <= 16), w [Cin, 1, 4, 4], bias [1] -> out [N, 1, 2Hi, 2Wi].
+ * Backward from g = dLoss/dout and the saved out: gz [N, Cin, Hi, Wi], dw [Cin, 1, 4, 4], db [1]
+ * (deterministic; workspace: lvae_deconv2_sigmoid_workspace_size bytes).                        */
+size_t lvae_deconv2_sigmoid_workspace_size(int N, int Cin, int Hi, int Wi);
+int lvae_deconv2_sigmoid_fwd_f32(const float* z, const float* w, const float* bias, int N, int Cin, int Hi, int Wi,
+                                 float* out, void* stream);
+int lvae_deconv2_sigmoid_bwd_f32(const float* g, const float* out, const float* z, const float* w, int N, int Cin,
+                                 int Hi, int Wi, float* gz, float* dw, float* db, void* workspace, void* stream);
 
 /* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
  * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject

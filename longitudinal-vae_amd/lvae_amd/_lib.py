@@ -105,6 +105,9 @@ SIGNATURES = {
     "lvae_relu_maxpool2_bias_fwd_f32": (_I32, [_VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     "lvae_relu_maxpool2_bias_bwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_conv3x3_pool_wgrad_workspace_size": (_SZ, [_I32, _I32, _I32]),
+    "lvae_deconv2_sigmoid_workspace_size": (_SZ, [_I32, _I32, _I32, _I32]),
+    "lvae_deconv2_sigmoid_fwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP]),
+    "lvae_deconv2_sigmoid_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
     "lvae_conv3x3_pool_wgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),

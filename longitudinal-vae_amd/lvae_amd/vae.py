@@ -127,6 +127,52 @@ def conv_relu_maxpool2(conv, x):
     return relu_maxpool2(conv(x))
 
 
+class _Deconv2Sigmoid(torch.autograd.Function):
+    """sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)(z)) (VAE.py:73-75) as one direct HIP pass
+    each way (lvae_deconv2_sigmoid_fwd/bwd_f32): the backward forms the pre-sigmoid gradient on the fly
+    and returns the input, weight and bias gradients together (no MIOpen transposed conv, no
+    sigmoid / bias-sum kernels)."""
+
+    @staticmethod
+    def forward(ctx, z, weight, bias):
+        from . import _lib
+        lib = _lib.lib()
+        zc, wc, bc = z.contiguous(), weight.contiguous(), bias.contiguous()
+        N, Cin, Hi, Wi = zc.shape
+        out = torch.empty(N, 1, 2 * Hi, 2 * Wi, dtype=z.dtype, device=z.device)
+        _lib.check(lib.lvae_deconv2_sigmoid_fwd_f32(_lib.ptr(zc), _lib.ptr(wc), _lib.ptr(bc), N, Cin, Hi, Wi,
+                                                     _lib.ptr(out), _lib.stream_ptr()), "deconv2_sigmoid_fwd")
+        ctx.save_for_backward(zc, wc, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        lib = _lib.lib()
+        z, w, out = ctx.saved_tensors
+        N, Cin, Hi, Wi = z.shape
+        g = g.contiguous()
+        gz = torch.empty_like(z)
+        dw = torch.empty_like(w)
+        db = torch.empty(1, dtype=z.dtype, device=z.device)
+        ws = torch.empty(lib.lvae_deconv2_sigmoid_workspace_size(N, Cin, Hi, Wi) // 4 + 1, dtype=torch.float32,
+                         device=z.device)
+        _lib.check(lib.lvae_deconv2_sigmoid_bwd_f32(_lib.ptr(g), _lib.ptr(out), _lib.ptr(z), _lib.ptr(w), N, Cin, Hi,
+                                                     Wi, _lib.ptr(gz), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                                     _lib.stream_ptr()), "deconv2_sigmoid_bwd")
+        return gz, dw, db
+
+
+def deconv_sigmoid(deconv, z):
+    """sigmoid(deconv(z)) for the decoder's last layer: fused HIP path for CUDA fp32."""
+    if (z.is_cuda and z.dtype == torch.float32 and deconv.weight.dtype == torch.float32 and deconv.bias is not None
+            and deconv.out_channels == 1 and deconv.in_channels <= 16 and tuple(deconv.kernel_size) == (4, 4)
+            and tuple(deconv.stride) == (2, 2) and tuple(deconv.padding) == (1, 1)
+            and tuple(deconv.output_padding) == (0, 0) and tuple(deconv.dilation) == (1, 1) and deconv.groups == 1):
+        return _Deconv2Sigmoid.apply(z, deconv.weight, deconv.bias)
+    return torch.sigmoid(deconv(z))
+
+
 def relu_maxpool2(x):
     """pool(relu(x)) of the encoder (VAE.py:44-50): fused HIP kernel for CUDA fp32 activations."""
     if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0:
@@ -187,7 +233,7 @@ class ConvVAE(nn.Module):
         x = F.relu(self.fc4(x))
         x = self.dropout2d_3(x.reshape(-1, 32, 9, 9))
         x = self.dropout2d_4(F.relu(self.deconv1(x)))
-        return torch.sigmoid(self.deconv2(x))
+        return deconv_sigmoid(self.deconv2, x)
 
     def sample_latent(self, mu, log_var, eps=None):
         std = torch.exp(0.5 * log_var)

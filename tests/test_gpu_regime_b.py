@@ -299,6 +299,29 @@ def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw, xgrad):
         assert float((a - b).abs().max() / b.abs().max()) < 1e-5
 
 
+@pytest.mark.parametrize("n,cin,hw", [(5, 16, 18), (37, 16, 18), (3, 5, 7)])
+def test_deconv_sigmoid_matches_torch(hip, n, cin, hw):
+    """Decoder output layer sigmoid(ConvTranspose2d(cin, 1, 4, 2, 1)(z)) as one HIP pass each way vs
+    torch (MIOpen transposed conv + sigmoid): output and all three gradients to fp32 rounding."""
+    from lvae_amd.vae import deconv_sigmoid
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    dc = torch.nn.ConvTranspose2d(cin, 1, 4, 2, 1).to(DEV)
+    z = torch.randn(n, cin, hw, hw, device=DEV, generator=gen)
+    g = None
+    outs = []
+    for fused in (True, False):
+        zr = z.clone().requires_grad_()
+        y = deconv_sigmoid(dc, zr) if fused else torch.sigmoid(dc(zr))
+        if g is None:
+            g = torch.randn(y.shape, device=DEV, generator=gen)
+        outs.append([y] + list(torch.autograd.grad(y, [zr, dc.weight, dc.bias], g)))
+    assert outs[0][0].shape == (n, 1, 2 * hw, 2 * hw)
+    # output and input gradient: a few fp32 roundings; weight / bias gradients: sums over n (2hw)^2
+    # terms of both signs in a different order than MIOpen's -> 1e-4 of their max
+    for a, b, tol in zip(*outs, (1e-5, 1e-5, 1e-4, 1e-4)):
+        assert float((a - b).abs().max() / b.abs().max()) < tol
+
+
 def _random_hypers(k, L, rng, scale=(0.3, 1.5), ell=(1.0, 4.0)):
     """[L, P] raw parameters: per-dim random scales and lengthscales (named_parameters order)."""
     return np.stack([np.log(rng.uniform(*scale, L)) if "scale" in n else np.log(rng.uniform(*ell, L))
