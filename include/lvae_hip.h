@@ -239,7 +239,7 @@ int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin);
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
                                 int Cin, int H, int W, float* dw, float* db, void* workspace, void* stream);
-/* ConvVAE decoder output (VAE.py:73-75): out = sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)
+/* ConvVAE decoder output (VAE.py:75, 124): out = sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)
  * (z) + bias), z [N, Cin, Hi, Wi] (Cin <= 16), w [Cin, 1, 4, 4], bias [1] -> out [N, 1, 2Hi, 2Wi].
  * Backward from g = dLoss/dout and the saved out: gz [N, Cin, Hi, Wi], dw [Cin, 1, 4, 4], db [1]
  * (deterministic; workspace: lvae_deconv2_sigmoid_workspace_size bytes).                        */

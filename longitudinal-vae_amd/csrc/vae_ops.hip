@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void bias_partial_sum_kernel(const float* __re
 
 constexpr int kPoolBiasPer = 16;  // images per backward block (x C channels in the grid)
 
-// ---- the decoder's last layer (VAE.py:73-75): recon = sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2,
+// ---- the decoder's last layer (VAE.py:75, 124): recon = sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2,
 // padding 1)(z) + b), z [N, Cin, Hi, Wi] -> [N, 1, 2 Hi, 2 Wi].  Output (oy, ox) takes input rows
 // iy = (oy + 1 - ky) / 2 for the two ky of parity (oy + 1) & 1 (same for columns): 4 taps per input
 // channel.  MIOpen's transposed conv for this shape took ~230 us forward and ~250 us backward.

@@ -128,7 +128,7 @@ def conv_relu_maxpool2(conv, x):
 
 
 class _Deconv2Sigmoid(torch.autograd.Function):
-    """sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)(z)) (VAE.py:73-75) as one direct HIP pass
+    """sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)(z)) (VAE.py:75, 124) as one direct HIP pass
     each way (lvae_deconv2_sigmoid_fwd/bwd_f32): the backward forms the pre-sigmoid gradient on the fly
     and returns the input, weight and bias gradients together (no MIOpen transposed conv, no
     sigmoid / bias-sum kernels)."""
