@@ -99,9 +99,27 @@ class LatentShardedClosedStep:
         from .kernels import kernel_spec_and_params
         W, r = self.world, self.rank
         self.opt.zero_grad(set_to_none=False)
-        recon, mu, log_var = self.vae(img, eps)
-        mse, nll = self.vae.loss_function(recon, img, mask)
-        recon_loss, nll_loss = mse.sum(), nll.sum()
+        mu, log_var = self.vae.encode(img)
+        z = self.vae.sample_latent(mu, log_var, eps)
+        side = None
+        if img.is_cuda:
+            # decoder + recon loss + their backward (decoder / likelihood-scale gradients and dLoss/dz)
+            # on a second stream, beside the all-gather, the KL and the (mu, logvar) all-reduce below
+            mainst = torch.cuda.current_stream(img.device)
+            side = getattr(self, "_dec_stream", None)
+            if side is None or side.device != img.device:
+                side = self._dec_stream = torch.cuda.Stream(device=img.device)
+            z_d = z.detach().requires_grad_()
+            side.wait_stream(mainst)
+            with torch.cuda.stream(side):
+                recon = self.vae.decode(z_d)
+                mse, nll = self.vae.loss_function(recon, img, mask)
+                recon_loss, nll_loss = mse.sum(), nll.sum()
+                (recon_loss if self.loss_function == "mse" else nll_loss).backward()
+        else:
+            recon = self.vae.decode(z)
+            mse, nll = self.vae.loss_function(recon, img, mask)
+            recon_loss, nll_loss = mse.sum(), nll.sum()
         n_loc, L = mu.shape
         N = X.shape[0]
         if n_loc * W != N:
@@ -132,8 +150,15 @@ class LatentShardedClosedStep:
         # every rank's rows of d loss / d(mu, logvar): one SUM all-reduce (one contributor per entry)
         dist.all_reduce(gmv, op=dist.ReduceOp.SUM, group=self.group)
         g_loc = gmv[r * n_loc:(r + 1) * n_loc]
-        main = recon_loss if self.loss_function == "mse" else nll_loss
-        (main + (mu * g_loc[:, :L]).sum() + (log_var * g_loc[:, L:]).sum()).backward()
+        if side is not None:
+            mainst.wait_stream(side)
+            gz = z_d.grad
+            for t in (recon_loss, nll_loss, gz):
+                t.record_stream(mainst)
+            ((z * gz).sum() + (mu * g_loc[:, :L]).sum() + (log_var * g_loc[:, L:]).sum()).backward()
+        else:
+            main = recon_loss if self.loss_function == "mse" else nll_loss
+            (main + (mu * g_loc[:, :L]).sum() + (log_var * g_loc[:, L:]).sum()).backward()
         # network gradients (sum over image shards) + kernel / likelihood gradients (owner rows only)
         GradAllReduce(self.params, W, self.group, average=False)()
         self.opt.step()

@@ -23,13 +23,37 @@ class ClosedStep:
         self.weight, self.loss_function, self.constrain_scales = weight, loss_function, constrain_scales
         self.grad_hook = grad_hook  # e.g. the data-parallel all-reduce
 
+    def _decoder_stream(self, device):
+        s = getattr(self, "_dec_stream", None)
+        if s is None or s.device != device:
+            s = self._dec_stream = torch.cuda.Stream(device=device)
+        return s
+
     def forward_backward(self, img, mask, X, eps=None):
         self.opt.zero_grad(set_to_none=True)
-        recon, mu, log_var = self.vae(img, eps)
-        mse, nll = self.vae.loss_function(recon, img, mask)
-        recon_loss, nll_loss = mse.sum(), nll.sum()
+        if img.is_cuda:
+            # The decoder and the recon loss depend on the encoder only, not on the KL: they run on
+            # a second stream beside the KL forward (Gram + sweep), and autograd runs their backward
+            # on that stream beside the KL backward (S GEMM + Gram adjoint), joining at the encoder.
+            main = torch.cuda.current_stream(img.device)
+            side = self._decoder_stream(img.device)
+            mu, log_var = self.vae.encode(img)
+            z = self.vae.sample_latent(mu, log_var, eps)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                recon = self.vae.decode(z)
+                mse, nll = self.vae.loss_function(recon, img, mask)
+                recon_loss, nll_loss = mse.sum(), nll.sum()
+            kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var)
+            main.wait_stream(side)
+            recon_loss.record_stream(main)
+            nll_loss.record_stream(main)
+        else:
+            recon, mu, log_var = self.vae(img, eps)
+            mse, nll = self.vae.loss_function(recon, img, mask)
+            recon_loss, nll_loss = mse.sum(), nll.sum()
+            kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var)
         L = mu.shape[1]
-        kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var)
         if self.loss_function == "mse":
             gp = kl.sum() / L
             net = recon_loss + self.weight * gp

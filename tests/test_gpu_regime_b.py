@@ -553,6 +553,51 @@ def test_closed_step_vs_oracle(hip):
             assert rel(p.grad, q.grad) < 1e-3, name
 
 
+def test_latent_sharded_closed_step_cuda_path(hip):
+    """LatentShardedClosedStep's CUDA path (decoder + recon backward on a second stream beside the
+    all-gather / KL / all-reduce, dLoss/dz joined into the encoder backward) in a world-1 gloo group
+    on the GPU, against the oracle's whole-batch step: loss terms and every gradient."""
+    import socket
+    import torch.distributed as dist
+    import lvae_amd as la
+    from lvae_amd.distributed import LatentShardedClosedStep
+    from lvae_amd.vae import ConvVAE
+    from lvae_amd.data import health_mnist_batch
+    L, P, T = 4, 32, 16
+    img, mask, X = health_mnist_batch(P, T, seed=9, dtype=torch.float64)
+    ref_vae = O.ConvVAE(L).double()
+    ref_vae.load_state_dict(O.vae_weights(ref_vae, 22))
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).double()
+    vae.load_state_dict(ref_vae.state_dict())
+    vae = vae.float().to(DEV)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    set_raw(k, _random_hypers(k, L, np.random.default_rng(9)))
+    raw = torch.stack([p.detach().clone() for _, p in k.named_parameters()], 1).requires_grad_()
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    eps = torch.randn(P * T, L, generator=torch.Generator().manual_seed(2), dtype=torch.float64)
+    loss, recon, gp = O.closed_step(ref_vae, O.spec_full(**CFG), raw, torch.ones(L, dtype=torch.float64), img, mask,
+                                    X, eps, 0.15)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        opt = torch.optim.SGD(list(vae.parameters()) + list(kd.parameters()), lr=0.0)
+        step = LatentShardedClosedStep(vae, kd, lik, opt, weight=0.15, loss_function="mse")
+        net, rl, _, g = step(img.float().to(DEV), mask.float().to(DEV), X.to(DEV), eps.float().to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert rel(net, loss) < 1e-4
+    assert rel(rl, recon) < 1e-4
+    assert rel(g, gp) < 1e-4
+    assert rel(torch.stack([p.grad for _, p in kd.named_parameters()], 1), raw.grad) < 1e-4
+    for (name, p), (_, q) in zip(vae.named_parameters(), ref_vae.named_parameters()):
+        if q.grad is not None:
+            assert rel(p.grad, q.grad) < 1e-3, name
+
+
 VAR_CFG = dict(cat_kernel=[2, 3], bin_kernel=[5], sqexp_kernel=[0],
                cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
                                {'cont_covariate': 1, 'cat_covariate': 4}],
