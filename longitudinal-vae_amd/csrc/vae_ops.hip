@@ -322,7 +322,9 @@ __global__ __launch_bounds__(256) void conv1_relu_maxpool2_fwd_kernel(const floa
     idx[o] = k;
   }
 }
-constexpr int kWgradPer = 4;      // images per conv3x3_pool_wgrad block
+// images per block of the per-image LDS-staged kernels: 4 at large batches (fewer partials), 1 below
+// 2048 images, where the grid would not fill the GPU
+static inline int imgs_per_block(int N) { return N >= 2048 ? 4 : 1; }
 
 // Weight and bias gradients of a 3 x 3 / stride-1 / padding-1 conv followed by the fused relu + 2x2
 // pool, straight from the pooled gradient: the routed full-resolution gradient has one nonzero per
@@ -485,8 +487,7 @@ int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float
   return 0;
 }
 
-constexpr int kDeconvPer = 4;  // images per deconv2 block
-static int deconv2_blocks(int N, int, int) { return (int)cdiv(N, kDeconvPer); }
+static int deconv2_blocks(int N, int, int) { return (int)cdiv(N, imgs_per_block(N)); }
 
 size_t lvae_deconv2_sigmoid_workspace_size(int N, int Cin, int Hi, int Wi) {
   return N <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)Cin * 16 + 1) * (size_t)deconv2_blocks(N, Hi, Wi);
@@ -500,8 +501,8 @@ int lvae_deconv2_sigmoid_fwd_f32(const float* z, const float* w, const float* bi
   if (total == 0) return 0;
   const size_t lds = sizeof(float) * Cin * (((Hi + 2) * (Wi + 2)) | 1);
   if (lds > 64 * 1024) return -3;
-  deconv2_sigmoid_fwd_kernel<<<cdiv(N, kDeconvPer), 256, lds, (hipStream_t)stream>>>(z, w, bias, N, Cin, Hi, Wi,
-                                                                                      kDeconvPer, out);
+  deconv2_sigmoid_fwd_kernel<<<cdiv(N, imgs_per_block(N)), 256, lds, (hipStream_t)stream>>>(
+      z, w, bias, N, Cin, Hi, Wi, imgs_per_block(N), out);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -520,7 +521,7 @@ int lvae_deconv2_sigmoid_bwd_f32(const float* g, const float* out, const float* 
   float* part = (float*)workspace;
   const size_t lds = sizeof(float) * ((size_t)(2 * Hi + 2) * (2 * Wi + 2) + (size_t)Cin * Hi * Wi);
   if (lds > 64 * 1024) return -3;
-  deconv2_sigmoid_bwd_kernel<<<nb, 256, lds, st>>>(g, out, z, w, N, Cin, Hi, Wi, kDeconvPer, gz, part);
+  deconv2_sigmoid_bwd_kernel<<<nb, 256, lds, st>>>(g, out, z, w, N, Cin, Hi, Wi, imgs_per_block(N), gz, part);
   wgrad_sum_kernel<<<cdiv(m, 64), 256, 0, st>>>(part, nb, m, Cin * 16, dw, db);
   LVAE_CHECK_LAUNCH();
   return 0;
@@ -549,7 +550,7 @@ static size_t conv3x3_pool_wgrad_lds(int C, int Cin, int H, int W) {
 }
 
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin) {
-  return N <= 0 || C <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)C * Cin * 9 + C) * (size_t)cdiv(N, kWgradPer);
+  return N <= 0 || C <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)C * Cin * 9 + C) * (size_t)cdiv(N, imgs_per_block(N));
 }
 
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
@@ -566,14 +567,14 @@ int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* 
     (void)hipMemsetAsync(db, 0, sizeof(float) * C, st);
     return 0;
   }
-  const int nb = (int)cdiv(N, kWgradPer), m = Q * 9 + C;
+  const int per = imgs_per_block(N), nb = (int)cdiv(N, per), m = Q * 9 + C;
   float* part = (float*)workspace;
   const int Ho = H / 2, Wo = W / 2;
   switch (NP) {
-    case 1: conv3x3_pool_wgrad_kernel<1><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
-    case 2: conv3x3_pool_wgrad_kernel<2><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
-    case 3: conv3x3_pool_wgrad_kernel<3><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
-    default: conv3x3_pool_wgrad_kernel<4><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, kWgradPer, part); break;
+    case 1: conv3x3_pool_wgrad_kernel<1><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, per, part); break;
+    case 2: conv3x3_pool_wgrad_kernel<2><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, per, part); break;
+    case 3: conv3x3_pool_wgrad_kernel<3><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, per, part); break;
+    default: conv3x3_pool_wgrad_kernel<4><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, per, part); break;
   }
   wgrad_sum_kernel<<<cdiv(m, 64), 256, 0, st>>>(part, nb, m, Q * 9, dw, db);
   LVAE_CHECK_LAUNCH();

@@ -94,7 +94,8 @@ class _ConvReluMaxPool2(torch.autograd.Function):
         N, C, H, W = ctx.shape
         gy = gy.contiguous()
         Cin = x.shape[1]
-        if C * Cin <= 1024 and 4 * (Cin * (((H + 2) * (W + 2)) | 1) + 2 * C * (H // 2) * (W // 2)) <= 65536:
+        if N >= 512 and C * Cin <= 1024 and 4 * (Cin * (((H + 2) * (W + 2)) | 1) + 2 * C * (H // 2) * (W // 2)) <= 65536:
+            # (below a few hundred images the per-image kernel cannot fill the GPU: MIOpen path)
             # weight and bias gradients from the pooled gradient (lvae_conv3x3_pool_wgrad_f32); the routed
             # full-resolution gradient only feeds the input gradient (MIOpen backward-data), and the
             # first conv (image input) needs none
