@@ -118,6 +118,17 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
                            const double* params, const double* noise, const double* mu, const double* logv,
                            int ld_mu, double* kl, int32_t* info, void* workspace, int need_bwd,
                            void* stream);
+/* The same forward in two calls, for callers that overlap the factorisation with the work that
+ * produces (mu, logv) (the encoder): _factor_f32 needs only the covariates and hyperparameters
+ * (Gram + the sweep: K^-1, log|K|, info into the workspace); _reduce_f32 then takes mu / logv
+ * (alpha = K^-1 mu, the trace and quadratic terms, kl, and with need_bwd the S-GEMM operand).
+ * factor then reduce on one stream (or with the reduce stream waiting on the factor's) equals
+ * lvae_kl_closed_fwd_f32.                                                                        */
+int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                              const double* params, const double* noise, int32_t* info, void* workspace,
+                              void* stream);
+int lvae_kl_closed_reduce_f32(int n, int L, const double* mu, const double* logv, int ld_mu, double* kl,
+                              void* workspace, int need_bwd, void* stream);
 
 /* Backward of lvae_kl_closed_fwd_f32 given dL/dkl[l] = gkl[l]:
  *   dmu[i,l] = gkl_l (K^-1 mu)_i,  dlogv[i,l] = gkl_l/2 (v_i (K^-1)_ii - 1),

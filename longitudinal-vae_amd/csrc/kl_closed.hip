@@ -181,6 +181,59 @@ size_t lvae_kl_closed_workspace_size(int n, int L) {
   return KLWorkspace(nullptr, np_, L).bytes;
 }
 
+int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                              const double* params, const double* noise, int32_t* info, void* workspace,
+                              void* stream) {
+  if (!spec) return -1;
+  if (!x) return -2;
+  if (n <= 0) return -4;
+  if (L <= 0) return -5;
+  if (!params) return -6;
+  if (!noise) return -7;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -9;
+  hipStream_t st = (hipStream_t)stream;
+  const int np_ = lvae_kl_closed_padded_n(n);
+  KLWorkspace ws((char*)workspace, np_, L);
+  {
+    ProfScope ps(LVAE_PH_GRAM, st);
+    LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
+  }
+  {
+    // K^-1 and log|K|: the block symmetric sweep (spd_sweep.hip: 16 rank-256 passes at np = 4096,
+    // pivot inverses overlapped on a second stream)
+    ProfScope ps(LVAE_PH_POTRF, st);
+    LVAE_TRY(spd_sweep_f32(np_, L, ws.A, ws.sweep, ws.Kinv, ws.logdet, info, st));
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_kl_closed_reduce_f32(int n, int L, const double* mu, const double* logv, int ld_mu, double* kl,
+                              void* workspace, int need_bwd, void* stream) {
+  if (n <= 0) return -1;
+  if (L <= 0) return -2;
+  if (!mu || !logv || ld_mu < L) return -3;
+  if (!kl) return -6;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -7;
+  hipStream_t st = (hipStream_t)stream;
+  const int np_ = lvae_kl_closed_padded_n(n);
+  KLWorkspace ws((char*)workspace, np_, L);
+  ProfScope ps(LVAE_PH_KL_REDUCE, st);
+  kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v, ws.sv);
+  const int64_t per = (int64_t)L * np_ * np_;
+  if (need_bwd) {
+    kl_bdiag_kernel<<<L, 256, 0, st>>>(ws.Kinv, ws.sv, np_, ws.gb);
+    kl_alpha_kernel<true><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.gb, ws.alpha, ws.kdiag,
+                                                             ws.rsc, ws.planes, ws.planes + per);
+  } else {
+    kl_alpha_kernel<false><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, nullptr, ws.alpha,
+                                                              ws.kdiag, nullptr, nullptr, nullptr);
+  }
+  kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
 int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,
                            const double* noise, const double* mu, const double* logv, int ld_mu, double* kl,
                            int32_t* info, void* workspace, int need_bwd, void* stream) {
@@ -191,36 +244,10 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   if (!params) return -6;
   if (!noise) return -7;
   if (!mu || !logv || ld_mu < L) return -8;
+  if (!kl) return -11;
   if (!workspace || ((uintptr_t)workspace & 255)) return -13;
-  hipStream_t st = (hipStream_t)stream;
-  const int np_ = lvae_kl_closed_padded_n(n);
-  KLWorkspace ws((char*)workspace, np_, L);
-  {
-    ProfScope ps(LVAE_PH_GRAM, st);
-    LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
-    kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v, ws.sv);
-  }
-  {
-    // K^-1 and log|K|: the block symmetric sweep (spd_sweep.hip: 16 rank-256 passes at np = 4096,
-    // pivot inverses overlapped on a second stream)
-    ProfScope ps(LVAE_PH_POTRF, st);
-    LVAE_TRY(spd_sweep_f32(np_, L, ws.A, ws.sweep, ws.Kinv, ws.logdet, info, st));
-  }
-  {
-    ProfScope ps(LVAE_PH_KL_REDUCE, st);
-    const int64_t per = (int64_t)L * np_ * np_;
-    if (need_bwd) {
-      kl_bdiag_kernel<<<L, 256, 0, st>>>(ws.Kinv, ws.sv, np_, ws.gb);
-      kl_alpha_kernel<true><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.gb, ws.alpha, ws.kdiag,
-                                                               ws.rsc, ws.planes, ws.planes + per);
-    } else {
-      kl_alpha_kernel<false><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, nullptr, ws.alpha,
-                                                                ws.kdiag, nullptr, nullptr, nullptr);
-    }
-    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
-  }
-  LVAE_CHECK_LAUNCH();
-  return 0;
+  LVAE_TRY(lvae_kl_closed_factor_f32(spec, x, ldx, n, L, params, noise, info, workspace, stream));
+  return lvae_kl_closed_reduce_f32(n, L, mu, logv, ld_mu, kl, workspace, need_bwd, stream);
 }
 
 int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,

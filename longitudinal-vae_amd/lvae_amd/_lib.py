@@ -83,6 +83,8 @@ SIGNATURES = {
                                  _VP, _VP, _VP]),
     "lvae_kl_closed_padded_n": (_I32, [_I32]),
     "lvae_kl_closed_workspace_size": (_SZ, [_I32, _I32]),
+    "lvae_kl_closed_factor_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
+    "lvae_kl_closed_reduce_f32": (_I32, [_I32, _I32, _VP, _VP, _I32, _VP, _VP, _I32, _VP]),
     "lvae_kl_closed_fwd_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _I32, _VP, _VP, _VP,
                                       _I32, _VP]),
     "lvae_kl_closed_bwd_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _VP, _VP, _VP, _VP,

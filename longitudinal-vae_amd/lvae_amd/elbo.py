@@ -51,26 +51,80 @@ def check_pending(pend=None):
 # ------------------------------------------------------------------------------------------
 # Regime B: exact KL (elbo_functions.py:8-34), batched over latent dims
 # ------------------------------------------------------------------------------------------
+class KLFactor:
+    """K^-1 and log|K| of the L covariances, computed ahead of (mu, logvar) on a caller stream
+    (lvae_kl_closed_factor_f32): kl_closed_prefactor launches it, KL_closed_batched(..., factor=)
+    waits for it and finishes with lvae_kl_closed_reduce_f32."""
+
+    def __init__(self, spec, params, noise, x, stream):
+        lib = _lib.lib()
+        self.spec, self.params, self.noise = spec, params, noise
+        L = params.shape[0]
+        n = x.shape[0]
+        dev = params.device
+        main = torch.cuda.current_stream(dev)
+        stream.wait_stream(main)
+        with torch.cuda.stream(stream):
+            self.x64 = x.detach().to(torch.float64).contiguous()
+            self.p = params.detach().to(torch.float64).contiguous()
+            nz = noise.detach().to(torch.float64).reshape(L).contiguous()
+            self.ws = torch.empty(int(lib.lvae_kl_closed_workspace_size(n, L)), dtype=torch.uint8, device=dev)
+            self.info = torch.empty(L, dtype=torch.int32, device=dev)
+            rc = lib.lvae_kl_closed_factor_f32(spec, _lib.ptr(self.x64), self.x64.shape[1], n, L, _lib.ptr(self.p),
+                                               _lib.ptr(nz), _lib.ptr(self.info), _lib.ptr(self.ws),
+                                               _lib.stream_ptr())
+            _lib.check(rc, "kl_closed_factor")
+            nz.record_stream(stream)
+        self.stream = stream
+        self.n, self.L = n, L
+
+    def join(self):
+        """Make the current stream wait for the factorisation (and own its buffers)."""
+        cur = torch.cuda.current_stream(self.ws.device)
+        cur.wait_stream(self.stream)
+        for t in (self.ws, self.info, self.x64, self.p):
+            t.record_stream(cur)
+
+
+def kl_closed_prefactor(covar_modules, train_x, likelihoods, L, stream):
+    """Launch the (mu, logvar)-independent part of KL_closed_batched -- the Gram and its sweep
+    inverse -- on ``stream`` now; pass the result as KL_closed_batched(..., factor=)."""
+    spec, params = _stack_modules(covar_modules)
+    if params.shape[0] != L:
+        raise ValueError(f"kernel batch {params.shape[0]} != latent dims {L}")
+    noise = _noise_vector(likelihoods, L).to(params.device)
+    return KLFactor(spec, params, noise, train_x, stream)
+
+
 class _KLClosedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, params, noise, mu, logv, x, spec):
+    def forward(ctx, params, noise, mu, logv, x, spec, factor=None):
         lib = _lib.lib()
         n, L = mu.shape
         dev = mu.device
-        x64 = x.detach().to(torch.float64).contiguous()
-        p = params.detach().to(torch.float64).contiguous()
-        nz = noise.detach().to(torch.float64).reshape(L).contiguous()
         mu64 = mu.detach().to(torch.float64).contiguous()
         lv64 = logv.detach().to(torch.float64).contiguous()
-        ws = torch.empty(int(lib.lvae_kl_closed_workspace_size(n, L)), dtype=torch.uint8, device=dev)
         kl = torch.empty(L, dtype=torch.float64, device=dev)
-        info = torch.empty(L, dtype=torch.int32, device=dev)
         # the backward's S GEMM operand is written by the forward only when a backward can follow
         need_bwd = int(any(t.requires_grad for t in (params, noise, mu, logv)))
-        rc = lib.lvae_kl_closed_fwd_f32(spec, _lib.ptr(x64), x64.shape[1], n, L, _lib.ptr(p), _lib.ptr(nz),
-                                        _lib.ptr(mu64), _lib.ptr(lv64), L, _lib.ptr(kl), _lib.ptr(info),
-                                        _lib.ptr(ws), need_bwd, _lib.stream_ptr())
-        _lib.check(rc, "kl_closed_fwd")
+        if factor is not None:
+            if factor.n != n or factor.L != L:
+                raise ValueError(f"factor is for n={factor.n}, L={factor.L}; got n={n}, L={L}")
+            factor.join()
+            x64, p, ws, info = factor.x64, factor.p, factor.ws, factor.info
+            rc = lib.lvae_kl_closed_reduce_f32(n, L, _lib.ptr(mu64), _lib.ptr(lv64), L, _lib.ptr(kl), _lib.ptr(ws),
+                                               need_bwd, _lib.stream_ptr())
+            _lib.check(rc, "kl_closed_reduce")
+        else:
+            x64 = x.detach().to(torch.float64).contiguous()
+            p = params.detach().to(torch.float64).contiguous()
+            nz = noise.detach().to(torch.float64).reshape(L).contiguous()
+            ws = torch.empty(int(lib.lvae_kl_closed_workspace_size(n, L)), dtype=torch.uint8, device=dev)
+            info = torch.empty(L, dtype=torch.int32, device=dev)
+            rc = lib.lvae_kl_closed_fwd_f32(spec, _lib.ptr(x64), x64.shape[1], n, L, _lib.ptr(p), _lib.ptr(nz),
+                                            _lib.ptr(mu64), _lib.ptr(lv64), L, _lib.ptr(kl), _lib.ptr(info),
+                                            _lib.ptr(ws), need_bwd, _lib.stream_ptr())
+            _lib.check(rc, "kl_closed_fwd")
         _check_info(info, "KL_closed cholesky")
         ctx.save_for_backward(p, mu64, lv64, x64, ws)
         ctx.spec = spec
@@ -92,7 +146,7 @@ class _KLClosedFn(torch.autograd.Function):
                                         _lib.ptr(dnz), _lib.ptr(ws), _lib.stream_ptr())
         _lib.check(rc, "kl_closed_bwd")
         pd, nd, nshape, md, ld = ctx.in_dtypes
-        return dp.to(pd), dnz.to(nd).reshape(nshape), dmu.to(md), dlv.to(ld), None, None
+        return dp.to(pd), dnz.to(nd).reshape(nshape), dmu.to(md), dlv.to(ld), None, None, None
 
 
 def _stack_modules(covar_modules):
@@ -110,10 +164,14 @@ def _noise_vector(likelihoods, L):
     return nz.expand(L) if nz.numel() == 1 else nz
 
 
-def KL_closed_batched(covar_modules, train_x, likelihoods, mu, log_var):
-    """Per-dim exact KLs [L] for mu / log_var [N, L] (one batched HIP pass for all dims)."""
-    spec, params = _stack_modules(covar_modules)
+def KL_closed_batched(covar_modules, train_x, likelihoods, mu, log_var, factor=None):
+    """Per-dim exact KLs [L] for mu / log_var [N, L] (one batched HIP pass for all dims).
+    ``factor``: a kl_closed_prefactor result for the same modules / covariates, whose Gram and
+    inverse were launched ahead (its hyperparameters are the ones differentiated)."""
     L = mu.shape[1]
+    if factor is not None:
+        return _KLClosedFn.apply(factor.params, factor.noise, mu, log_var, train_x, factor.spec, factor)
+    spec, params = _stack_modules(covar_modules)
     if params.shape[0] != L:
         raise ValueError(f"kernel batch {params.shape[0]} != latent dims {L}")
     noise = _noise_vector(likelihoods, L).to(params.device)

@@ -13,7 +13,8 @@ updates) so that a data-parallel all-reduce can sit between two captured graphs.
 """
 import torch
 
-from .elbo import KL_closed_batched, minibatch_KLD_upper_bound, natural_gradient_update, take_pending
+from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_bound, natural_gradient_update,
+                   take_pending)
 
 
 class ClosedStep:
@@ -23,29 +24,40 @@ class ClosedStep:
         self.weight, self.loss_function, self.constrain_scales = weight, loss_function, constrain_scales
         self.grad_hook = grad_hook  # e.g. the data-parallel all-reduce
 
-    def _decoder_stream(self, device):
-        s = getattr(self, "_dec_stream", None)
+    def _stream(self, name, device):
+        s = getattr(self, name, None)
         if s is None or s.device != device:
-            s = self._dec_stream = torch.cuda.Stream(device=device)
+            s = torch.cuda.Stream(device=device)
+            setattr(self, name, s)
         return s
 
     def forward_backward(self, img, mask, X, eps=None):
         self.opt.zero_grad(set_to_none=True)
         if img.is_cuda:
-            # The decoder and the recon loss depend on the encoder only, not on the KL: they run on
-            # a second stream beside the KL forward (Gram + sweep), and autograd runs their backward
-            # on that stream beside the KL backward (S GEMM + Gram adjoint), joining at the encoder.
+            # The Gram and its inverse need only the covariates and hyperparameters: they are
+            # enqueued first, on the caller's stream, and the whole ConvVAE runs on one second stream
+            # beside them -- the encoder (its (mu, logvar) join the KL through an event), then the
+            # decoder and recon loss, which do not depend on the KL at all.  Autograd runs each
+            # backward op on its forward's stream: the decoder backward beside the KL backward (S
+            # GEMM + Gram adjoint), the encoder backward after both.  (Two extra streams at most: the
+            # box exposes 4 hardware queues, and the sweep keeps one side stream of its own.)
             main = torch.cuda.current_stream(img.device)
-            side = self._decoder_stream(img.device)
-            mu, log_var = self.vae.encode(img)
-            z = self.vae.sample_latent(mu, log_var, eps)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
+            vst = self._stream("_vae_stream", img.device)
+            vst.wait_stream(main)  # the previous step's updates, before the factorisation is queued
+            factor = kl_closed_prefactor(self.kernel, X, self.lik, self.vae.latent_dim, main)
+            enc_done = torch.cuda.Event()
+            with torch.cuda.stream(vst):
+                mu, log_var = self.vae.encode(img)
+                enc_done.record(vst)
+                z = self.vae.sample_latent(mu, log_var, eps)
                 recon = self.vae.decode(z)
                 mse, nll = self.vae.loss_function(recon, img, mask)
                 recon_loss, nll_loss = mse.sum(), nll.sum()
-            kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var)
-            main.wait_stream(side)
+            main.wait_event(enc_done)
+            mu.record_stream(main)
+            log_var.record_stream(main)
+            kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var, factor=factor)
+            main.wait_stream(vst)
             recon_loss.record_stream(main)
             nll_loss.record_stream(main)
         else:

@@ -100,6 +100,33 @@ def test_kl_closed_vs_oracle(hip, P, L):
         assert rel(draw, r.grad) < 1e-4
 
 
+def test_kl_closed_prefactor_matches(hip):
+    """KL_closed_batched with the Gram + inverse launched ahead on another stream
+    (kl_closed_prefactor -> lvae_kl_closed_factor_f32, then lvae_kl_closed_reduce_f32) equals the
+    one-call forward bit for bit, values and every gradient."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    P, T, L = 40, 16, 3
+    X = torch.tensor(health_mnist_covariates(P, T, seed=5), device=DEV)
+    k = la.generate_kernel(**CFG, latent_dim=L).double()
+    set_raw(k, _random_hypers(k, L, np.random.default_rng(5)))
+    k = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    gen = torch.Generator().manual_seed(5)
+    mu0 = torch.randn(P * T, L, generator=gen, dtype=torch.float64).to(DEV)
+    lv0 = (0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)).to(DEV)
+    out = []
+    for pre in (False, True):
+        k.zero_grad()
+        mu, lv = mu0.clone().requires_grad_(), lv0.clone().requires_grad_()
+        f = la.kl_closed_prefactor(k, X, lik, L, torch.cuda.Stream()) if pre else None
+        kl = la.KL_closed_batched(k, X, lik, mu, lv, factor=f)
+        (kl * torch.arange(1, L + 1, device=DEV)).sum().backward()
+        out.append([kl.detach(), mu.grad, lv.grad] + [p.grad.clone() for _, p in k.named_parameters()])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_not_positive_definite_raises(hip):
     import lvae_amd as la
     from lvae_amd.data import health_mnist_covariates
