@@ -382,6 +382,7 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
                                                          int np_, int qs, const double* __restrict__ params,
                                                          const float* __restrict__ Kinv,
                                                          const float* __restrict__ S,
+                                                         const float* __restrict__ Sx, int nsplit,
                                                          const double* __restrict__ alpha,
                                                          double* __restrict__ part, int ntiles) {
   __shared__ double sx1[kGT * kMaxQB];
@@ -414,6 +415,13 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
       const int64_t o = (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc;
       kv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(ki + o));
       sv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(si + o));
+    }
+    for (int q = 1; q < nsplit; ++q) {  // K-split partials of S (syrk_x3_splits)
+      const float* sq = Sx + (int64_t)(q - 1) * gridDim.y * np_ * np_ + (int64_t)l * np_ * np_;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        sv4[a] += __builtin_nontemporal_load(
+            reinterpret_cast<const g_f32x4*>(sq + (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc));
     }
     __syncthreads();  // previous tile's LDS readers done
     stage_cov(x, ldx, n, qs, i0, j0, sx1, sx2);
@@ -584,8 +592,9 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L) {
 }
 
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
-                const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
-                double* part, double* dparams, double* dnoise, hipStream_t st) {
+                const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
+                const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
+                hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
   if (!bucket || qs > kMaxQB || spec->n_params > 64) return -1;
@@ -604,11 +613,11 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
   const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2, G = kl_gram_bwd_groups(np_, L);
   const size_t dyn = (size_t)(spec->n_params + 1) * 256 * sizeof(float);
   if (bucket == 1)
-    kl_gram_bwd_tiles<8, 2><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part,
-                                                           ntiles);
+    kl_gram_bwd_tiles<8, 2><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                           alpha, part, ntiles);
   else
-    kl_gram_bwd_tiles<16, 4><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, alpha, part,
-                                                            ntiles);
+    kl_gram_bwd_tiles<16, 4><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                            alpha, part, ntiles);
   kl_gram_bwd_reduce<<<dim3(spec->n_params + 1, L), 256, 0, st>>>(pinfo, spec->n_params, part, G, params, gkl,
                                                                   dparams, dnoise);
   LVAE_CHECK_LAUNCH();

@@ -22,15 +22,18 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
                  const double* params, const double* noise, float* K, hipStream_t st);
 size_t kl_gram_bwd_partials_bytes(int np_, int L);
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
-                const double* params, const float* Kinv, const float* S, const double* alpha, const double* gkl,
-                double* part, double* dparams, double* dnoise, hipStream_t st);
-int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, hipStream_t st);
+                const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
+                const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
+                hipStream_t st);
+int syrk_x3_splits(int np_, int L);
+int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
 int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
                   hipStream_t st);
 size_t spd_sweep_scratch_bytes(int np_, int L);
 
 struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
+  float* Sx;         // K-split partials 1.. of the S GEMM (syrk_x3_splits(np, L) - 1 matrices; few dims only)
   _Float16* planes;  // fp16 hi / lo planes of the S GEMM operand: 2 L np^2 halves
   float* rsc;        // [L, np] their per-row split scales
   float* gb;         // [L] max_j sqrt(Kinv_jj v_j) (kl_bdiag_kernel)
@@ -58,6 +61,7 @@ struct KLWorkspace {
     logdet = (double*)take((size_t)L * sizeof(double));
     sweep = take(spd_sweep_scratch_bytes(np_, L));
     part = (double*)take(kl_gram_bwd_partials_bytes(np_, L));
+    Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
     bytes = off;
   }
 };
@@ -263,12 +267,12 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   // K^-1 diag(sqrt v) the forward wrote (need_bwd; np is a multiple of 256: lvae_kl_closed_padded_n)
   {
     ProfScope ps(LVAE_PH_SYRK, st);
-    LVAE_TRY(syrk_x3_f32(np_, L, ws.rsc, ws.planes, ws.A, st));
+    LVAE_TRY(syrk_x3_f32(np_, L, ws.rsc, ws.planes, ws.A, ws.Sx, st));
   }
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);
-    LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, ws.A, ws.alpha, gkl, ws.part, dparams, dnoise,
-                         st));
+    LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, ws.A, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
+                         gkl, ws.part, dparams, dnoise, st));
   }
   {
     ProfScope ps(LVAE_PH_BWD_ELEM, st);

@@ -16,11 +16,12 @@
 //   prepW(k)  W_i = C_i P^-1 from the planes (one 256 x 256 x3 tile GEMM per block), written IN
 //             PLACE into the column's tiles (transposed into tile (k, i) for i < k) and as the
 //             planes of -W_i
-//   U1(k)     row / column k+1 (incl. the next pivot block): A_ij += (-W_i) C_j^T
+//   U1(k)     row / column k+1: A_ij += (-W_i) C_j^T (at few latent dims per call without the next
+//             pivot block, which pivot(k+1) updates itself: see the schedules below)
 //   U2(k)     the interior tiles (I, J not in {k, k+1}), pre-split planes DMA-staged, C streamed
 //             non-temporally under the MFMAs; the last pass writes -A to Kinv (both triangles)
 //   finish    the last swept column and pivot block to Kinv
-// with lookahead: pivot(k+1), prepC(k+1) and prepW(k+1) run on a side stream beside U2(k).
+// with lookahead: the next pass's chain runs on a side stream beside U2(k) (host sequencing below).
 //
 // Split scales.  Every GEMM operand is split x sc = hi + lo into fp16 planes with a per-(dim, pass)
 // power of two sc = x3_scale(bound), bound >= max |x|, so nothing overflows fp16 whatever the scale
@@ -257,8 +258,95 @@ __device__ inline void pv_trinv(float* D, int lane) {
   pv_store(y, D, rl, hh);
 }
 
+// lower 32 x 32 blocks n = i (i + 1) / 2 + j of the pivot block per wave (up to 3): longest-processing-
+// time assignment for the L^-T L^-1 products (block n costs 8 - i), reused as the wave -> block map
+// of the fused diagonal-block update
+__constant__ signed char kLauum[16][3] = {{0, -1, -1},  {1, 31, -1},  {2, 32, -1},  {3, 26, -1},
+                                          {4, 27, -1},  {5, 28, 33},  {6, 22, 34},  {7, 23, 35},
+                                          {8, 24, -1},  {9, 25, -1},  {10, 17, -1}, {11, 18, -1},
+                                          {12, 19, -1}, {13, 20, -1}, {14, 21, 29}, {15, 16, 30}};
+__device__ inline void pv_ij(int n, int& i, int& j) {
+  i = 0;
+  while ((i + 1) * (i + 2) / 2 <= n) ++i;
+  j = n - i * (i + 1) / 2;
+}
+
+// The pivot block's own pending update from pass kp = kb - 1 (lookahead: the pivot does not wait for
+// U1): lf <- A_kk + (-W_k sW)(C_k sC)^T / (sW sC) on the lower 32 x 32 blocks, from the pass-kp planes
+// (3-product split, as U1 / U2), K = 256 in 4 chunks of 64 staged in the pivot's LDS ([4 parts][256
+// rows][72 halves]: the 144-B row pitch puts a 16-lane ds_read_b128 phase on 16 distinct bank groups).
+constexpr int kPvKC = 64, kPvKP = kPvKC + 8;
+__device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np_, const SwScratch& S, int l, int kb,
+                                         float* __restrict__ lf) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int kp = kb - 1;
+  const SwScales sc = sw_scales(S, l, kp);
+  const float inv = 1.0f / (sc.w * sc.c);
+  const int64_t o = (int64_t)l * np_ * kSwB + (int64_t)kb * kSwBB;
+  const _Float16* src[4] = {S.Wh[kp & 1] + o, S.Wl[kp & 1] + o, S.Ch[kp & 1] + o, S.Cl[kp & 1] + o};
+  _Float16* st = reinterpret_cast<_Float16*>(lf);
+  pv_f32x16 acc[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
+  for (int kc = 0; kc < kSwB; kc += kPvKC) {
+    x3_half8 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {  // 4 parts x 256 rows x 8 16-B chunks = 8 per thread
+      const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
+      v[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * kSwB + kc + 8 * c8);
+    }
+    __syncthreads();  // the previous chunk's readers are done
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
+      *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = v[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int n = kLauum[w][h];
+      if (n < 0) continue;
+      int I, J;
+      pv_ij(n, I, J);
+      const _Float16* ar = st + (32 * I + rl) * kPvKP;
+      const _Float16* br = st + (2 * kSwB + 32 * J + rl) * kPvKP;
+#pragma unroll
+      for (int ks = 0; ks < kPvKC / 16; ++ks) {
+        const int ko = 16 * ks + 8 * hh;
+        const x3_half8 aH = *reinterpret_cast<const x3_half8*>(ar + ko);
+        const x3_half8 aL = *reinterpret_cast<const x3_half8*>(ar + kSwB * kPvKP + ko);
+        const x3_half8 bH = *reinterpret_cast<const x3_half8*>(br + ko);
+        const x3_half8 bL = *reinterpret_cast<const x3_half8*>(br + kSwB * kPvKP + ko);
+        acc[h] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH, acc[h], 0, 0, 0);
+        acc[h] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL, acc[h], 0, 0, 0);
+        acc[h] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH, acc[h], 0, 0, 0);
+      }
+    }
+  }
+  // A_kk (old) + update -> the LDS blocks (after every wave's last staging read)
+  float old[3][16];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n < 0) continue;
+    int I, J;
+    pv_ij(n, I, J);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) old[h][e] = T[(int64_t)(32 * I + pv_row(e, hh)) * np_ + 32 * J + rl];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) lf[n * kPvBlk + pv_row(e, hh) * kPvL + rl] = old[h][e] + acc[h][e] * inv;
+  }
+}
+
 __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall, int np_, int kb, SwScratch S,
-                                                        double* __restrict__ logdet, int32_t* __restrict__ info) {
+                                                        double* __restrict__ logdet, int32_t* __restrict__ info,
+                                                        int pending) {
   __shared__ float lf[kPvBlocks * kPvBlk];
   __shared__ float colsum[kSwB];
   __shared__ uint32_t pmax_s, pn1_s;
@@ -273,8 +361,11 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   if (tid < kSwB) colsum[tid] = 0.f;
   PV_T(0);
   // lower blocks -> LDS (row r = tid >> 5 of a block, 32 consecutive columns per 32 threads); all 36
-  // loads in flight before the first LDS write
-  {
+  // loads in flight before the first LDS write.  With `pending` (kb > 0 in the sweep), the block still
+  // lacks pass kb-1's update, which is applied here from that pass's planes (pv_pending_update).
+  if (pending) {
+    pv_pending_update(T, np_, S, l, kb, lf);
+  } else {
     const int r = tid >> 5, c = tid & 31;
     float v[kPvBlocks];
 #pragma unroll
@@ -360,10 +451,6 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
 
   // 3. P^-1 = L^-T L^-1: block n = i (i + 1) / 2 + j costs 8 - i products; longest-processing-time
   //    assignment, 7-8 products per wave, 30 per SIMD
-  constexpr signed char kLauum[16][3] = {{0, -1, -1},  {1, 31, -1},  {2, 32, -1},  {3, 26, -1},
-                                         {4, 27, -1},  {5, 28, 33},  {6, 22, 34},  {7, 23, 35},
-                                         {8, 24, -1},  {9, 25, -1},  {10, 17, -1}, {11, 18, -1},
-                                         {12, 19, -1}, {13, 20, -1}, {14, 21, 29}, {15, 16, 30}};
   pv_f32x16 res[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
@@ -581,11 +668,12 @@ __global__ __launch_bounds__(512) void sw_prepw_kernel(float* __restrict__ Aall,
 // ~200 us, the GEMM alone ~200 us, together 293 us per launch (a 256 x 128 half-tile form with two
 // workgroups per CU moved 1.5x the plane bytes and took 350-410 us).  Three tile sets (MODE):
 //   kSwU2    the interior: I, J not in {k, k+1} -- on the caller's stream, beside
-//   kSwU1    row / column k+1 (incl. the next pivot block) -- on the side stream, ahead of the next
+//   kSwU1    row / column k+1 (without the next pivot block in schedule (a)) -- on the caller's stream, ahead of the next
 //            pivot and prep (lookahead: those do not wait for the interior update)
 //   kSwLast  every tile of the last pass (I, J != k): -result to Kinv (I, J) and its mirror
 // ------------------------------------------------------------------------------------------
 constexpr int kSwU2 = 0, kSwU1 = 1, kSwLast = 2;
+constexpr int kSwFuseMaxL = 8;  // latent dims per call up to which the pivot updates its own block
 template <int MODE, int CAUX = MODE == kSwLast ? 0 : 2>
 __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall, SwScratch S,
                                                            float* __restrict__ Kinv, int np_, int k,
@@ -596,9 +684,14 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int l = wgid / ntl, t = wgid % ntl, nt = np_ / kSwB;
   int I, J;
-  if constexpr (MODE == kSwU1) {  // t < k: (k+1, t); t == k: (k+1, k+1); t > k: (t+1, k+1)
-    I = t > k ? t + 1 : k + 1;
-    J = t > k ? k + 1 : (t < k ? t : k + 1);
+  if constexpr (MODE == kSwU1) {
+    if (ntl == nt - 1) {  // t < k: (k+1, t); t == k: (k+1, k+1); t > k: (t+1, k+1)
+      I = t > k ? t + 1 : k + 1;
+      J = t > k ? k + 1 : (t < k ? t : k + 1);
+    } else {  // without the pivot block (it updates itself): t < k: (k+1, t); t >= k: (t+2, k+1)
+      I = t >= k ? t + 2 : k + 1;
+      J = t >= k ? k + 1 : t;
+    }
   } else if constexpr (MODE == kSwU2) {
     sx_tri_blocked(t, nt - 2, I, J);
     I += I >= k ? 2 : 0;
@@ -786,22 +879,30 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------
 // host sequencing
 // ------------------------------------------------------------------------------------------
-// Lookahead schedule.  Per pass the caller's stream updates row / column k+1 first (U1(k), one
-// short launch) and then the interior (U2(k)); the side stream (highest priority, so its workgroups
-// are dispatched ahead of U2's as CUs free) runs the next pass's critical chain beside U2(k):
-//     main:  wait ev_prep (prep(k));  U1(k); record ev_u1;  U2(k)
-//     side:  wait ev_u1;  pivot(k+1); prep(k+1); record ev_prep
-// (prep(k+1) writes the other plane buffer, whose readers U1 / U2(k-1) precede U1(k) on the main
-// stream; it copies the swept column k into tiles U2(k) does not touch).  A pass costs
-// U1 + max(U2, pivot + prep) instead of prep + max(U2, U1 + pivot).  (Running U1 on the side stream
-// instead measured slower: its 240 tiles then queue behind U2's for CU slots.)
+// Lookahead schedules.  The side stream has the highest priority, so its workgroups are dispatched
+// ahead of U2's as CUs free.
+// (a) Few latent dims per GPU (L <= kSwFuseMaxL; latent-dim sharding): a pass is bound by its critical
+//     chain, which is shortened by letting the pivot apply pass k's update to its own block from pass k's
+//     planes (pv_pending_update) -- it then waits neither for U1(k) nor for prepC(k+1):
+//       main:  wait ev_prep (prepW(k));  U1(k) (row / column k+1 without the pivot block);  prepC(k+1);
+//              record ev_c;  U2(k);  record ev_u2
+//       side:  wait ev_u2 (U2(k-1): the last writer of block k+1 up to pass k-1);  pivot(k+1);
+//              wait ev_c;  prepW(k+1);  record ev_prep
+//     chain per pass: max(pivot, U1 + prepC) + prepW (was U1 + pivot + prepC + prepW).
+// (b) Many latent dims (the headline L = 16): a pass is bound by total work; the chain runs whole on the
+//     side stream beside U2 (measured 0.3 ms per step faster than (a) at L = 16):
+//       main:  wait ev_prep;  U1(k) (row / column k+1 with the pivot block);  record ev_c;  U2(k)
+//       side:  wait ev_c;  pivot(k+1);  prepC(k+1);  prepW(k+1);  record ev_prep
+// Buffers: prepC(k+1) / prepW(k+1) write the plane set (k+1) & 1, whose readers (U1 / U2(k-1), pivot(k)'s
+// pending update) precede them on the main stream or the side stream; pivot(k+1) writes only its own
+// block and the P planes (read by prepW(k+1), after it).
 // One stream + event set per (device, caller stream), created on first use; the map and every
 // enqueue sequence hold g_side_mu, so host threads sharing a caller stream cannot interleave their
 // records / waits, and callers on different streams never share a side stream.  (Disjoint CU masks
 // for the two streams were measured 2.6 ms per step slower: every masked queue slowed the rest.)
 struct SwSide {
   hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, prep = nullptr, u1 = nullptr;
+  hipEvent_t fork = nullptr, prep = nullptr, c = nullptr, u2 = nullptr;
 };
 
 static std::mutex g_side_mu;
@@ -815,7 +916,7 @@ static int sw_side(hipStream_t caller, SwSide*& out) {  // g_side_mu held by the
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (hipStreamCreateWithPriority(&sd.s, hipStreamNonBlocking, greatest) != hipSuccess) return LVAE_ERR_LAUNCH;
-    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.u1})
+    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.c, &sd.u2})
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
   }
   out = &sd;
@@ -833,31 +934,42 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   LVAE_TRY(sw_side(st, sd));
   SwScratch S((char*)scratch, np_, L);
   const int nt = np_ / kSwB;
-  const int ntl2 = (nt - 2) * (nt - 1) / 2, ntl1 = nt - 1, ntll = (nt - 1) * nt / 2;
+  const int ntl2 = (nt - 2) * (nt - 1) / 2, ntll = (nt - 1) * nt / 2;
   auto ok = [](hipError_t e) { return e == hipSuccess; };
   (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
   (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
   (void)hipMemsetAsync(S.cmax, 0, sizeof(uint32_t) * L * nt, st);
   if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
   if (nt > 1) sw_colmax_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
-  sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info);
+  sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
   if (nt > 1) {
     sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, 0);
     sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, 0);
   }
   if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+  const bool fuse = L <= kSwFuseMaxL;
+  const int ntl1 = fuse ? nt - 2 : nt - 1;
   for (int k = 0; k + 1 < nt; ++k) {
-    if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prep(k)
-    sw_update_kernel<kSwU1><<<ntl1 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl1, ntl1 * L);
-    if (!ok(hipEventRecord(sd->u1, st)) || !ok(hipStreamWaitEvent(sd->s, sd->u1, 0))) return LVAE_ERR_LAUNCH;
-    sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info);
-    sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, k + 1);
+    if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prepW(k)
+    if (ntl1 > 0) sw_update_kernel<kSwU1><<<ntl1 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl1, ntl1 * L);
+    if (fuse) {
+      sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, st>>>(A, S, np_, k + 1);
+      if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
+      if (k > 0 && !ok(hipStreamWaitEvent(sd->s, sd->u2, 0))) return LVAE_ERR_LAUNCH;  // U2(k-1)
+      sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 1);
+      if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;  // prepC(k+1)
+    } else {
+      if (!ok(hipEventRecord(sd->c, st)) || !ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
+      sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0);
+      sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, k + 1);
+    }
     sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, k + 1);
     if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
     if (ntl2 > 0) {
       ProfScope ps(LVAE_PH_SWEEP_UPD, st);
       sw_update_kernel<kSwU2><<<ntl2 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl2, ntl2 * L);
     }
+    if (fuse && !ok(hipEventRecord(sd->u2, st))) return LVAE_ERR_LAUNCH;
   }
   if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // the whole side chain
   if (ntll > 0) sw_update_kernel<kSwLast><<<ntll * L, 512, 0, st>>>(A, S, Kinv, np_, nt - 1, ntll, ntll * L);
@@ -872,7 +984,7 @@ extern "C" {
 #ifdef LVAE_PV_TIMING
 int lvae_pv_timing(float* A, int np_, int L, void* scratch, double* logdet, int32_t* info, unsigned long long* out) {
   lvae::SwScratch S((char*)scratch, np_, L);
-  lvae::sw_pivot_kernel<<<L, 1024>>>(A, np_, 0, S, logdet, info);
+  lvae::sw_pivot_kernel<<<L, 1024>>>(A, np_, 0, S, logdet, info, 0);
   (void)hipDeviceSynchronize();
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lvae::g_pv_t), sizeof(unsigned long long) * 64);
 }

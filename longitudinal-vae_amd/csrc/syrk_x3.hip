@@ -26,20 +26,21 @@ namespace lvae {
 
 __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
                                                       const float* __restrict__ rsc, float* __restrict__ S,
-                                                      int np_, int ntl, int nwg) {
+                                                      float* __restrict__ Sx, int np_, int ntl, int nwg, int L,
+                                                      int kspan) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];  // 128 KB, the only LDS object
   // XCD-contiguous remap (bijective): blocks sharing blockIdx % 8 take a contiguous wgid range
   const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int l = wgid / ntl;
+  const int sp = wgid / (ntl * L), l = (wgid / ntl) % L;  // K split, latent dim
   int I, J;
   sx_tri(wgid % ntl, I, J);
   const int64_t ld = np_;
-  const int64_t base = (int64_t)l * np_ * np_;
-  const _Float16* ah = Bh + base + (int64_t)I * kSxT * ld;
-  const _Float16* al = Bl + base + (int64_t)I * kSxT * ld;
-  const _Float16* bh = Bh + base + (int64_t)J * kSxT * ld;
-  const _Float16* bl = Bl + base + (int64_t)J * kSxT * ld;
+  const int64_t base = (int64_t)l * np_ * np_, k0 = (int64_t)sp * kspan;
+  const _Float16* ah = Bh + base + (int64_t)I * kSxT * ld + k0;
+  const _Float16* al = Bl + base + (int64_t)I * kSxT * ld + k0;
+  const _Float16* bh = Bh + base + (int64_t)J * kSxT * ld + k0;
+  const _Float16* bl = Bl + base + (int64_t)J * kSxT * ld + k0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
   const int r32 = lane & 31, kh = lane >> 5;
@@ -51,11 +52,11 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-  sx_gemm(ah, al, bh, bl, ld, np_, lds, acc);
+  sx_gemm(ah, al, bh, bl, ld, kspan, lds, acc);
   // epilogue: C layout of 32x32 blocks -- row (e&3) + 8(e>>2) + 4(lane>>5), col lane&31
   // per-row split scales of B: S_ij = (B sc)_i (B sc)_j^T / (sc_i sc_j) (exact: powers of two)
   const float* rs = rsc + (int64_t)l * np_;
-  float* C = S + base + (int64_t)(I * kSxT + wm) * ld + J * kSxT + wn;
+  float* C = (sp == 0 ? S : Sx + (int64_t)(sp - 1) * L * np_ * np_) + base + (int64_t)(I * kSxT + wm) * ld + J * kSxT + wn;
   float icol[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b) icol[b] = 1.0f / rs[J * kSxT + wn + 32 * b + r32];
@@ -70,15 +71,34 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
     }
 }
 
+// K splits of the S GEMM: a 256-CU chip holds one 512-thread workgroup per CU (128 KB of LDS), so
+// L * nt (nt + 1) / 2 tiles run in ceil(tiles / 256) rounds; with few latent dims per GPU (latent-dim
+// sharding) the last round is mostly empty (L = 2: 272 tiles = 2 rounds for 1.06 rounds of work).
+// Splitting K into s parts (partials summed by the Gram adjoint, which reads S anyway) runs
+// ceil(s tiles / 256) rounds of 1/s the length, s in {2, 4}, taken only where the round count drops
+// by more than 30%: a split pays its own prologue / epilogue and s-fold partial traffic (measured at
+// np = 4096: L = 2 0.71 -> 0.60 ms with s = 4; L = 4 and L = 8 no gain or slower, L = 1 slower).
+int syrk_x3_splits(int np_, int L) {
+  const int nt = np_ / kSxT, tiles = L * nt * (nt + 1) / 2;
+  auto cost = [&](int s) { return (double)((tiles * s + 255) / 256) / s; };
+  int best = 1;
+  for (int s : {2, 4})
+    if (cost(s) < 0.7 * cost(best)) best = s;
+  return best;
+}
+
 // S (lower 256-tiles of [L, np, np] fp32) = K^-1 diag(v) K^-1 from the fp16 hi / lo planes of
 // B = K^-1 diag(sqrt v) (2 L np^2 halves: hi then lo), row i scaled by rsc[l][i] (kl_alpha_kernel).
-int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, hipStream_t st) {
+// With s = syrk_x3_splits(np, L) > 1 the K-split partials go to S (split 0) and Sx[j - 1] (split j).
+int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, float* Sx, hipStream_t st) {
   if (np_ % kSxT) return -1;
   const int64_t per = (int64_t)np_ * np_;
   const _Float16* Bh = planes;
   const _Float16* Bl = planes + (int64_t)L * per;
-  const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L;
-  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, rsc, S, np_, ntl, nwg);
+  const int ns = syrk_x3_splits(np_, L);
+  if (ns > 1 && !Sx) return -2;
+  const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L * ns;
+  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, rsc, S, Sx, np_, ntl, nwg, L, np_ / ns);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
