@@ -43,17 +43,6 @@ class _ReluMaxPool2(torch.autograd.Function):
         return gx
 
 
-_SIDE = {}
-
-
-def _side_stream(device):
-    """One extra stream per device for kernels that overlap a layer's own backward."""
-    s = _SIDE.get(device)
-    if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device)
-    return s
-
-
 class _ConvReluMaxPool2(torch.autograd.Function):
     """max_pool2d(relu(conv2d(x, w, b, padding=1)), 2, 2) (VAE.py:44-50).
     Forward: a 1-channel input (the first conv) is one direct HIP pass (lvae_conv1_relu_maxpool2_fwd_f32);
@@ -100,21 +89,13 @@ class _ConvReluMaxPool2(torch.autograd.Function):
             # full-resolution gradient only feeds the input gradient (MIOpen backward-data), and the
             # first conv (image input) needs none
             xc = x.contiguous()
-            main = torch.cuda.current_stream(gy.device)
-            # with an input gradient to form, the weight-gradient pass runs on a second stream beside
-            # the routing pass and MIOpen's backward-data conv
-            # (not inside a graph capture: the small-batch Hensman step is launch-bound)
-            wst = (_side_stream(gy.device) if ctx.needs_input_grad[0] and not torch.cuda.is_current_stream_capturing()
-                   else main)
-            wst.wait_stream(main)
-            with torch.cuda.stream(wst):
-                dw = torch.empty_like(weight)
-                db = torch.empty(C, dtype=gy.dtype, device=gy.device)
-                ws = torch.empty(lib.lvae_conv3x3_pool_wgrad_workspace_size(N, C, Cin) // 4 + 1, dtype=torch.float32,
-                                 device=gy.device)
-                _lib.check(lib.lvae_conv3x3_pool_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N, C,
-                                                            Cin, H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
-                                                            _lib.stream_ptr()), "conv3x3_pool_wgrad")
+            dw = torch.empty_like(weight)
+            db = torch.empty(C, dtype=gy.dtype, device=gy.device)
+            ws = torch.empty(lib.lvae_conv3x3_pool_wgrad_workspace_size(N, C, Cin) // 4 + 1, dtype=torch.float32,
+                             device=gy.device)
+            _lib.check(lib.lvae_conv3x3_pool_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N, C, Cin,
+                                                        H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                                        _lib.stream_ptr()), "conv3x3_pool_wgrad")
             gx = None
             if ctx.needs_input_grad[0]:
                 g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
@@ -122,10 +103,6 @@ class _ConvReluMaxPool2(torch.autograd.Function):
                                                            _lib.ptr(g0), _lib.stream_ptr()), "relu_maxpool2_bwd")
                 gx = torch.ops.aten.convolution_backward(g0, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
-            if wst is not main:
-                main.wait_stream(wst)
-                dw.record_stream(main)  # allocated on wst, consumed on main
-                db.record_stream(main)
             return gx, dw if ctx.needs_input_grad[1] else None, db if ctx.needs_input_grad[2] else None
         g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
         db = torch.empty(C, dtype=gy.dtype, device=gy.device)
