@@ -11,29 +11,27 @@
 //
 // Per pass k (all L latent dims in every launch):
 //   pivot(k)  P = A_kk -> -P^-1 into A_kk and the fp16 planes of P^-1 (blocked Cholesky in LDS on
-//             fp32 MFMA, one 1024-thread workgroup per dim), log|P|, info, split bounds
-//   prepC(k)  C_i = A_ik for i != k (the unswept column; tile (k, i)^T where i < k) -> its planes
+//             fp32 MFMA, one 1024-thread workgroup per dim), log|P|, info, its split scale
 //   prepW(k)  W_i = C_i P^-1 from the planes (one 256 x 256 x3 tile GEMM per block), written IN
 //             PLACE into the column's tiles (transposed into tile (k, i) for i < k) and as the
-//             planes of -W_i
-//   U1(k)     row / column k+1: A_ij += (-W_i) C_j^T (at few latent dims per call without the next
-//             pivot block, which pivot(k+1) updates itself: see the schedules below)
+//             planes of -W_i; block k+1 (W_{k+1} = tile (k+1, k)) also as block k of pass k+1's C
+//   U1(k)     row / column k+1: A_ij += (-W_i) C_j^T, written straight as the planes of pass k+1's C
+//             operand (C_i = A_{i,k+1}; at few latent dims per call without the next pivot block,
+//             which pivot(k+1) updates itself: see the schedules below)
 //   U2(k)     the interior tiles (I, J not in {k, k+1}), pre-split planes DMA-staged, C streamed
 //             non-temporally under the MFMAs; the last pass writes -A to Kinv (both triangles)
 //   finish    the last swept column and pivot block to Kinv
-// with lookahead: the next pass's chain runs on a side stream beside U2(k) (host sequencing below).
+// (pass 0's C operand, column 0 of the Gram, is split by prep0).  With lookahead: the next pass's
+// chain runs on a side stream beside U2(k) (host sequencing below).
 //
-// Split scales.  Every GEMM operand is split x sc = hi + lo into fp16 planes with a per-(dim, pass)
-// power of two sc = x3_scale(bound), bound >= max |x|, so nothing overflows fp16 whatever the scale
-// of K (entries of K^-1 grow like 1 / noise):
-//   C_j = A_jk            bound c_k = max |column k| (measured: the producers of column k -- the
-//                         previous pass's U2 tiles of row / column k and W_{k-1}'s block k -- fold
-//                         their max |x| into cmax[l][k] with an integer atomicMax on the fp32 bits)
-//   P^-1                  bound max |P^-1|            (pivot(k), pnorm[l][k][0])
-//   W_i = A_ik P^-1       bound c_k ||P^-1||_1        (pivot(k), pnorm[l][k][1]: max column sum)
+// Split scales.  Every GEMM operand is split x sc = hi + lo into fp16 planes with a power of two
+// sc = x3_scale(max |x|) per 256 x 256 block, taken from the block's EXACT max by the kernel that
+// produces it (U1 / prep0 / prepW for C_i, prepW for W_i, the pivot for P^-1): nothing overflows fp16
+// whatever the scale of K (entries of K^-1 grow like 1 / noise) and every block keeps its top entries
+// at 2^13..2^14.  A tile product W_I C_J^T accumulates in sW_I sC_J units (exact powers of two).
 //
 // Scratch (spd_sweep_scratch_bytes): planes Wh Wl Ch Cl 2 x [L, np, 256] fp16 (by pass parity),
-// Ph Pl [L, 256, 256] fp16, cmax [L, nt] u32, pnorm [L, nt, 2] fp32.  A [L, np, np]: lower
+// Ph Pl [L, 256, 256] fp16, csc / wsc [L, nt, nt] and psc [L, nt] fp32 scales.  A [L, np, np]: lower
 // 256-block tiles read, overwritten.  Kinv [L, np, np]: out, full symmetric.  np % 256 == 0.
 #include "mfma_x3.hpp"
 #include "prof.hpp"
@@ -47,14 +45,15 @@
 namespace lvae {
 
 constexpr int kSwB = 256;  // pivot block
-constexpr int kSwT = 128;  // sub-tile of the prepC / finish copies
+constexpr int kSwT = 128;  // sub-tile of the finish copies
 constexpr int kSwBB = kSwB * kSwB;
 
 struct SwScratch {
   _Float16 *Wh[2], *Wl[2], *Ch[2], *Cl[2];  // [L][np][256], by pass parity (prep(k+1) runs beside U2(k))
   _Float16 *Ph, *Pl;                         // [L][256][256] planes of P^-1 sP
-  uint32_t* cmax;               // [L][nt]   fp32 bits of max |column k| (atomicMax)
-  float* pnorm;                 // [L][nt][2] max |P_k^-1|, max column abs-sum of P_k^-1
+  float* csc;                   // [L][nt][nt] split scale of block i of the C operand of pass k
+  float* wsc;                   // [L][nt][nt] split scale of block i of the W operand of pass k
+  float* psc;                   // [L][nt]     split scale of P_k^-1
   int nt;
   size_t bytes;
   SwScratch(char* base, int np_, int L) {
@@ -74,40 +73,23 @@ struct SwScratch {
     Ph = (_Float16*)take((size_t)L * kSwBB * 2);
     Pl = (_Float16*)take((size_t)L * kSwBB * 2);
     nt = np_ / kSwB;
-    cmax = (uint32_t*)take((size_t)L * nt * 4);
-    pnorm = (float*)take((size_t)L * nt * 2 * 4);
+    csc = (float*)take((size_t)L * nt * nt * 4);
+    wsc = (float*)take((size_t)L * nt * nt * 4);
+    psc = (float*)take((size_t)L * nt * 4);
     bytes = off;
   }
+  __device__ float& c_scale(int l, int k, int i) const { return csc[((int64_t)l * nt + k) * nt + i]; }
+  __device__ float& w_scale(int l, int k, int i) const { return wsc[((int64_t)l * nt + k) * nt + i]; }
 };
 
-// split scales of pass k for latent dim l (see the header): {sW, sC, sP}
-struct SwScales {
-  float w, c, p;
-};
-__device__ inline SwScales sw_scales(const SwScratch& S, int l, int k) {
-  const float cm = __uint_as_float(S.cmax[l * S.nt + k]);
-  const float* pn = S.pnorm + ((int64_t)l * S.nt + k) * 2;
-  return SwScales{x3_scale(cm * pn[1]), x3_scale(cm), x3_scale(pn[0])};
-}
-
-// fold max |v| of a wave into *dst (fp32 bits of non-negative floats order like the integers)
-__device__ inline void sw_fold_max(float v, uint32_t* dst) {
+// max over a 512- or 1024-thread workgroup of the threads' v >= 0 (red: a __shared__ word zeroed by
+// the caller before an earlier barrier); every thread gets the result
+__device__ inline float sw_block_max(float v, uint32_t* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(dst, __float_as_uint(v));
-}
-
-// max |A| over the lower tiles (i, 0), i >= 1 (the C operand of pass 0): grid (nt - 1, L)
-__global__ __launch_bounds__(256) void sw_colmax_kernel(const float* __restrict__ Aall, int np_, SwScratch S) {
-  const int l = blockIdx.y, i = blockIdx.x + 1;
-  const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_;
-  float m = 0.f;
-  for (int e = threadIdx.x; e < kSwB * kSwB / 4; e += 256) {
-    const int r = e >> 6, c = (e & 63) * 4;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(T + (int64_t)r * np_ + c);
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-  }
-  sw_fold_max(m, S.cmax + l * S.nt);
+  if ((threadIdx.x & 63) == 0) atomicMax(red, __float_as_uint(v));
+  __syncthreads();
+  return __uint_as_float(*red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -280,8 +262,7 @@ __device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np
                                          float* __restrict__ lf) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   const int kp = kb - 1;
-  const SwScales sc = sw_scales(S, l, kp);
-  const float inv = 1.0f / (sc.w * sc.c);
+  const float inv = 1.0f / (S.w_scale(l, kp, kb) * S.c_scale(l, kp, kb));
   const int64_t o = (int64_t)l * np_ * kSwB + (int64_t)kb * kSwBB;
   const _Float16* src[4] = {S.Wh[kp & 1] + o, S.Wl[kp & 1] + o, S.Ch[kp & 1] + o, S.Cl[kp & 1] + o};
   _Float16* st = reinterpret_cast<_Float16*>(lf);
@@ -348,17 +329,14 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
                                                         double* __restrict__ logdet, int32_t* __restrict__ info,
                                                         int pending) {
   __shared__ float lf[kPvBlocks * kPvBlk];
-  __shared__ float colsum[kSwB];
-  __shared__ uint32_t pmax_s, pn1_s;
+  __shared__ uint32_t pmax_s;
   __shared__ int bad_s;
   const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
   if (tid == 0) {
     bad_s = INT_MAX;
     pmax_s = 0u;
-    pn1_s = 0u;
   }
-  if (tid < kSwB) colsum[tid] = 0.f;
   PV_T(0);
   // lower blocks -> LDS (row r = tid >> 5 of a block, 32 consecutive columns per 32 threads); all 36
   // loads in flight before the first LDS write.  With `pending` (kb > 0 in the sweep), the block still
@@ -485,12 +463,11 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
 
   // 4. out: T = -P^-1 (both triangles) and the planes of P^-1 sP for prepW (a wave writes 256
   //    consecutive elements of one row; the LDS reads are consecutive (lower part) or pitch-33
-  //    strided (mirror): conflict-free); the column abs-sums (split bound of W)
+  //    strided (mirror): conflict-free)
   const int c = tid & 255;
   const float sP = x3_scale(__uint_as_float(pmax_s));
   _Float16* ph = S.Ph + (int64_t)l * kSwBB;
   _Float16* pl = S.Pl + (int64_t)l * kSwBB;
-  float cs = 0.f;
   for (int r = tid >> 8; r < kSwB; r += 4) {
     const float v = r >= c ? pv_blk(lf, r >> 5, c >> 5)[(r & 31) * kPvL + (c & 31)]
                            : pv_blk(lf, c >> 5, r >> 5)[(c & 31) * kPvL + (r & 31)];
@@ -499,18 +476,12 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
     const _Float16 yh = (_Float16)y;
     ph[r * kSwB + c] = yh;
     pl[r * kSwB + c] = (_Float16)(y - (float)yh);
-    cs += fabsf(v);
   }
-  atomicAdd(&colsum[c], cs);
   if (w == 0 && lane == 0) bad_s = bad;
-  __syncthreads();
-  if (tid < kSwB) atomicMax(&pn1_s, __float_as_uint(colsum[tid]));
   __syncthreads();
   PV_T(23);
   if (tid == 0) {
-    float* pn = S.pnorm + ((int64_t)l * S.nt + kb) * 2;
-    pn[0] = __uint_as_float(pmax_s);
-    pn[1] = __uint_as_float(pn1_s);
+    S.psc[(int64_t)l * S.nt + kb] = sP;
     logdet[l] += ld;
     if (bad_s != INT_MAX && info[l] == 0) info[l] = kb * kSwB + bad_s + 1;
   }
@@ -567,50 +538,89 @@ __device__ inline void sw_split4(f32x4 v, float s, _Float16* __restrict__ hi, _F
 }
 
 // ------------------------------------------------------------------------------------------
-// prepC(k): the planes of C_i = A_ik (i != k; tile (i, k), or tile (k, i)^T for i < k, which for
-// i = k-1 already holds the previous pass's swept W^{k-1}_k^T in place), scale sC.  grid (4 nt, L):
-// (block i, 128 x 128 sub-tile (sm, sn)), 256 threads -- a wide launch of its own: folded into the
-// GEMM's workgroups (one per block) the same work measured slower (126 vs 55 + 79 us per pass).
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sw_prepc_kernel(const float* __restrict__ Aall, SwScratch S, int np_, int k) {
-  __shared__ float lds[64 * 129];
-  const int l = blockIdx.y, w = blockIdx.x, i = w >> 2, sm = (w >> 1) & 1, sn = w & 1;
-  if (i == k) return;
-  const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
-  const float* A = Aall + l * np2;
-  const int64_t sub = (int64_t)i * kSwBB + sm * kSwT * kSwB + sn * kSwT;
-  const float* src = i > k ? A + ((int64_t)i * kSwB + sm * kSwT) * np_ + k * kSwB + sn * kSwT
-                           : A + ((int64_t)k * kSwB + sn * kSwT) * np_ + i * kSwB + sm * kSwT;
-  _Float16* h = S.Ch[k & 1] + l * col + sub;
-  _Float16* lo = S.Cl[k & 1] + l * col + sub;
-  const float scc = sw_scales(S, l, k).c;
-  blk128_visit(src, np_, i < k, lds,
-               [&](int r, int c, f32x4 v) { sw_split4(v, scc, h + r * kSwB + c, lo + r * kSwB + c); });
+// the pass-0 C operand: blocks i >= 1 of column 0 (tile (i, 0)), each with its own split scale from its
+// exact max.  grid (nt - 1, L), 256 threads: one pass for the max, one for the planes.
+__global__ __launch_bounds__(256) void sw_prep0_kernel(const float* __restrict__ Aall, int np_, SwScratch S) {
+  __shared__ uint32_t red;
+  const int l = blockIdx.y, i = blockIdx.x + 1, t = threadIdx.x;
+  const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_;
+  if (t == 0) red = 0u;
+  float m = 0.f;
+  for (int e = t; e < kSwBB / 4; e += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + (int64_t)(e >> 6) * np_ + (e & 63) * 4);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((t & 63) == 0) atomicMax(&red, __float_as_uint(m));
+  __syncthreads();
+  const float sc = x3_scale(__uint_as_float(red));
+  const int64_t o = (int64_t)l * np_ * kSwB + (int64_t)i * kSwBB;
+  for (int e = t; e < kSwBB / 4; e += 256) {
+    const int r = e >> 6, c = (e & 63) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + (int64_t)r * np_ + c);
+    sw_split4(v, sc, S.Ch[0] + o + r * kSwB + c, S.Cl[0] + o + r * kSwB + c);
+  }
+  if (t == 0) S.c_scale(l, 0, i) = sc;
 }
 
 // ------------------------------------------------------------------------------------------
-// prepW(k): W_i = A_ik P^-1 = (C_i sC)(P^-1 sP) / (sC sP) for i != k: one 512-thread workgroup per
+// 256 x 256 tile in accumulators (value = acc * mul) out TRANSPOSED through the workgroup's 128 KB LDS
+// stage, per 128-row half: fn(c, r0, v) gets v = (value(r0 + q, c))_{q < 4} -- row c of the transpose,
+// columns r0 .. r0 + 3 -- every (c, r0) once (coalesced 512-B rows whatever fn stores).  Starts with a
+// barrier: the caller's last reads of the LDS stage must precede it.
+// ------------------------------------------------------------------------------------------
+template <typename Fn>
+__device__ inline void sx_transposed_out(const sx_f32x16 (&acc)[4][2], float mul, _Float16* lds, Fn fn) {
+  float* U = reinterpret_cast<float*>(lds);
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    __syncthreads();  // hh = 0: the caller's last LDS reads; hh = 1: the half-0 readers
+    if ((w >> 2) == hh) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int rl = sx_row(a, e) - 128 * hh, c = sx_col(b);
+            U[c * 128 + (rl ^ ((c & 31) << 2))] = acc[a][b][e] * mul;
+          }
+    }
+    __syncthreads();
+    const int t4 = tid & 31;
+#pragma unroll 4
+    for (int cc = 0; cc < kSwB; cc += 16) {
+      const int c = cc + (tid >> 5), rl = 4 * t4;
+      fn(c, 128 * hh + rl, *reinterpret_cast<const f32x4*>(&U[c * 128 + (rl ^ ((c & 31) << 2))]));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// prepW(k): W_i = A_ik P^-1 = (C_i sC_i)(P^-1 sP) / (sC_i sP) for i != k: one 512-thread workgroup per
 // 256 x 256 block on the pre-split planes (sx_gemm, K = 256), grid (nt - 1, L).  W_i goes IN PLACE
 // into the swept column -- tile (i, k), or transposed (through LDS) into tile (k, i) for i < k: the
-// column's readers are done (prepC read it, U1 / U2 read only planes) -- and as the planes of -W_i sW.
-// W_{k+1} is part of column k+1, so its max |W| folds into cmax[k+1].
+// column's readers are done (U1 / U2 read only planes) -- and as the planes of -W_i sW_i, sW_i from
+// the block's exact max.  W_{k+1} = tile (k+1, k) is also block k of the NEXT pass's C operand
+// (column k+1): its transpose goes to that pass's C planes with the same scale.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(512) void sw_prepw_kernel(float* __restrict__ Aall, SwScratch S, int np_, int k) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  __shared__ uint32_t red;
   const int l = blockIdx.y, i = blockIdx.x < k ? blockIdx.x : blockIdx.x + 1;
   const int64_t np2 = (int64_t)np_ * np_, col = (int64_t)np_ * kSwB;
   const int64_t oc = l * col + (int64_t)i * kSwBB, op = (int64_t)l * kSwBB;
-  const SwScales sc = sw_scales(S, l, k);
+  if (threadIdx.x == 0) red = 0u;
   sx_f32x16 acc[4][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
   sx_gemm(S.Ch[k & 1] + oc, S.Cl[k & 1] + oc, S.Ph + op, S.Pl + op, kSwB, kSwB, lds, acc);
-  const float inv = 1.0f / (sc.c * sc.p);
-  _Float16* wh = S.Wh[k & 1] + oc;
-  _Float16* wl = S.Wl[k & 1] + oc;
-  float* A = Aall + l * np2;
+  const float inv = 1.0f / (S.c_scale(l, k, i) * S.psc[(int64_t)l * S.nt + k]);
   float wm = 0.f;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -618,45 +628,42 @@ __global__ __launch_bounds__(512) void sw_prepw_kernel(float* __restrict__ Aall,
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
+        acc[a][b][e] *= inv;
+        wm = fmaxf(wm, fabsf(acc[a][b][e]));
+      }
+  const float sw = x3_scale(sw_block_max(wm, &red));
+  _Float16* wh = S.Wh[k & 1] + oc;
+  _Float16* wl = S.Wl[k & 1] + oc;
+  float* A = Aall + l * np2;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
         const int r = sx_row(a, e), c = sx_col(b);
-        const float v = acc[a][b][e] * inv;
-        acc[a][b][e] = v;
-        wm = fmaxf(wm, fabsf(v));
-        const float y = -v * sc.w;
+        const float v = acc[a][b][e];
+        const float y = -v * sw;
         const _Float16 yh = (_Float16)y;
         wh[r * kSwB + c] = yh;
         wl[r * kSwB + c] = (_Float16)(y - (float)yh);
         if (i > k) A[(int64_t)(i * kSwB + r) * np_ + k * kSwB + c] = v;
       }
-  if (i < k) {  // tile (k, i) = W_i^T, per 128-row half of W through LDS (coalesced 512-B rows)
-    float* U = reinterpret_cast<float*>(lds);
-    const int tid = threadIdx.x, w = tid >> 6;
+  if (threadIdx.x == 0) S.w_scale(l, k, i) = sw;
+  if (i < k) {  // tile (k, i) = W_i^T
     float* Ot = A + (int64_t)k * kSwB * np_ + i * kSwB;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      __syncthreads();  // hh = 0: the GEMM's last LDS reads; hh = 1: the half-0 readers
-      if ((w >> 2) == hh) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-              const int rl = sx_row(a, e) - 128 * hh, c = sx_col(b);
-              U[c * 128 + (rl ^ ((c & 31) << 2))] = acc[a][b][e];
-            }
-      }
-      __syncthreads();
-      const int t4 = tid & 31;
-#pragma unroll 4
-      for (int cc = 0; cc < kSwB; cc += 16) {
-        const int c = cc + (tid >> 5), rl = 4 * t4;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(&U[c * 128 + (rl ^ ((c & 31) << 2))]);
-        *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + 128 * hh + rl) = v;
-      }
-    }
+    sx_transposed_out(acc, 1.0f, lds, [&](int c, int r0, f32x4 v) {
+      *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
+    });
+  } else if (i == k + 1) {  // block k of the C operand of pass k+1 = W_{k+1}^T
+    const int64_t on = l * col + (int64_t)k * kSwBB;
+    _Float16* ch = S.Ch[(k + 1) & 1] + on;
+    _Float16* cl = S.Cl[(k + 1) & 1] + on;
+    sx_transposed_out(acc, 1.0f, lds, [&](int c, int r0, f32x4 v) {
+      sw_split4(v, sw, ch + c * kSwB + r0, cl + c * kSwB + r0);
+    });
+    if (threadIdx.x == 0) S.c_scale(l, k + 1, k) = sw;
   }
-  if (i == k + 1) sw_fold_max(wm, S.cmax + l * S.nt + k + 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -680,6 +687,8 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
                                                            int ntl, int nwg) {
   constexpr bool LAST = MODE == kSwLast;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  __shared__ uint32_t red;
+  if (MODE == kSwU1 && threadIdx.x == 0) red = 0u;
   const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int l = wgid / ntl, t = wgid % ntl, nt = np_ / kSwB;
@@ -707,8 +716,7 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
   const int64_t oa = l * col + (int64_t)I * kSwBB, ob = l * col + (int64_t)J * kSwBB;
-  const SwScales sc = sw_scales(S, l, k);
-  const float cs = sc.w * sc.c, inv = 1.0f / cs;  // accumulate in sW sC units (exact powers of two)
+  const float cs = S.w_scale(l, k, I) * S.c_scale(l, k, J), inv = 1.0f / cs;  // sW_I sC_J units (powers of 2)
   const _Float16* ah = S.Wh[k & 1] + oa;
   const _Float16* al = S.Wl[k & 1] + oa;
   const _Float16* bh = S.Ch[k & 1] + ob;
@@ -772,21 +780,61 @@ __global__ __launch_bounds__(512) void sw_update_kernel(float* __restrict__ Aall
   U2_T(2, wall_clock64());
   U2_T(4, t_wait);
 #endif
-  if constexpr (!LAST) {
-    float mx = 0.f;
+  if constexpr (MODE == kSwU1) {
+    if (I == J) {  // the next pivot block (schedule (b)): stored for the pivot
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), rc, vo,
+                                                  ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
+    } else {
+      // a tile of column k+1 = one block of the next pass's C operand: straight to its planes with the
+      // block's own split scale (its fp32 copy is dead: prepW(k+1) overwrites the column in place)
+      float mx = 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) mx = fmaxf(mx, fabsf(acc[a][b][e] * inv));
+      const float sc = x3_scale(sw_block_max(mx, &red));
+      const int blk = J == k + 1 ? I : J;
+      const int64_t on = l * col + (int64_t)blk * kSwBB;
+      _Float16* ch = S.Ch[(k + 1) & 1] + on;
+      _Float16* cl = S.Cl[(k + 1) & 1] + on;
+      if (J == k + 1) {  // tile (I, k+1): block I as is
+        const float m = inv * sc;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int r = sx_row(a, e), c = sx_col(b);
+              const float y = acc[a][b][e] * m;
+              const _Float16 yh = (_Float16)y;
+              ch[r * kSwB + c] = yh;
+              cl[r * kSwB + c] = (_Float16)(y - (float)yh);
+            }
+      } else {  // tile (k+1, J): block J is its transpose
+        sx_transposed_out(acc, inv, lds, [&](int c, int r0, f32x4 v) {
+          sw_split4(v, sc, ch + c * kSwB + r0, cl + c * kSwB + r0);
+        });
+      }
+      if (threadIdx.x == 0) S.c_scale(l, k + 1, blk) = sc;
+    }
+  } else if constexpr (!LAST) {
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int e = 0; e < 16; ++e)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const float v = acc[a][b][e] * inv;
-          mx = fmaxf(mx, fabsf(v));
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, vo,
+        for (int b = 0; b < 2; ++b)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), rc, vo,
                                                 ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
-        }
-    // tiles of row / column k+1 (not the next pivot block): the C operand of the next pass
-    if (MODE == kSwU1 && I != J) sw_fold_max(mx, S.cmax + l * S.nt + k + 1);
 #ifdef LVAE_PV_TIMING
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     U2_T(3, wall_clock64());
@@ -883,19 +931,21 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 // ahead of U2's as CUs free.
 // (a) Few latent dims per GPU (L <= kSwFuseMaxL; latent-dim sharding): a pass is bound by its critical
 //     chain, which is shortened by letting the pivot apply pass k's update to its own block from pass k's
-//     planes (pv_pending_update) -- it then waits neither for U1(k) nor for prepC(k+1):
-//       main:  wait ev_prep (prepW(k));  U1(k) (row / column k+1 without the pivot block);  prepC(k+1);
-//              record ev_c;  U2(k);  record ev_u2
+//     planes (pv_pending_update) -- it then does not wait for U1(k):
+//       main:  wait ev_prep (prepW(k));  U1(k) (row / column k+1 without the pivot block: pass k+1's
+//              C planes);  record ev_c;  U2(k);  record ev_u2
 //       side:  wait ev_u2 (U2(k-1): the last writer of block k+1 up to pass k-1);  pivot(k+1);
 //              wait ev_c;  prepW(k+1);  record ev_prep
-//     chain per pass: max(pivot, U1 + prepC) + prepW (was U1 + pivot + prepC + prepW).
+//     chain per pass: max(pivot, U1) + prepW (was U1 + pivot + prepW).
 // (b) Many latent dims (the headline L = 16): a pass is bound by total work; the chain runs whole on the
 //     side stream beside U2 (measured 0.3 ms per step faster than (a) at L = 16):
 //       main:  wait ev_prep;  U1(k) (row / column k+1 with the pivot block);  record ev_c;  U2(k)
-//       side:  wait ev_c;  pivot(k+1);  prepC(k+1);  prepW(k+1);  record ev_prep
-// Buffers: prepC(k+1) / prepW(k+1) write the plane set (k+1) & 1, whose readers (U1 / U2(k-1), pivot(k)'s
-// pending update) precede them on the main stream or the side stream; pivot(k+1) writes only its own
-// block and the P planes (read by prepW(k+1), after it).
+//       side:  wait ev_c;  pivot(k+1);  prepW(k+1);  record ev_prep
+// Buffers: U1(k) and prepW(k) write the C planes of pass k+1, prepW(k+1) the W planes of pass k+1 and
+// block k+1 of pass k+2's C planes, all in the plane set (k+1) & 1 (block k+1 of set k & 1 for the
+// latter, whose last readers, U1(k) and pivot(k+1), precede prepW(k+1)); the readers of set (k+1) & 1
+// from pass k-1 (U1 / U2(k-1), prepW(k-1), pivot(k)'s pending update) precede its writers on the main
+// or the side stream.  pivot(k+1) writes only its own block and the P planes (read by prepW(k+1)).
 // One stream + event set per (device, caller stream), created on first use; the map and every
 // enqueue sequence hold g_side_mu, so host threads sharing a caller stream cannot interleave their
 // records / waits, and callers on different streams never share a side stream.  (Disjoint CU masks
@@ -938,12 +988,10 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   auto ok = [](hipError_t e) { return e == hipSuccess; };
   (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
   (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
-  (void)hipMemsetAsync(S.cmax, 0, sizeof(uint32_t) * L * nt, st);
   if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
-  if (nt > 1) sw_colmax_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
   sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
   if (nt > 1) {
-    sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, 0);
+    sw_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
     sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, 0);
   }
   if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
@@ -952,16 +1000,14 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   for (int k = 0; k + 1 < nt; ++k) {
     if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prepW(k)
     if (ntl1 > 0) sw_update_kernel<kSwU1><<<ntl1 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl1, ntl1 * L);
+    if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;  // U1(k): the C planes of pass k+1
     if (fuse) {
-      sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, st>>>(A, S, np_, k + 1);
-      if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
       if (k > 0 && !ok(hipStreamWaitEvent(sd->s, sd->u2, 0))) return LVAE_ERR_LAUNCH;  // U2(k-1)
       sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 1);
-      if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;  // prepC(k+1)
+      if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
     } else {
-      if (!ok(hipEventRecord(sd->c, st)) || !ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
+      if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
       sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0);
-      sw_prepc_kernel<<<dim3(4 * nt, L), 256, 0, sd->s>>>(A, S, np_, k + 1);
     }
     sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, k + 1);
     if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
