@@ -269,13 +269,16 @@ __device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np
   pv_f32x16 acc[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
-  for (int kc = 0; kc < kSwB; kc += kPvKC) {
-    x3_half8 v[8];
+  x3_half8 v[8];
+  auto load = [&](int kc) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {  // 4 parts x 256 rows x 8 16-B chunks = 8 per thread
       const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
       v[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * kSwB + kc + 8 * c8);
     }
+  };
+  load(0);
+  for (int kc = 0; kc < kSwB; kc += kPvKC) {
     __syncthreads();  // the previous chunk's readers are done
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -283,6 +286,7 @@ __device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np
       *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = v[u];
     }
     __syncthreads();
+    if (kc + kPvKC < kSwB) load(kc + kPvKC);  // the next chunk's loads fly under this chunk's MFMAs
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
       const int n = kLauum[w][h];

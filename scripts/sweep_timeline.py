@@ -3,9 +3,9 @@ import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-key = [("sw_pivot_kernel", "pivot"), ("sw_prepc_kernel", "prepC"), ("sw_prepw_kernel", "prepW"),
+key = [("sw_pivot_kernel", "pivot"), ("sw_prep0_kernel", "prep0"), ("sw_prepw_kernel", "prepW"),
        ("sw_update_kernel<1", "U1"), ("sw_update_kernel<0", "U2"), ("sw_update_kernel<2", "LAST"),
-       ("sw_finish_kernel", "finish"), ("sw_colmax_kernel", "colmax")]
+       ("sw_finish_kernel", "finish")]
 ev = []
 for r in rows:
     name = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
@@ -13,9 +13,9 @@ for r in rows:
         if k in name:
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short))
 ev.sort()
-# the last sweep starts at the last colmax
-starts = [i for i, e in enumerate(ev) if e[2] == "colmax"]
-ev = ev[starts[-1]:]
+# the last sweep starts with the pivot before its prep0
+starts = [i for i, e in enumerate(ev) if e[2] == "prep0"]
+ev = ev[max(starts[-1] - 1, 0):]
 t0 = ev[0][0]
 tot = {}
 for s, e, n in ev:

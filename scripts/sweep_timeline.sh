@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel timeline of the batched sweep alone (rocprofv3 kernel trace of scripts/sweep_micro.py):
-# per pass, start / end of pivot, prepC, prepW, U1, U2 relative to the sweep's first kernel.
+# per pass, start / end of pivot, prep0, prepW, U1, U2 relative to the sweep's first kernel.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/${TL_NAME:-timeline}
