@@ -50,7 +50,8 @@ constexpr int kSwBB = kSwB * kSwB;
 
 struct SwScratch {
   _Float16 *Wh[2], *Wl[2], *Ch[2], *Cl[2];  // [L][np][256], by pass parity (prep(k+1) runs beside U2(k))
-  _Float16 *Ph, *Pl;                         // [L][256][256] planes of P^-1 sP
+  _Float16 *Ph[2], *Pl[2];                   // [L][256][256] planes of P^-1 sP, by pass parity
+  _Float16 *Xh, *Xl;                         // [L][256][256] the pivot's own W block (schedule (a))
   float* csc;                   // [L][nt][nt] split scale of block i of the C operand of pass k
   float* wsc;                   // [L][nt][nt] split scale of block i of the W operand of pass k
   float* psc;                   // [L][nt]     split scale of P_k^-1
@@ -70,8 +71,12 @@ struct SwScratch {
       Ch[b] = (_Float16*)take(col * 2);
       Cl[b] = (_Float16*)take(col * 2);
     }
-    Ph = (_Float16*)take((size_t)L * kSwBB * 2);
-    Pl = (_Float16*)take((size_t)L * kSwBB * 2);
+    for (int b = 0; b < 2; ++b) {
+      Ph[b] = (_Float16*)take((size_t)L * kSwBB * 2);
+      Pl[b] = (_Float16*)take((size_t)L * kSwBB * 2);
+    }
+    Xh = (_Float16*)take((size_t)L * kSwBB * 2);
+    Xl = (_Float16*)take((size_t)L * kSwBB * 2);
     nt = np_ / kSwB;
     csc = (float*)take((size_t)L * nt * nt * 4);
     wsc = (float*)take((size_t)L * nt * nt * 4);
@@ -253,22 +258,18 @@ __device__ inline void pv_ij(int n, int& i, int& j) {
   j = n - i * (i + 1) / 2;
 }
 
-// The pivot block's own pending update from pass kp = kb - 1 (lookahead: the pivot does not wait for
-// U1): lf <- A_kk + (-W_k sW)(C_k sC)^T / (sW sC) on the lower 32 x 32 blocks, from the pass-kp planes
-// (3-product split, as U1 / U2), K = 256 in 4 chunks of 64 staged in the pivot's LDS ([4 parts][256
-// rows][72 halves]: the 144-B row pitch puts a 16-lane ds_read_b128 phase on 16 distinct bank groups).
+// acc[h] += A(I_h) B(J_h)^T over K = 256 on the f16 cores (x3 split) for up to NB 32 x 32 blocks per
+// wave (I_h < 0: none), A = (src[0] hi, src[1] lo) and B = (src[2], src[3]) fp16 planes, 256 rows of
+// 256 halves each.  K in 4 chunks of 64 staged in the pivot's LDS ([4 parts][256 rows][72 halves]: the
+// 144-B row pitch puts a 16-lane ds_read_b128 phase on 16 distinct bank groups); PREF: the next chunk's
+// global loads are issued under the current chunk's MFMAs (8 more VGPR quads).  Ends after a barrier
+// only if the caller adds one: the staging area is still being read.
 constexpr int kPvKC = 64, kPvKP = kPvKC + 8;
-__device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np_, const SwScratch& S, int l, int kb,
-                                         float* __restrict__ lf) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
-  const int kp = kb - 1;
-  const float inv = 1.0f / (S.w_scale(l, kp, kb) * S.c_scale(l, kp, kb));
-  const int64_t o = (int64_t)l * np_ * kSwB + (int64_t)kb * kSwBB;
-  const _Float16* src[4] = {S.Wh[kp & 1] + o, S.Wl[kp & 1] + o, S.Ch[kp & 1] + o, S.Cl[kp & 1] + o};
+template <int NB, bool PREF>
+__device__ inline void pv_x3_gemm(const _Float16* const* src, float* __restrict__ lf, const int* bi, const int* bj,
+                                  pv_f32x16* acc) {
+  const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
   _Float16* st = reinterpret_cast<_Float16*>(lf);
-  pv_f32x16 acc[3];
-#pragma unroll
-  for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
   x3_half8 v[8];
   auto load = [&](int kc) {
 #pragma unroll
@@ -277,24 +278,38 @@ __device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np
       v[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * kSwB + kc + 8 * c8);
     }
   };
-  load(0);
+  if (PREF) load(0);
   for (int kc = 0; kc < kSwB; kc += kPvKC) {
     __syncthreads();  // the previous chunk's readers are done
+    if (PREF) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
-      *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = v[u];
+      for (int u = 0; u < 8; ++u) {
+        const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
+        *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = v[u];
+      }
+    } else {  // two rounds of 4 (fewer live registers beside a 4-block accumulator set)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        x3_half8 t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = tid + 1024 * (4 * q + u), p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
+          t[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * kSwB + kc + 8 * c8);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = tid + 1024 * (4 * q + u), p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
+          *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = t[u];
+        }
+      }
     }
     __syncthreads();
-    if (kc + kPvKC < kSwB) load(kc + kPvKC);  // the next chunk's loads fly under this chunk's MFMAs
+    if (PREF && kc + kPvKC < kSwB) load(kc + kPvKC);
 #pragma unroll
-    for (int h = 0; h < 3; ++h) {
-      const int n = kLauum[w][h];
-      if (n < 0) continue;
-      int I, J;
-      pv_ij(n, I, J);
-      const _Float16* ar = st + (32 * I + rl) * kPvKP;
-      const _Float16* br = st + (2 * kSwB + 32 * J + rl) * kPvKP;
+    for (int h = 0; h < NB; ++h) {
+      if (bi[h] < 0) continue;
+      const _Float16* ar = st + (32 * bi[h] + rl) * kPvKP;
+      const _Float16* br = st + (2 * kSwB + 32 * bj[h] + rl) * kPvKP;
 #pragma unroll
       for (int ks = 0; ks < kPvKC / 16; ++ks) {
         const int ko = 16 * ks + 8 * hh;
@@ -308,18 +323,83 @@ __device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np
       }
     }
   }
-  // A_kk (old) + update -> the LDS blocks (after every wave's last staging read)
-  float old[3][16];
+}
+
+// The pivot block's own pending update from pass kp = kb - 1 (schedule (a): the pivot waits neither
+// for U1 nor for prepW of the previous pass):
+//   X = W_kb = C_kb P_kp^-1   (C_kb: block kb of pass kp's C planes, P_kp^-1: the previous pivot's
+//                              planes; x3 GEMM, all 64 blocks, 4 per wave), split at its exact max into
+//                              the planes of -X (Xh / Xl, this dim's scratch)
+//   lf <- A_kk + (-X) C_kb^T  (the 36 lower blocks, kLauum's wave map)
+// red: a __shared__ word zeroed by the caller before an earlier barrier.
+__device__ inline void pv_pending_update(const float* __restrict__ T, int64_t np_, const SwScratch& S, int l, int kb,
+                                         float* __restrict__ lf, uint32_t* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int kp = kb - 1;
+  const int64_t oc = (int64_t)l * np_ * kSwB + (int64_t)kb * kSwBB, op = (int64_t)l * kSwBB;
+  const float sc = S.c_scale(l, kp, kb);
+  float sxo;  // X's split scale (the same in every thread)
+  // X = C_kb P^-1 (P^-1 symmetric: its rows are the B operand)
+  {
+    const _Float16* src[4] = {S.Ch[kp & 1] + oc, S.Cl[kp & 1] + oc, S.Ph[kp & 1] + op, S.Pl[kp & 1] + op};
+    int bi[4], bj[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) bi[h] = (4 * w + h) >> 3, bj[h] = (4 * w + h) & 7;
+    pv_f32x16 x[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) x[h] = pv_f32x16{};
+    pv_x3_gemm<4, false>(src, lf, bi, bj, x);
+    const float inv = 1.0f / (sc * S.psc[(int64_t)l * S.nt + kp]);
+    float m = 0.f;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        x[h][e] *= inv;
+        m = fmaxf(m, fabsf(x[h][e]));
+      }
+    const float sx = x3_scale(sw_block_max(m, red));
+    _Float16* xh = S.Xh + op;
+    _Float16* xl = S.Xl + op;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = 32 * bi[h] + pv_row(e, hh), c = 32 * bj[h] + rl;
+        const float y = -x[h][e] * sx;
+        const _Float16 yh = (_Float16)y;
+        xh[r * kSwB + c] = yh;
+        xl[r * kSwB + c] = (_Float16)(y - (float)yh);
+      }
+    sxo = sx;
+    __syncthreads();  // the X planes are visible to the workgroup (workgroup-scope release / acquire)
+  }
+  const float sx = sxo;
+  // lf <- A_kk + (-X) C_kb^T on the lower blocks
+  const _Float16* src[4] = {S.Xh + op, S.Xl + op, S.Ch[kp & 1] + oc, S.Cl[kp & 1] + oc};
+  int bi[3], bj[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
     const int n = kLauum[w][h];
-    if (n < 0) continue;
-    int I, J;
-    pv_ij(n, I, J);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) old[h][e] = T[(int64_t)(32 * I + pv_row(e, hh)) * np_ + 32 * J + rl];
+    if (n < 0) {
+      bi[h] = bj[h] = -1;
+    } else {
+      pv_ij(n, bi[h], bj[h]);
+    }
   }
-  __syncthreads();
+  pv_f32x16 acc[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
+  pv_x3_gemm<3, true>(src, lf, bi, bj, acc);
+  const float inv = 1.0f / (sx * sc);
+  float old[3][16];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    if (bi[h] < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) old[h][e] = T[(int64_t)(32 * bi[h] + pv_row(e, hh)) * np_ + 32 * bj[h] + rl];
+  }
+  __syncthreads();  // every wave's last staging read
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
     const int n = kLauum[w][h];
@@ -333,20 +413,22 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
                                                         double* __restrict__ logdet, int32_t* __restrict__ info,
                                                         int pending) {
   __shared__ float lf[kPvBlocks * kPvBlk];
-  __shared__ uint32_t pmax_s;
+  __shared__ uint32_t pmax_s, xmax_s;
   __shared__ int bad_s;
   const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
   if (tid == 0) {
     bad_s = INT_MAX;
     pmax_s = 0u;
+    xmax_s = 0u;
   }
   PV_T(0);
   // lower blocks -> LDS (row r = tid >> 5 of a block, 32 consecutive columns per 32 threads); all 36
   // loads in flight before the first LDS write.  With `pending` (kb > 0 in the sweep), the block still
   // lacks pass kb-1's update, which is applied here from that pass's planes (pv_pending_update).
   if (pending) {
-    pv_pending_update(T, np_, S, l, kb, lf);
+    __syncthreads();  // xmax_s
+    pv_pending_update(T, np_, S, l, kb, lf, &xmax_s);
   } else {
     const int r = tid >> 5, c = tid & 31;
     float v[kPvBlocks];
@@ -470,8 +552,8 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   //    strided (mirror): conflict-free)
   const int c = tid & 255;
   const float sP = x3_scale(__uint_as_float(pmax_s));
-  _Float16* ph = S.Ph + (int64_t)l * kSwBB;
-  _Float16* pl = S.Pl + (int64_t)l * kSwBB;
+  _Float16* ph = S.Ph[kb & 1] + (int64_t)l * kSwBB;
+  _Float16* pl = S.Pl[kb & 1] + (int64_t)l * kSwBB;
   for (int r = tid >> 8; r < kSwB; r += 4) {
     const float v = r >= c ? pv_blk(lf, r >> 5, c >> 5)[(r & 31) * kPvL + (c & 31)]
                            : pv_blk(lf, c >> 5, r >> 5)[(c & 31) * kPvL + (r & 31)];
@@ -623,7 +705,7 @@ __global__ __launch_bounds__(512) void sw_prepw_kernel(float* __restrict__ Aall,
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
-  sx_gemm(S.Ch[k & 1] + oc, S.Cl[k & 1] + oc, S.Ph + op, S.Pl + op, kSwB, kSwB, lds, acc);
+  sx_gemm(S.Ch[k & 1] + oc, S.Cl[k & 1] + oc, S.Ph[k & 1] + op, S.Pl[k & 1] + op, kSwB, kSwB, lds, acc);
   const float inv = 1.0f / (S.c_scale(l, k, i) * S.psc[(int64_t)l * S.nt + k]);
   float wm = 0.f;
 #pragma unroll
@@ -934,13 +1016,16 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 // Lookahead schedules.  The side stream has the highest priority, so its workgroups are dispatched
 // ahead of U2's as CUs free.
 // (a) Few latent dims per GPU (L <= kSwFuseMaxL; latent-dim sharding): a pass is bound by its critical
-//     chain, which is shortened by letting the pivot apply pass k's update to its own block from pass k's
-//     planes (pv_pending_update) -- it then does not wait for U1(k):
-//       main:  wait ev_prep (prepW(k));  U1(k) (row / column k+1 without the pivot block: pass k+1's
-//              C planes);  record ev_c;  U2(k);  record ev_u2
-//       side:  wait ev_u2 (U2(k-1): the last writer of block k+1 up to pass k-1);  pivot(k+1);
-//              wait ev_c;  prepW(k+1);  record ev_prep
-//     chain per pass: max(pivot, U1) + prepW (was U1 + pivot + prepW).
+//     chain, so the side stream runs the pivots BACK TO BACK: pivot(m) applies pass m-1's update to its
+//     own block itself, computing the W block it needs from the previous pivot's P planes and the C
+//     planes (pv_pending_update), and waits only for U2(m-2), the last writer of its block up to pass
+//     m-2; prepW, U1 and U2 of pass m follow on the caller's stream once pivot(m) is done:
+//       side:  pivot(0);  [wait ev_u2(m-1) (ev_c = prep0 for m = 0);  pivot(m+1);  record ev_piv(m+1)]...
+//       main:  prep0;  record ev_c;  [wait ev_piv(m);  prepW(m);  U1(m) (row / column m+1 without the
+//              pivot block: pass m+1's C planes);  U2(m);  record ev_u2(m)]...
+//     chain per pass: the pivot alone (r3: 160 us at L = 2 with its 256 x 256 x 256 W block, against
+//     133 us pivot + 33 us prepW + ~20 us of launch gaps in r3's first form).  Events and P planes
+//     alternate by pass parity (pivot(m+1) runs beside pass m's prepW, which reads P planes m).
 // (b) Many latent dims (the headline L = 16): a pass is bound by total work; the chain runs whole on the
 //     side stream beside U2 (measured 0.3 ms per step faster than (a) at L = 16):
 //       main:  wait ev_prep;  U1(k) (row / column k+1 with the pivot block);  record ev_c;  U2(k)
@@ -949,14 +1034,15 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 // block k+1 of pass k+2's C planes, all in the plane set (k+1) & 1 (block k+1 of set k & 1 for the
 // latter, whose last readers, U1(k) and pivot(k+1), precede prepW(k+1)); the readers of set (k+1) & 1
 // from pass k-1 (U1 / U2(k-1), prepW(k-1), pivot(k)'s pending update) precede its writers on the main
-// or the side stream.  pivot(k+1) writes only its own block and the P planes (read by prepW(k+1)).
+// or the side stream.  pivot(k+1) writes its own block, its X scratch and the P planes of parity
+// (k+1) & 1, whose previous readers (prepW(k-1)) precede U2(k-1).
 // One stream + event set per (device, caller stream), created on first use; the map and every
 // enqueue sequence hold g_side_mu, so host threads sharing a caller stream cannot interleave their
 // records / waits, and callers on different streams never share a side stream.  (Disjoint CU masks
 // for the two streams were measured 2.6 ms per step slower: every masked queue slowed the rest.)
 struct SwSide {
   hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, prep = nullptr, c = nullptr, u2 = nullptr;
+  hipEvent_t fork = nullptr, prep = nullptr, c = nullptr, u2p[2] = {}, piv[2] = {};
 };
 
 static std::mutex g_side_mu;
@@ -970,7 +1056,7 @@ static int sw_side(hipStream_t caller, SwSide*& out) {  // g_side_mu held by the
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (hipStreamCreateWithPriority(&sd.s, hipStreamNonBlocking, greatest) != hipSuccess) return LVAE_ERR_LAUNCH;
-    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.c, &sd.u2})
+    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.c, &sd.u2p[0], &sd.u2p[1], &sd.piv[0], &sd.piv[1]})
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
   }
   out = &sd;
@@ -994,34 +1080,51 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
   if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
   sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
-  if (nt > 1) {
-    sw_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
-    sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, 0);
-  }
-  if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
   const bool fuse = L <= kSwFuseMaxL;
-  const int ntl1 = fuse ? nt - 2 : nt - 1;
-  for (int k = 0; k + 1 < nt; ++k) {
-    if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prepW(k)
-    if (ntl1 > 0) sw_update_kernel<kSwU1><<<ntl1 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl1, ntl1 * L);
-    if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;  // U1(k): the C planes of pass k+1
-    if (fuse) {
-      if (k > 0 && !ok(hipStreamWaitEvent(sd->s, sd->u2, 0))) return LVAE_ERR_LAUNCH;  // U2(k-1)
-      sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 1);
-      if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
-    } else {
+  if (fuse) {
+    if (!ok(hipEventRecord(sd->piv[0], sd->s))) return LVAE_ERR_LAUNCH;
+    if (nt > 1) sw_prep0_kernel<<<dim3(nt - 1, L), 256, 0, st>>>(A, np_, S);  // beside pivot(0)
+    if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
+    // schedule (a): the side stream runs the pivots back to back; the caller's stream runs each pass's
+    // prepW, U1, U2 once its pivot is done
+    for (int m = 0; m < nt; ++m) {
+      if (m + 1 < nt) {  // pivot(m+1): block m+1 current up to pass m-1 (U2(m-1); prep0 for m = 0)
+        if (!ok(hipStreamWaitEvent(sd->s, m == 0 ? sd->c : sd->u2p[(m - 1) & 1], 0))) return LVAE_ERR_LAUNCH;
+        sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1);
+        if (!ok(hipEventRecord(sd->piv[(m + 1) & 1], sd->s))) return LVAE_ERR_LAUNCH;
+      }
+      if (!ok(hipStreamWaitEvent(st, sd->piv[m & 1], 0))) return LVAE_ERR_LAUNCH;  // pivot(m)
+      if (nt > 1) sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, st>>>(A, S, np_, m);
+      if (m + 1 < nt) {
+        if (nt - 2 > 0) sw_update_kernel<kSwU1><<<(nt - 2) * L, 512, 0, st>>>(A, S, Kinv, np_, m, nt - 2, (nt - 2) * L);
+        if (ntl2 > 0) {
+          ProfScope ps(LVAE_PH_SWEEP_UPD, st);
+          sw_update_kernel<kSwU2><<<ntl2 * L, 512, 0, st>>>(A, S, Kinv, np_, m, ntl2, ntl2 * L);
+        }
+        if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
+      }
+    }
+  } else {
+    if (nt > 1) {
+      sw_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
+      sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, 0);
+    }
+    if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+    for (int k = 0; k + 1 < nt; ++k) {
+      if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // prepW(k)
+      sw_update_kernel<kSwU1><<<(nt - 1) * L, 512, 0, st>>>(A, S, Kinv, np_, k, nt - 1, (nt - 1) * L);
+      if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;  // U1(k): the C planes of pass k+1
       if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
       sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0);
+      sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, k + 1);
+      if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+      if (ntl2 > 0) {
+        ProfScope ps(LVAE_PH_SWEEP_UPD, st);
+        sw_update_kernel<kSwU2><<<ntl2 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl2, ntl2 * L);
+      }
     }
-    sw_prepw_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(A, S, np_, k + 1);
-    if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
-    if (ntl2 > 0) {
-      ProfScope ps(LVAE_PH_SWEEP_UPD, st);
-      sw_update_kernel<kSwU2><<<ntl2 * L, 512, 0, st>>>(A, S, Kinv, np_, k, ntl2, ntl2 * L);
-    }
-    if (fuse && !ok(hipEventRecord(sd->u2, st))) return LVAE_ERR_LAUNCH;
   }
-  if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // the whole side chain
+  if (!fuse && !ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // the whole side chain
   if (ntll > 0) sw_update_kernel<kSwLast><<<ntll * L, 512, 0, st>>>(A, S, Kinv, np_, nt - 1, ntll, ntll * L);
   sw_finish_kernel<<<dim3(4 * (2 * (nt - 1) + 1), L), 256, 0, st>>>(A, S, Kinv, np_, nt);
   LVAE_CHECK_LAUNCH();
