@@ -5,8 +5,8 @@
  * device memory inside, all work enqueued asynchronously on the caller's hipStream_t (passed as
  * void*), safe to call from several host threads.  Process-wide state is limited to (1) the
  * opt-in phase timer (lvae_prof_*) and (2) the sweep's side stream (lvae_spd_sweep_f32,
- * lvae_kl_closed_fwd_f32): one high-priority stream + three events (fork, prep, u1) per (device,
- * caller stream), created on first use, kept for the process lifetime, and guarded by a mutex held
+ * lvae_kl_closed_fwd_f32): one high-priority stream + seven events (fork, prep, c, and two pairs
+ * alternating by pass parity) per (device, caller stream), created on first use, kept for the process lifetime, and guarded by a mutex held
  * for each call's whole enqueue sequence.  The calls are graph-capturable (the side stream joins
  * the capture through the fork event and is joined back before the call returns).  Return value: 0 = ok, <0 = -(index of the bad argument),
  * LVAE_ERR_LAUNCH on a HIP launch error.  Numerical failure (a non-positive-definite pivot) is

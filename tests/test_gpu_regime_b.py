@@ -174,12 +174,14 @@ def test_gram_batched_semantics(hip):
     assert rel(got, raw.grad) < 1e-12
 
 
-@pytest.mark.parametrize("n,L", [(256, 3), (512, 2), (768, 2), (1280, 2), (4096, 1)])
+@pytest.mark.parametrize("n,L", [(256, 3), (512, 2), (768, 2), (1280, 2), (4096, 1), (256, 9), (512, 9), (768, 10),
+                                 (1280, 9)])
 def test_spd_sweep(hip, n, L):
     """Block symmetric sweep (the default Regime B inverse) vs fp64 torch: A^-1 (both triangles
-    written) and log|A|.  nt = n / 256 = 1, 2, 3, 5, 16 pivot blocks; the upper triangle of A is
-    garbage (never read) and A's scale is uneven (diagonal 0.5 .. 50) as the unit-diagonal pivot
-    scaling must handle."""
+    written) and log|A|.  nt = n / 256 = 1, 2, 3, 5, 16 pivot blocks, under both host schedules
+    (L <= 8: pivots back to back, each computing its own W block; L > 8: the whole chain on the side
+    stream); the upper triangle of A is garbage (never read) and A's scale is uneven (diagonal
+    0.5 .. 50) as the unit-diagonal pivot scaling must handle."""
     import lvae_amd as la
     gen = torch.Generator().manual_seed(n + L)
     Xm = torch.randn(L, n, n, generator=gen, dtype=torch.float64) / n ** 0.5
