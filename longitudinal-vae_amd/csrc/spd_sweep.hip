@@ -547,21 +547,31 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   __syncthreads();
   PV_T(22);
 
-  // 4. out: T = -P^-1 (both triangles) and the planes of P^-1 sP for prepW (a wave writes 256
-  //    consecutive elements of one row; the LDS reads are consecutive (lower part) or pitch-33
-  //    strided (mirror): conflict-free)
-  const int c = tid & 255;
+  // 4. out: T = -P^-1 (both triangles) and the planes of P^-1 sP for prepW: thread (r0 = tid >> 6,
+  //    c = 4 (tid & 63)) writes rows r0, r0 + 16, ... at columns c .. c+3 -- a wave writes one whole
+  //    row (1 KB of float4 + 2 x 512 B of half4 per instruction); the LDS reads are consecutive
+  //    (lower part) or pitch-33 strided (mirror)
+  const int c = 4 * (tid & 63);
   const float sP = x3_scale(__uint_as_float(pmax_s));
   _Float16* ph = S.Ph[kb & 1] + (int64_t)l * kSwBB;
   _Float16* pl = S.Pl[kb & 1] + (int64_t)l * kSwBB;
-  for (int r = tid >> 8; r < kSwB; r += 4) {
-    const float v = r >= c ? pv_blk(lf, r >> 5, c >> 5)[(r & 31) * kPvL + (c & 31)]
-                           : pv_blk(lf, c >> 5, r >> 5)[(c & 31) * kPvL + (r & 31)];
-    T[(int64_t)r * np_ + c] = -v;
-    const float y = v * sP;
-    const _Float16 yh = (_Float16)y;
-    ph[r * kSwB + c] = yh;
-    pl[r * kSwB + c] = (_Float16)(y - (float)yh);
+  for (int r = tid >> 6; r < kSwB; r += 16) {
+    f32x4 v, t;
+    x3_half4 h4, l4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cq = c + q;
+      v[q] = r >= cq ? pv_blk(lf, r >> 5, cq >> 5)[(r & 31) * kPvL + (cq & 31)]
+                     : pv_blk(lf, cq >> 5, r >> 5)[(cq & 31) * kPvL + (r & 31)];
+      t[q] = -v[q];
+      const float y = v[q] * sP;
+      const _Float16 yh = (_Float16)y;
+      h4[q] = yh;
+      l4[q] = (_Float16)(y - (float)yh);
+    }
+    *reinterpret_cast<f32x4*>(T + (int64_t)r * np_ + c) = t;
+    *reinterpret_cast<x3_half4*>(ph + r * kSwB + c) = h4;
+    *reinterpret_cast<x3_half4*>(pl + r * kSwB + c) = l4;
   }
   if (w == 0 && lane == 0) bad_s = bad;
   __syncthreads();
