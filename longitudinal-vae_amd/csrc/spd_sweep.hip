@@ -170,6 +170,53 @@ __device__ inline void pv_mma(pv_f32x16& acc, const float* X, const float* Y, in
   acc += t;
 }
 
+// acc += op(X) op(Y)^T as pv_mma, on the f16 matrix cores with the 3-product split: each operand is
+// scaled by its block's power of two (sX, sY: x3_scale of the block's max |x|), split x s = hi + lo on
+// the way from LDS, and the 32 x 32 x 32 product is 2 k-blocks x 3 v_mfma_f32_32x32x16_f16 (vs 16
+// v_mfma_f32_32x32x2f32: ~5x the MFMA rate) accumulated in a temporary and unscaled into acc.
+// The f16 32x32x16 accumulator layout is that of the 32x32x2 f32 MFMA (pv_row).
+template <bool TX, bool TY>
+__device__ inline void pv_mma3(pv_f32x16& acc, const float* X, const float* Y, float sX, float sY, int rl, int hh) {
+  pv_f32x16 t = {};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    x3_half8 aH, aL, bH, bL;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * hh + j;
+      const float a = (TX ? X[k * kPvL + rl] : X[rl * kPvL + k]) * sX;
+      const float b = (TY ? Y[k * kPvL + rl] : Y[rl * kPvL + k]) * sY;
+      const _Float16 ah = (_Float16)a, bh = (_Float16)b;
+      aH[j] = ah;
+      aL[j] = (_Float16)(a - (float)ah);
+      bH[j] = bh;
+      bL[j] = (_Float16)(b - (float)bh);
+    }
+    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH, t, 0, 0, 0);
+  }
+  acc += t * (1.0f / (sX * sY));
+}
+
+// bsc[n] = x3_scale(max |block n|) for the 36 lower blocks in LDS (wave w: blocks w, w + 16, w + 32),
+// then a barrier
+__device__ inline void pv_block_scales(const float* lf, float* bsc, int w, int lane, int rl, int hh) {
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = w + 16 * h;
+    if (n < kPvBlocks) {
+      float m = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) m = fmaxf(m, fabsf(lf[n * kPvBlk + pv_row(e, hh) * kPvL + rl]));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      if (lane == 0) bsc[n] = x3_scale(m);
+    }
+  }
+  __syncthreads();
+}
+
 // Rank-1 elimination steps inside MFMA accumulators.  A 32 x 32 block held as one accumulator
 // (lane (c, hh), element e: row (e&3) + 8 (e>>2) + 4 hh, column c) keeps row p in element e(p) of the
 // lanes of half h(p).  An outer product u v^T is then ONE v_mfma_f32_32x32x2f32 whose k-slot h(p)
@@ -414,6 +461,7 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
                                                         int pending) {
   __shared__ float lf[kPvBlocks * kPvBlk];
   __shared__ uint32_t pmax_s, xmax_s;
+  __shared__ float bsc[kPvBlocks];  // split scales of the L^-1 blocks (LAUUM on the f16 cores)
   __shared__ int bad_s;
   const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
@@ -490,23 +538,41 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   }
   __syncthreads();
   PV_T(24);
+  // levels 128 and 256 on the f16 cores (pv_mma3) with per-block split scales: all blocks' at the
+  // level start, the X blocks' from their accumulators as they are stored
 #pragma unroll 1
   for (int lv = 1; lv <= 2; ++lv) {
+    pv_block_scales(lf, bsc, w, lane, rl, hh);
     const int h = 1 << lv;                 // half width in blocks (2, 4)
     const int per = h * h;                 // blocks of B per instance
     const int inst = w / per, t = w % per;
     const bool act = inst < 4 / h;         // 2 instances of 128, 1 of 256
     const int o = 2 * h * inst;            // first block row / column of the instance
     const int i = o + h + t / h, j = o + t % h;
+    const int nij = i * (i + 1) / 2 + j;
     pv_f32x16 acc = {};
     if (act)  // X_ij = sum_{k=j}^{o+h-1} L_ik (A^-1)_kj
-      for (int k = j; k < o + h; ++k) pv_mma<false, true>(acc, pv_blk(lf, i, k), pv_blk(lf, k, j), rl, hh);
+      for (int k = j; k < o + h; ++k) {
+        const int a = i * (i + 1) / 2 + k, b = k * (k + 1) / 2 + j;
+        pv_mma3<false, true>(acc, lf + a * kPvBlk, lf + b * kPvBlk, bsc[a], bsc[b], rl, hh);
+      }
     __syncthreads();
-    if (act) pv_store(acc, pv_blk(lf, i, j), rl, hh);
+    if (act) {
+      pv_store(acc, pv_blk(lf, i, j), rl, hh);
+      float m = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) m = fmaxf(m, fabsf(acc[e]));
+#pragma unroll
+      for (int q = 32; q > 0; q >>= 1) m = fmaxf(m, __shfl_xor(m, q, 64));
+      if (lane == 0) bsc[nij] = x3_scale(m);
+    }
     __syncthreads();
     acc = pv_f32x16{};
     if (act)  // Y_ij = sum_{k=o+h}^{i} (C^-1)_ik X_kj
-      for (int k = o + h; k <= i; ++k) pv_mma<false, true>(acc, pv_blk(lf, i, k), pv_blk(lf, k, j), rl, hh);
+      for (int k = o + h; k <= i; ++k) {
+        const int a = i * (i + 1) / 2 + k, b = k * (k + 1) / 2 + j;
+        pv_mma3<false, true>(acc, lf + a * kPvBlk, lf + b * kPvBlk, bsc[a], bsc[b], rl, hh);
+      }
     __syncthreads();
     if (act) pv_store(acc, pv_blk(lf, i, j), rl, hh, -1.f);
     __syncthreads();
@@ -514,7 +580,9 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   PV_T(21);
 
   // 3. P^-1 = L^-T L^-1: block n = i (i + 1) / 2 + j costs 8 - i products; longest-processing-time
-  //    assignment, 7-8 products per wave, 30 per SIMD
+  //    assignment, 7-8 products per wave, 30 per SIMD; the products on the f16 cores (pv_mma3) with
+  //    per-block split scales of L^-1 (bsc)
+  pv_block_scales(lf, bsc, w, lane, rl, hh);
   pv_f32x16 res[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
@@ -524,7 +592,10 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
       while ((i + 1) * (i + 2) / 2 <= n) ++i;
       const int j = n - i * (i + 1) / 2;
       res[h] = pv_f32x16{};
-      for (int k = i; k < 8; ++k) pv_mma<true, true>(res[h], pv_blk(lf, k, i), pv_blk(lf, k, j), rl, hh);
+      for (int k = i; k < 8; ++k) {
+        const int bi = k * (k + 1) / 2 + i, bj = k * (k + 1) / 2 + j;
+        pv_mma3<true, true>(res[h], lf + bi * kPvBlk, lf + bj * kPvBlk, bsc[bi], bsc[bj], rl, hh);
+      }
     }
   }
   {  // max |P^-1| before the planes are written (their split scale)
