@@ -49,7 +49,7 @@ constexpr int kSwT = 128;  // sub-tile of the finish copies
 constexpr int kSwBB = kSwB * kSwB;
 
 struct SwScratch {
-  _Float16 *Wh[2], *Wl[2], *Ch[2], *Cl[2];  // [L][np][256], by pass parity (prep(k+1) runs beside U2(k))
+  _Float16 *Wh[2], *Wl[2], *Ch[2], *Cl[2];  // [L][np][256], by pass parity (pass k+1's chain runs beside U2(k))
   _Float16 *Ph[2], *Pl[2];                   // [L][256][256] planes of P^-1 sP, by pass parity
   _Float16 *Xh, *Xl;                         // [L][256][256] the pivot's own W block (schedule (a))
   float* csc;                   // [L][nt][nt] split scale of block i of the C operand of pass k
@@ -98,10 +98,12 @@ __device__ inline float sw_block_max(float v, uint32_t* red) {
 }
 
 // ------------------------------------------------------------------------------------------
-// pivot: T = A_kk (lower triangle read) -> T = -P^-1 (full), Pinv = P^-1, log|P|, info, split bounds.
+// pivot: T = A_kk (lower triangle read) -> T = -P^-1 (full), the planes of P^-1, log|P|, info, its split scale.
 // One 1024-thread workgroup per dim; the 36 lower 32 x 32 blocks of P live in LDS (pitch 33, 152 KB)
-// for the whole kernel and every block operation is a chain of 16 v_mfma_f32_32x32x2f32 reading its
-// operands straight from LDS (fp32 products and sums: the accuracy of LAPACK spotrf + spotri):
+// for the whole kernel and every block operation reads its operands straight from LDS: the Cholesky
+// as chains of v_mfma_f32_32x32x2f32 (fp32 products and sums: the accuracy of LAPACK spotrf), the
+// L^-1 levels of 128 / 256 rows and L^-T L^-1 as x3-split f16 MFMA products with per-block scales
+// (pv_mma3, fp32-equivalent):
 //   1. blocked right-looking Cholesky P = L L^T, 8 panels q:
 //        diagonal block: one wave factors it in registers and inverts its factor (pv_diag), the
 //                        diagonal slot then holds L_qq^-1;
@@ -109,11 +111,9 @@ __device__ inline float sw_block_max(float v, uint32_t* red) {
 //        trailing:       A_ij -= L_iq L_jq^T, q < j <= i             (all waves; wave 0 takes
 //                        (q+1, q+1) first and factors it right away: the next diagonal factor
 //                        overlaps the rest of the trailing update)
-//   2. L^-1 in place, block row by block row: (L^-1)_ij = -L_ii^-1 sum_{k=j}^{i-1} L_ik (L^-1)_kj
-//      (the outer product by L_ii^-1 takes the inner sum straight from the accumulator registers as
-//      the B operand, with the K index permuted to the accumulator layout)
+//   2. L^-1 in place by recursive doubling over levels of 64, 128, 256 rows (see the code)
 //   3. P^-1 = L^-T L^-1, all 36 lower blocks at once (sum_{k >= i} (L^-1)_ki^T (L^-1)_kj), written
-//      back after one barrier, then streamed out (both triangles, coalesced) with the split bounds.
+//      back after one barrier, then streamed out (both triangles, coalesced) with its split scale.
 // The Cholesky form (rather than an explicit-inverse block sweep) keeps the block updates backward
 // stable: a 32-wide explicit-inverse update loses cond(P_qq) digits (measured 20x larger K^-1 error).
 // ------------------------------------------------------------------------------------------
