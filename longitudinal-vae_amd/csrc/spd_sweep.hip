@@ -199,6 +199,53 @@ __device__ inline void pv_mma3(pv_f32x16& acc, const float* X, const float* Y, f
   acc += t * (1.0f / (sX * sY));
 }
 
+// As pv_mma3 on blocks already split IN PLACE (pv_pack_blocks: each fp32 word replaced by the packed
+// fp16 pair (hi | lo << 16) of x s): a fragment is 8 LDS words regrouped by v_perm_b32 into its hi and
+// lo halves (1 VALU per element instead of 5).
+typedef unsigned int pv_u32x4 __attribute__((ext_vector_type(4)));
+template <bool TX, bool TY>
+__device__ inline void pv_mma3p(pv_f32x16& acc, const float* X, const float* Y, float sX, float sY, int rl, int hh) {
+  pv_f32x16 t = {};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    unsigned wa[8], wb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * hh + j;
+      wa[j] = __float_as_uint(TX ? X[k * kPvL + rl] : X[rl * kPvL + k]);
+      wb[j] = __float_as_uint(TY ? Y[k * kPvL + rl] : Y[rl * kPvL + k]);
+    }
+    pv_u32x4 ah, al, bh, bl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ah[q] = __builtin_amdgcn_perm(wa[2 * q + 1], wa[2 * q], 0x05040100u);
+      al[q] = __builtin_amdgcn_perm(wa[2 * q + 1], wa[2 * q], 0x07060302u);
+      bh[q] = __builtin_amdgcn_perm(wb[2 * q + 1], wb[2 * q], 0x05040100u);
+      bl[q] = __builtin_amdgcn_perm(wb[2 * q + 1], wb[2 * q], 0x07060302u);
+    }
+    const x3_half8 aH = __builtin_bit_cast(x3_half8, ah), aL = __builtin_bit_cast(x3_half8, al);
+    const x3_half8 bH = __builtin_bit_cast(x3_half8, bh), bL = __builtin_bit_cast(x3_half8, bl);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH, t, 0, 0, 0);
+  }
+  acc += t * (1.0f / (sX * sY));
+}
+
+// every element of the 36 LDS blocks x -> the packed fp16 pair (hi | lo << 16) of x bsc[block], then a
+// barrier (the blocks are read only through pv_mma3p afterwards, until overwritten)
+__device__ inline void pv_pack_blocks(float* lf, const float* bsc) {
+  for (int e = threadIdx.x; e < kPvBlocks * 1024; e += 1024) {
+    const int n = e >> 10, r = (e >> 5) & 31, c = e & 31;
+    float* p = lf + n * kPvBlk + r * kPvL + c;
+    const float y = *p * bsc[n];
+    const _Float16 h = (_Float16)y, lo = (_Float16)(y - (float)h);
+    *p = __uint_as_float((unsigned)__builtin_bit_cast(unsigned short, h) |
+                         ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16));
+  }
+  __syncthreads();
+}
+
 // bsc[n] = x3_scale(max |block n|) for the 36 lower blocks in LDS (wave w: blocks w, w + 16, w + 32),
 // then a barrier
 __device__ inline void pv_block_scales(const float* lf, float* bsc, int w, int lane, int rl, int hh) {
@@ -583,6 +630,7 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
   //    assignment, 7-8 products per wave, 30 per SIMD; the products on the f16 cores (pv_mma3) with
   //    per-block split scales of L^-1 (bsc)
   pv_block_scales(lf, bsc, w, lane, rl, hh);
+  pv_pack_blocks(lf, bsc);
   pv_f32x16 res[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
@@ -594,7 +642,7 @@ __global__ __launch_bounds__(1024) void sw_pivot_kernel(float* __restrict__ Aall
       res[h] = pv_f32x16{};
       for (int k = i; k < 8; ++k) {
         const int bi = k * (k + 1) / 2 + i, bj = k * (k + 1) / 2 + j;
-        pv_mma3<true, true>(res[h], lf + bi * kPvBlk, lf + bj * kPvBlk, bsc[bi], bsc[bj], rl, hh);
+        pv_mma3p<true, true>(res[h], lf + bi * kPvBlk, lf + bj * kPvBlk, bsc[bi], bsc[bj], rl, hh);
       }
     }
   }
