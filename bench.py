@@ -44,7 +44,7 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2s_pmc_summary.json")
 U2_NAME = "sw_update_kernel<0,2>"       # the sweep's interior rank-256 update U2 (spd_sweep.hip, MODE kSwU2)
 
 

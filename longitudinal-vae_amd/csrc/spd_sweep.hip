@@ -1152,8 +1152,8 @@ __global__ __launch_bounds__(256) void sw_finish_kernel(const float* __restrict_
 //       side:  pivot(0);  [wait ev_u2(m-1) (ev_c = prep0 for m = 0);  pivot(m+1);  record ev_piv(m+1)]...
 //       main:  prep0;  record ev_c;  [wait ev_piv(m);  prepW(m);  U1(m) (row / column m+1 without the
 //              pivot block: pass m+1's C planes);  U2(m);  record ev_u2(m)]...
-//     chain per pass: the pivot alone (r3: 160 us at L = 2 with its 256 x 256 x 256 W block, against
-//     133 us pivot + 33 us prepW + ~20 us of launch gaps in r3's first form).  Events and P planes
+//     chain per pass: the pivot alone (r2s: 160 us at L = 2 with its 256 x 256 x 256 W block, against
+//     133 us pivot + 33 us prepW + ~20 us of launch gaps in r2s's first form).  Events and P planes
 //     alternate by pass parity (pivot(m+1) runs beside pass m's prepW, which reads P planes m).
 // (b) Many latent dims (the headline L = 16): a pass is bound by total work; the chain runs whole on the
 //     side stream beside U2 (measured 0.3 ms per step faster than (a) at L = 16):

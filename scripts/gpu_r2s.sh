@@ -1,8 +1,8 @@
 #!/bin/bash
-# r3 GPU pass: full -m gpu suite, default bench (+ rocprof of the closed step), an L = 2 closed-step
+# r2s GPU pass: full -m gpu suite, default bench (+ rocprof of the closed step), an L = 2 closed-step
 # bench (the per-rank load of the 8-GPU latent-sharded step), and the 2-rank gloo rehearsal.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-OUT=gpurun_out; mkdir -p $OUT; TAG=${TAG:-r3}
+OUT=gpurun_out; mkdir -p $OUT; TAG=${TAG:-r2s}
 stage() { echo "[$(date +%T)] $*"; }
 if [ "${TESTS:-1}" = "1" ]; then
   stage pytest
