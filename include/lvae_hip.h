@@ -18,8 +18,8 @@
  *   covar_module(x1, x2).evaluate()       -> lvae_gram_*            (GP_model.py:31-144,
  *                                             kernel_gen.py:9-310, call sites elbo_functions.py:22,56,171-174)
  *   autograd of that Gram wrt (scale, lengthscale) -> lvae_gram_bwd_*
- *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_spd_sweep_f32
- *                                             (elbo_functions.py:26-29)
+ *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_spd_inv_chol_f32 (also
+ *                                             lvae_spd_sweep_f32; elbo_functions.py:26-29)
  *   KL_closed forward + autograd backward -> lvae_kl_closed_fwd_f32 / _bwd_f32 (elbo_functions.py:8-34)
  *   batched small fp64 factor + inverse   -> lvae_spd_inv_small_f64 (elbo_functions.py:176-186,
  *                                             training.py:130-134)
@@ -120,15 +120,18 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
                            void* stream);
 /* The same forward in two calls, for callers that overlap the factorisation with the work that
  * produces (mu, logv) (the encoder): _factor_f32 needs only the covariates and hyperparameters
- * (Gram + the sweep: K^-1, log|K|, info into the workspace); _reduce_f32 then takes mu / logv
- * (alpha = K^-1 mu, the trace and quadratic terms, kl, and with need_bwd the S-GEMM operand).
- * factor then reduce on one stream (or with the reduce stream waiting on the factor's) equals
+ * (Gram + the blocked Cholesky inverse: K^-1, log|K|, info into the workspace); _reduce_f32 then
+ * takes mu / logv (alpha = K^-1 mu with one fp64 refinement step -- the residual mu - K alpha0 is
+ * evaluated from the covariates in fp64, hence spec / x / params / noise again, the same as the
+ * factor's -- the trace and quadratic terms, kl, and with need_bwd the S-GEMM operand).  factor then
+ * reduce on one stream (or with the reduce stream waiting on the factor's) equals
  * lvae_kl_closed_fwd_f32.                                                                        */
 int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
                               const double* params, const double* noise, int32_t* info, void* workspace,
                               void* stream);
-int lvae_kl_closed_reduce_f32(int n, int L, const double* mu, const double* logv, int ld_mu, double* kl,
-                              void* workspace, int need_bwd, void* stream);
+int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                              const double* params, const double* noise, const double* mu, const double* logv,
+                              int ld_mu, double* kl, void* workspace, int need_bwd, void* stream);
 
 /* Backward of lvae_kl_closed_fwd_f32 given dL/dkl[l] = gkl[l]:
  *   dmu[i,l] = gkl_l (K^-1 mu)_i,  dlogv[i,l] = gkl_l/2 (v_i (K^-1)_ii - 1),
@@ -153,6 +156,19 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
 size_t lvae_spd_sweep_scratch_size(int np_, int L);
 int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
                        void* stream);
+
+/* A^-1 and log|A| of L padded SPD matrices by a blocked Cholesky factorisation, triangular inverse
+ * and product (LAPACK potrf + trtri + lauum, 256-wide blocks; the inverse lvae_kl_closed_* use):
+ * potrf's pivot blocks factored and inverted in LDS (fp32 MFMA), its panel / rank-256 trailing
+ * updates and trtri / lauum's whole-block GEMMs on the f16 cores with the 3-product split; the next
+ * pivot runs on a side stream beside each trailing update.  Same arguments and outputs as
+ * lvae_spd_sweep_f32 (A overwritten, Ainv full symmetric, info LAPACK-style); scratch:
+ * lvae_spd_inv_chol_scratch_size(np, L) bytes, 256-B aligned.  Backward-stable in the Cholesky sense:
+ * |I - A Ainv| ~ cond(A) 2^-24, against ~100x that for the sweep at cond 1e5.
+ * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).         */
+size_t lvae_spd_inv_chol_scratch_size(int np_, int L);
+int lvae_spd_inv_chol_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
+                          void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Regime A: Hensman SVI, fp64 (elbo_functions.py:144-216; training.py:129-135)             */
@@ -280,9 +296,9 @@ int lvae_predict_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec
 /* the number of bracketed intervals into count[phase], and forgets them.                  */
 /* ---------------------------------------------------------------------------------------- */
 enum lvae_phase {
-  LVAE_PH_GRAM = 0, LVAE_PH_POTRF = 1 /* the whole inverse (sweep) */, LVAE_PH_POTRI = 2 /* unused */, LVAE_PH_KL_REDUCE = 3, LVAE_PH_SYRK = 4,
+  LVAE_PH_GRAM = 0, LVAE_PH_POTRF = 1 /* potrf (or the whole sweep) */, LVAE_PH_POTRI = 2 /* trtri + lauum */, LVAE_PH_KL_REDUCE = 3, LVAE_PH_SYRK = 4,
   LVAE_PH_GRAM_BWD = 5, LVAE_PH_BWD_ELEM = 6, LVAE_PH_HENSMAN_FWD = 7, LVAE_PH_HENSMAN_BWD = 8,
-  LVAE_PH_NATGRAD = 9, LVAE_PH_SWEEP_UPD = 10 /* the sweep's U2 launches, nested in POTRF */, LVAE_N_PHASES = 11
+  LVAE_PH_NATGRAD = 9, LVAE_PH_SWEEP_UPD = 10 /* the trailing rank-256 update launches (U2), nested in POTRF */, LVAE_N_PHASES = 11
 };
 int lvae_prof_enable(int on);
 int lvae_prof_collect(double* ms, int32_t* count, int n_phases);

@@ -1,0 +1,836 @@
+// chol_inv.hip -- K^-1 and log|K| of L batched SPD np x np fp32 covariances by a blocked Cholesky
+// factorisation, a blocked triangular inverse and their product (LAPACK potrf + trtri + lauum), the
+// Regime B inverse of the exact KL: torch.cholesky(K1), cholesky_solve(I, LK1) and the log-det of
+// elbo_functions.py:26-29.  256-wide blocks, every GEMM on the f16 matrix cores with the fp32-accurate
+// 3-product split (mfma_x3.hpp / x3_dma.hpp: x s = hi + lo per operand block, a power-of-two split
+// scale s = x3_scale(max |block|) per 256 x 256 block from the block's exact max, taken by the kernel
+// that writes the block).
+//
+// Why Cholesky and not the block sweep (spd_sweep.hip): the sweep (Gauss-Jordan on SPD) updates the
+// already inverted part in every pass, and its K^-1 error grows ~100x faster with cond(K) (emulated
+// in fp32 at N = 1024, cond 1.3e5: |I - K X|_2 = 2.7 against 0.03 here).  Same n^3 flops.
+//
+//   1. potrf, right-looking, one pass per block column k (all L dims in every launch):
+//        pivot(k)  A_kk -> L_kk (blocked Cholesky in LDS on fp32 MFMA, pv_lds.hpp), log|A_kk|, info,
+//                  and Y_kk = L_kk^-1 (recursive doubling) as fp16 planes: row-major into D (the panel's
+//                  operand) and transposed into tile (k, k) of the Y^T planes
+//        panel(k)  L_ik = A_ik Y_kk^T for i > k, from the planes of the updated column (C) -> the
+//                  planes of L (tile (i, k)), one 256 x 256 x3 tile GEMM per block
+//        U1(k)     column k+1: A_I,k+1 -= L_Ik L_k+1,k^T, written straight as the planes of pass k+1's
+//                  C operand (+ the next pivot block in fp32 when the pivot does not update it itself)
+//        U2(k)     the trailing tiles I >= J >= k+2: A_IJ -= L_Ik L_Jk^T, in place (HBM-streaming rank-256
+//                  update, A read and written under the MFMAs as in the sweep)
+//      with lookahead: the next pivot (+ panel) runs on the side stream beside U2 (schedules below).
+//   2. trtri, Y = L^-1 by recursive doubling over levels of h = 1, 2, 4, ... blocks: for every aligned
+//      pair of inverted diagonal groups [A 0; B C] (A = rows [o, o+h), C = [o+h, o+2h)), B <- -C^-1 B A^-1:
+//        X_ij = sum_{k=j}^{o+h-1} L_ik Y_kj,   Y_ij = -sum_{k=o+h}^{i} Y_ik X_kj    (ci_gemm_kernel)
+//      two launches per level, every GEMM K-deep over whole blocks (MFMA-bound, not HBM-bound)
+//   3. lauum, K^-1 = Y^T Y: (K^-1)_IJ = sum_{k >= I} Y_kI^T Y_kJ for I >= J, written with its mirror.
+//
+// GEMM operands are pre-split fp16 planes [row][k] (x3_dma.hpp's NT form: both operands k-contiguous),
+// so Y is kept in both orientations: Y planes (row-major, the A operand of the Y step) and Y^T planes
+// (the B operand of the X step and both operands of lauum); X is written transposed.  A K range that
+// crosses blocks changes the operand scales: the accumulators are rescaled by the (power-of-two) ratio
+// at each block boundary (exact).
+//
+// Buffers (ci_inverse): A [L, np, np] fp32 (lower tiles read; dead after potrf, then reused as the Y
+// planes), YT [L, np, np] x 2 halves (Y^T planes; caller-provided), Kinv [L, np, np] fp32 out (reused as
+// the X^T planes during trtri), scratch (CiScratch): C planes 2 x [L, np, 256] by pass parity, the
+// pivot's X block, D [L, nt, 256, 256], the L planes [L, np, np] and the per-tile scales.
+#include "prof.hpp"
+#include "pv_lds.hpp"
+#include "side_stream.hpp"
+
+namespace lvae {
+
+struct CiScratch {
+  _Float16 *Ch[2], *Cl[2];  // [L][np][256] planes of the updated column (pass k's C operand), by parity
+  _Float16 *Xh, *Xl;        // [L][256][256] the pivot's own L_{k,k-1} block (schedule (a))
+  _Float16 *Dh, *Dl;        // [L][nt][256][256] planes of Y_kk = L_kk^-1 (row-major)
+  _Float16 *Lh, *Ll;        // [L][np][np] planes of L (off-diagonal lower tiles)
+  float* csc;               // [L][nt][nt] (l, k, i): block i of pass k's C operand
+  float* lsc;               // [L][nt][nt] (l, i, k): tile (i, k) of L
+  float* ysc;               // [L][nt][nt] (l, i, j): tile (i, j) of Y (both plane orientations; D for i == j)
+  float* xsc;               // [L][nt][nt] (l, i, j): tile (i, j) of the trtri intermediate X
+  int nt;
+  size_t bytes;
+  CiScratch(char* base, int np_, int L) {
+    size_t off = 0;
+    auto take = [&](size_t b) {
+      char* p = base ? base + off : nullptr;
+      off += align256(b);
+      return p;
+    };
+    nt = np_ / kSwB;
+    const size_t col = (size_t)L * np_ * kSwB;
+    for (int b = 0; b < 2; ++b) {
+      Ch[b] = (_Float16*)take(col * 2);
+      Cl[b] = (_Float16*)take(col * 2);
+    }
+    Xh = (_Float16*)take((size_t)L * kSwBB * 2);
+    Xl = (_Float16*)take((size_t)L * kSwBB * 2);
+    Dh = (_Float16*)take(col * 2);
+    Dl = (_Float16*)take(col * 2);
+    const size_t full = (size_t)L * np_ * np_;
+    Lh = (_Float16*)take(full * 2);
+    Ll = (_Float16*)take(full * 2);
+    csc = (float*)take((size_t)L * nt * nt * 4);
+    lsc = (float*)take((size_t)L * nt * nt * 4);
+    ysc = (float*)take((size_t)L * nt * nt * 4);
+    xsc = (float*)take((size_t)L * nt * nt * 4);
+    bytes = off;
+  }
+  __device__ float& c_scale(int l, int k, int i) const { return csc[((int64_t)l * nt + k) * nt + i]; }
+  __device__ float& t_scale(float* s, int l, int i, int j) const { return s[((int64_t)l * nt + i) * nt + j]; }
+};
+
+// ------------------------------------------------------------------------------------------
+// pivot(kb): A_kk (lower triangle) -> L_kk in LDS -> Y_kk = L_kk^-1; out: Y_kk planes (D, row-major; Y^T
+// tile (kb, kb), transposed) with the split scale of max |Y_kk|, log|A_kk|, info.  One 1024-thread
+// workgroup per dim.  With `pending` (schedule (a), kb > 0) the block still lacks pass kb-1's update,
+// applied here: X = L_{kb,kb-1} = C_kb Y_{kb-1}^T (C planes of pass kb-1, block kb; D of kb-1), split
+// at its exact max into Xh / Xl, then A_kk - X X^T.
+// ------------------------------------------------------------------------------------------
+__device__ inline void ci_pending_update(const float* __restrict__ T, int64_t np_, const CiScratch& S, int l, int kb,
+                                         float* __restrict__ lf, uint32_t* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int kp = kb - 1;
+  const int64_t oc = (int64_t)l * np_ * kSwB + (int64_t)kb * kSwBB, od = ((int64_t)l * S.nt + kp) * kSwBB;
+  const int64_t ox = (int64_t)l * kSwBB;
+  float sxo;
+  {
+    const _Float16* src[4] = {S.Ch[kp & 1] + oc, S.Cl[kp & 1] + oc, S.Dh + od, S.Dl + od};
+    int bi[4], bj[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) bi[h] = (4 * w + h) >> 3, bj[h] = (4 * w + h) & 7;
+    pv_f32x16 x[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) x[h] = pv_f32x16{};
+    pv_x3_gemm<4, false>(src, lf, bi, bj, x);
+    const float inv = 1.0f / (S.c_scale(l, kp, kb) * S.ysc[((int64_t)l * S.nt + kp) * S.nt + kp]);
+    float m = 0.f;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        x[h][e] *= inv;
+        m = fmaxf(m, fabsf(x[h][e]));
+      }
+    const float sx = x3_scale(sw_block_max(m, red));
+    _Float16* xh = S.Xh + ox;
+    _Float16* xl = S.Xl + ox;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = 32 * bi[h] + pv_row(e, hh), c = 32 * bj[h] + rl;
+        const float y = x[h][e] * sx;
+        const _Float16 yh = (_Float16)y;
+        xh[r * kSwB + c] = yh;
+        xl[r * kSwB + c] = (_Float16)(y - (float)yh);
+      }
+    sxo = sx;
+    __syncthreads();  // the X planes are visible to the workgroup
+  }
+  const float sx = sxo;
+  const _Float16* src[4] = {S.Xh + ox, S.Xl + ox, S.Xh + ox, S.Xl + ox};
+  int bi[3], bj[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n < 0) {
+      bi[h] = bj[h] = -1;
+    } else {
+      pv_ij(n, bi[h], bj[h]);
+    }
+  }
+  pv_f32x16 acc[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
+  pv_x3_gemm<3, true>(src, lf, bi, bj, acc);
+  const float inv = 1.0f / (sx * sx);
+  float old[3][16];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    if (bi[h] < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) old[h][e] = T[(int64_t)(32 * bi[h] + pv_row(e, hh)) * np_ + 32 * bj[h] + rl];
+  }
+  __syncthreads();  // every wave's last staging read
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) lf[n * kPvBlk + pv_row(e, hh) * kPvL + rl] = old[h][e] - acc[h][e] * inv;
+  }
+}
+
+__global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict__ Aall, int np_, int kb, CiScratch S,
+                                                        _Float16* __restrict__ YTh, _Float16* __restrict__ YTl,
+                                                        double* __restrict__ logdet, int32_t* __restrict__ info,
+                                                        int pending) {
+  __shared__ float lf[kPvBlocks * kPvBlk];
+  __shared__ uint32_t ymax_s, xmax_s;
+  __shared__ float bsc[kPvBlocks];
+  __shared__ int bad_s;
+  const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
+  if (tid == 0) {
+    bad_s = INT_MAX;
+    ymax_s = 0u;
+    xmax_s = 0u;
+  }
+  if (pending) {
+    __syncthreads();  // xmax_s
+    ci_pending_update(T, np_, S, l, kb, lf, &xmax_s);
+  } else {
+    const int r = tid >> 5, c = tid & 31;
+    float v[kPvBlocks];
+#pragma unroll
+    for (int R = 0, b = 0; R < 8; ++R)
+#pragma unroll
+      for (int C = 0; C <= R; ++C, ++b) v[b] = T[(int64_t)(32 * R + r) * np_ + 32 * C + c];
+#pragma unroll
+    for (int b = 0; b < kPvBlocks; ++b) lf[b * kPvBlk + r * kPvL + c] = v[b];
+  }
+  __syncthreads();
+  double ld = 0.0;
+  int bad = INT_MAX;
+
+  // 1. Cholesky A_kk = L L^T, panel by panel, then the trailing update A_ij -= L_iq L_jq^T
+  for (int q = 0; q < 8; ++q) {
+    if (w <= 7 - q) {
+      pv_panel(lf, q, w, lane, ld, bad);
+    } else {
+      __syncthreads();  // pv_panel's barrier
+    }
+    __syncthreads();
+    const int m = 7 - q, nb = m * (m + 1) / 2;
+    for (int t = w; t < nb; t += 16) {
+      int jj = 0, u = t;
+      while (u >= m - jj) {
+        u -= m - jj;
+        ++jj;
+      }
+      const int j = q + 1 + jj, i = j + u;
+      pv_f32x16 acc;
+      float* Bij = pv_blk(lf, i, j);
+      pv_load(acc, Bij, rl, hh);
+      pv_mma<false, false>(acc, pv_blk(lf, i, q), pv_blk(lf, j, q), rl, hh, -1.f);
+      pv_store(acc, Bij, rl, hh);
+    }
+    __syncthreads();
+  }
+  if (w < 8) pv_trinv(pv_blk(lf, w, w), lane);
+  __syncthreads();
+
+  // 2. L^-1 in place by recursive doubling (levels of 64, 128, 256 rows; see spd_sweep.hip's pivot)
+  if (w < 4) {
+    const int a = 2 * w;
+    pv_f32x16 X = {}, Y = {};
+    pv_mma<false, true>(X, pv_blk(lf, a + 1, a), pv_blk(lf, a, a), rl, hh);
+    const float* Ci = pv_blk(lf, a + 1, a + 1);
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      Y = __builtin_amdgcn_mfma_f32_32x32x2f32(Ci[rl * kPvL + pv_row(s, hh)], X[s], Y, 0, 0, 0);
+    pv_store(Y, pv_blk(lf, a + 1, a), rl, hh, -1.f);
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int lv = 1; lv <= 2; ++lv) {
+    pv_block_scales(lf, bsc, w, lane, rl, hh);
+    const int h = 1 << lv;
+    const int per = h * h;
+    const int inst = w / per, t = w % per;
+    const bool act = inst < 4 / h;
+    const int o = 2 * h * inst;
+    const int i = o + h + t / h, j = o + t % h;
+    const int nij = i * (i + 1) / 2 + j;
+    pv_f32x16 acc = {};
+    if (act)
+      for (int k = j; k < o + h; ++k) {
+        const int a = i * (i + 1) / 2 + k, b = k * (k + 1) / 2 + j;
+        pv_mma3<false, true>(acc, lf + a * kPvBlk, lf + b * kPvBlk, bsc[a], bsc[b], rl, hh);
+      }
+    __syncthreads();
+    if (act) {
+      pv_store(acc, pv_blk(lf, i, j), rl, hh);
+      float m = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) m = fmaxf(m, fabsf(acc[e]));
+#pragma unroll
+      for (int q = 32; q > 0; q >>= 1) m = fmaxf(m, __shfl_xor(m, q, 64));
+      if (lane == 0) bsc[nij] = x3_scale(m);
+    }
+    __syncthreads();
+    acc = pv_f32x16{};
+    if (act)
+      for (int k = o + h; k <= i; ++k) {
+        const int a = i * (i + 1) / 2 + k, b = k * (k + 1) / 2 + j;
+        pv_mma3<false, true>(acc, lf + a * kPvBlk, lf + b * kPvBlk, bsc[a], bsc[b], rl, hh);
+      }
+    __syncthreads();
+    if (act) pv_store(acc, pv_blk(lf, i, j), rl, hh, -1.f);
+    __syncthreads();
+  }
+
+  // 3. max |Y_kk| -> its split scale; out: D (row-major planes) and the transposed planes into tile
+  //    (kb, kb) of Y^T.  Thread (r0 = tid >> 6, c = 4 (tid & 63)) covers rows r0, r0 + 16, ... (a wave
+  //    writes one whole row of each: half4 runs).
+  {
+    float m = 0.f;
+    for (int e = tid; e < kPvBlocks * 1024; e += 1024) {
+      const int n = e >> 10, r = (e >> 5) & 31, c = e & 31;
+      m = fmaxf(m, fabsf(lf[n * kPvBlk + r * kPvL + c]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) atomicMax(&ymax_s, __float_as_uint(m));
+  }
+  __syncthreads();
+  const float sY = x3_scale(__uint_as_float(ymax_s));
+  const int c = 4 * (tid & 63);
+  const int64_t od = ((int64_t)l * S.nt + kb) * kSwBB;
+  const int64_t np2 = (int64_t)np_ * np_;
+  _Float16* dh = S.Dh + od;
+  _Float16* dl = S.Dl + od;
+  _Float16* th = YTh + l * np2 + (int64_t)kb * kSwB * np_ + kb * kSwB;
+  _Float16* tl = YTl + l * np2 + (int64_t)kb * kSwB * np_ + kb * kSwB;
+  for (int r = tid >> 6; r < kSwB; r += 16) {
+    x3_half4 h4, l4, ht4, lt4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cq = c + q;
+      const float v = r >= cq ? pv_blk(lf, r >> 5, cq >> 5)[(r & 31) * kPvL + (cq & 31)] : 0.f;       // Y(r, cq)
+      const float vt = cq >= r ? pv_blk(lf, cq >> 5, r >> 5)[(cq & 31) * kPvL + (r & 31)] : 0.f;      // Y(cq, r)
+      const float y = v * sY, yt = vt * sY;
+      const _Float16 yh = (_Float16)y, yth = (_Float16)yt;
+      h4[q] = yh;
+      l4[q] = (_Float16)(y - (float)yh);
+      ht4[q] = yth;
+      lt4[q] = (_Float16)(yt - (float)yth);
+    }
+    *reinterpret_cast<x3_half4*>(dh + r * kSwB + c) = h4;
+    *reinterpret_cast<x3_half4*>(dl + r * kSwB + c) = l4;
+    *reinterpret_cast<x3_half4*>(th + (int64_t)r * np_ + c) = ht4;
+    *reinterpret_cast<x3_half4*>(tl + (int64_t)r * np_ + c) = lt4;
+  }
+  if (w == 0 && lane == 0) bad_s = bad;
+  __syncthreads();
+  if (tid == 0) {
+    S.ysc[((int64_t)l * S.nt + kb) * S.nt + kb] = sY;
+    logdet[l] += ld;
+    if (bad_s != INT_MAX && info[l] == 0) info[l] = kb * kSwB + bad_s + 1;
+  }
+}
+
+__device__ inline void ci_split4(f32x4 v, float s, _Float16* __restrict__ hi, _Float16* __restrict__ lo) {
+  x3_half4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float y = v[e] * s;
+    const _Float16 hh = (_Float16)y;
+    h[e] = hh;
+    l[e] = (_Float16)(y - (float)hh);
+  }
+  *reinterpret_cast<x3_half4*>(hi) = h;
+  *reinterpret_cast<x3_half4*>(lo) = l;
+}
+
+// 256 x 256 accumulator tile (value = acc * mul) out TRANSPOSED through the 128 KB LDS stage:
+// fn(c, r0, v), v = (value(r0 + q, c))_{q < 4}; every (c, r0) once.  Starts with a barrier.
+template <typename Fn>
+__device__ inline void ci_transposed_out(const sx_f32x16 (&acc)[4][2], float mul, _Float16* lds, Fn fn) {
+  float* U = reinterpret_cast<float*>(lds);
+  const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    __syncthreads();
+    if ((w >> 2) == hh) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int rl = sx_row(a, e) - 128 * hh, c = sx_col(b);
+            U[c * 128 + (rl ^ ((c & 31) << 2))] = acc[a][b][e] * mul;
+          }
+    }
+    __syncthreads();
+    const int t4 = tid & 31;
+#pragma unroll 4
+    for (int cc = 0; cc < kSwB; cc += 16) {
+      const int c = cc + (tid >> 5), rl = 4 * t4;
+      fn(c, 128 * hh + rl, *reinterpret_cast<const f32x4*>(&U[c * 128 + (rl ^ ((c & 31) << 2))]));
+    }
+  }
+}
+
+// accumulator tile (value = acc * mul) -> fp16 planes hi / lo (row stride ld halves) scaled by s
+__device__ inline void ci_planes_out(const sx_f32x16 (&acc)[4][2], float mul, float s, _Float16* __restrict__ hi,
+                                     _Float16* __restrict__ lo, int64_t ld) {
+  const float m = mul * s;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = sx_row(a, e), c = sx_col(b);
+        const float y = acc[a][b][e] * m;
+        const _Float16 yh = (_Float16)y;
+        hi[r * ld + c] = yh;
+        lo[r * ld + c] = (_Float16)(y - (float)yh);
+      }
+}
+
+__device__ inline float ci_acc_absmax(const sx_f32x16 (&acc)[4][2]) {
+  float m = 0.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) m = fmaxf(m, fabsf(acc[a][b][e]));
+  return m;
+}
+
+// ------------------------------------------------------------------------------------------
+// pass-0 C operand: blocks i >= 1 of column 0 of A, each with the split scale of its exact max.
+// grid (nt - 1, L), 256 threads.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ci_prep0_kernel(const float* __restrict__ Aall, int np_, CiScratch S) {
+  __shared__ uint32_t red;
+  const int l = blockIdx.y, i = blockIdx.x + 1, t = threadIdx.x;
+  const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_;
+  if (t == 0) red = 0u;
+  float m = 0.f;
+  for (int e = t; e < kSwBB / 4; e += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + (int64_t)(e >> 6) * np_ + (e & 63) * 4);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((t & 63) == 0) atomicMax(&red, __float_as_uint(m));
+  __syncthreads();
+  const float sc = x3_scale(__uint_as_float(red));
+  const int64_t o = (int64_t)l * np_ * kSwB + (int64_t)i * kSwBB;
+  for (int e = t; e < kSwBB / 4; e += 256) {
+    const int r = e >> 6, c = (e & 63) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(T + (int64_t)r * np_ + c);
+    ci_split4(v, sc, S.Ch[0] + o + r * kSwB + c, S.Cl[0] + o + r * kSwB + c);
+  }
+  if (t == 0) S.c_scale(l, 0, i) = sc;
+}
+
+// ------------------------------------------------------------------------------------------
+// panel(k): L_ik = C_i Y_kk^T for i > k (C_i: block i of pass k's C planes; Y_kk rows from D), one
+// 512-thread workgroup per block, grid (nt - k - 1, L) -> the planes of L, tile (i, k), with the split
+// scale of the block's exact max.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void ci_panel_kernel(CiScratch S, int np_, int k) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  __shared__ uint32_t red;
+  const int l = blockIdx.y, i = k + 1 + blockIdx.x;
+  const int64_t oc = (int64_t)l * np_ * kSwB + (int64_t)i * kSwBB, od = ((int64_t)l * S.nt + k) * kSwBB;
+  if (threadIdx.x == 0) red = 0u;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  sx_gemm(S.Ch[k & 1] + oc, S.Cl[k & 1] + oc, S.Dh + od, S.Dl + od, kSwB, kSwB, lds, acc);
+  const float inv = 1.0f / (S.c_scale(l, k, i) * S.ysc[((int64_t)l * S.nt + k) * S.nt + k]);
+  const float sl = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
+  const int64_t ot = (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_ + k * kSwB;
+  ci_planes_out(acc, inv, sl, S.Lh + ot, S.Ll + ot, np_);
+  if (threadIdx.x == 0) S.lsc[((int64_t)l * S.nt + i) * S.nt + k] = sl;
+}
+
+// ------------------------------------------------------------------------------------------
+// update(k): A_IJ -= L_Ik L_Jk^T on lower 256-tiles, K = 256, one 512-thread workgroup per tile on the
+// pre-split planes of L (DMA-staged, double-buffered chunks of 32); A enters in 8 chunks of 16
+// accumulator elements INSIDE the K loop (non-temporal: the A stream does not evict the planes), as in
+// the sweep's update (spd_sweep.hip).  MODE:
+//   kCiU1  column k+1 (tiles (I, k+1), I >= k+1 with the next pivot block, I >= k+2 without it):
+//          written as the planes of pass k+1's C operand (the diagonal tile in fp32, for the pivot)
+//   kCiU2  the trailing tiles I >= J >= k+2, in place
+// ------------------------------------------------------------------------------------------
+constexpr int kCiU2 = 0, kCiU1 = 1;
+constexpr int kCiFuseMaxL = 8;  // latent dims per call up to which the pivot updates its own block
+template <int MODE>
+__global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall, CiScratch S, int np_, int k,
+                                                        int ntl, int nwg) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  __shared__ uint32_t red;
+  if (MODE == kCiU1 && threadIdx.x == 0) red = 0u;
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int l = wgid / ntl, t = wgid % ntl, nt = np_ / kSwB;
+  int I, J;
+  if constexpr (MODE == kCiU1) {
+    I = (ntl == nt - k - 1) ? k + 1 + t : k + 2 + t;  // with / without the pivot block
+    J = k + 1;
+  } else {
+    sx_tri_blocked(t, nt - k - 2, I, J);
+    I += k + 2;
+    J += k + 2;
+  }
+  const int64_t np2 = (int64_t)np_ * np_;
+  float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+  const int64_t oa = l * np2 + (int64_t)I * kSwB * np_ + k * kSwB, ob = l * np2 + (int64_t)J * kSwB * np_ + k * kSwB;
+  const float cs = S.lsc[((int64_t)l * S.nt + I) * S.nt + k] * S.lsc[((int64_t)l * S.nt + J) * S.nt + k];
+  const float ncs = -cs, ninv = -1.0f / cs;  // acc = L_I L_J^T - A (units of cs); the result is -acc / cs
+  const _Float16* ah = S.Lh + oa;
+  const _Float16* al = S.Ll + oa;
+  const _Float16* bh = S.Lh + ob;
+  const _Float16* bl = S.Ll + ob;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  constexpr int CAUX = 2;
+  float cv[2][16];
+  constexpr int nk = kSwB / kSxBK;
+  sx_issue(ah, al, bh, bl, np_, 0, lds);
+#pragma unroll
+  for (int s = 0; s < nk; ++s) {
+    if (s == 0) SX_WAIT_VM(0);
+    else __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): DMA s and A chunk s - 2 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nk) sx_issue(ah, al, bh, bl, np_, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
+    if (s >= 2) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = 16 * (s - 2) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+        acc[a][b][e] += cv[s & 1][q] * ncs;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = 16 * s + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      cv[s & 1][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX));
+    }
+    __builtin_amdgcn_s_setprio(1);
+    sx_mma_stage(lds + (s & 1) * 4 * kSxPart, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+#pragma unroll
+  for (int j = nk - 2; j < nk; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = 16 * j + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      acc[a][b][e] += cv[j & 1][q] * ncs;
+    }
+  if (MODE == kCiU1 && I != J) {
+    // a block of column k+1 = block I of the next pass's C operand: straight to its planes
+    const float sc = x3_scale(sw_block_max(ci_acc_absmax(acc) * fabsf(ninv), &red));
+    const int64_t on = (int64_t)l * np_ * kSwB + (int64_t)I * kSwBB;
+    ci_planes_out(acc, ninv, sc, S.Ch[(k + 1) & 1] + on, S.Cl[(k + 1) & 1] + on, kSwB);
+    if (threadIdx.x == 0) S.c_scale(l, k + 1, I) = sc;
+  } else {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * ninv), rc, vo,
+                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
+  }
+}
+
+// D (the pivots' Y_kk planes) -> the diagonal tiles of the row-major Y planes (after potrf: the Y
+// planes alias A).  grid (nt, L), 256 threads.
+__global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_, _Float16* __restrict__ Yh,
+                                                           _Float16* __restrict__ Yl) {
+  const int k = blockIdx.x, l = blockIdx.y;
+  const int64_t od = ((int64_t)l * S.nt + k) * kSwBB;
+  const int64_t ot = (int64_t)l * np_ * np_ + (int64_t)k * kSwB * np_ + k * kSwB;
+  for (int e = threadIdx.x; e < kSwBB / 8; e += 256) {
+    const int r = e >> 5, c = (e & 31) * 8;
+    *reinterpret_cast<x3_half8*>(Yh + ot + (int64_t)r * np_ + c) = *reinterpret_cast<const x3_half8*>(S.Dh + od + r * kSwB + c);
+    *reinterpret_cast<x3_half8*>(Yl + ot + (int64_t)r * np_ + c) = *reinterpret_cast<const x3_half8*>(S.Dl + od + r * kSwB + c);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// ci_gemm_kernel<MODE>: out tile (i, j) = sum_{kb in [kb0, kb1)} A(i, kb) B(kb, j) over whole 256-blocks
+// on the x3 DMA tile machinery (x3_dma.hpp), operands from full [L, np, np] plane arrays (row stride np:
+// the K range of a row is contiguous), the accumulators rescaled at every block boundary to the new
+// block pair's split scales (powers of two: exact).
+//   kCiX  (trtri, step 1): X_ij = sum_{k=j}^{o+h-1} L_ik Y_kj      A = L planes (i, k),  B = Y^T planes (j, k)
+//                          -> X^T planes, tile (j, i) (transposed out), scale xsc(i, j)
+//   kCiY  (trtri, step 2): Y_ij = -sum_{k=o+h}^{i} Y_ik X_kj      A = Y planes (i, k),  B = X^T planes (j, k)
+//                          -> Y planes (i, j) and Y^T planes (j, i), scale ysc(i, j)
+//   kCiLauum:  (K^-1)_IJ = sum_{k>=I} Y_kI^T Y_kJ                  A = Y^T planes (I, k), B = Y^T planes (J, k)
+//                          -> Kinv (I, J) and its mirror (J, I), fp32
+// trtri launches cover every (instance m, ii, jj) of level h: i = o + h + ii, j = o + jj, o = 2 h m
+// (workgroups with i >= nt exit at once); lauum the L nt (nt + 1) / 2 lower tiles.
+// ------------------------------------------------------------------------------------------
+constexpr int kCiX = 0, kCiY = 1, kCiLauum = 2;
+struct CiGemmArgs {
+  const _Float16 *ah, *al, *bh, *bl;  // full plane arrays
+  _Float16 *oh, *ol, *oth, *otl;      // outputs: row-major planes (kCiY), transposed planes (kCiX, kCiY)
+  float* Kinv;                         // kCiLauum
+  int np_, nt, h, per_dim, nwg;        // per_dim: workgroups per latent dim
+};
+
+template <int MODE>
+__global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  __shared__ float sprod[64];
+  __shared__ uint32_t red;
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int l = wgid / g.per_dim, t = wgid % g.per_dim, nt = g.nt, np_ = g.np_;
+  int i, j, kb0, kb1;
+  if constexpr (MODE == kCiLauum) {
+    sx_tri(t, i, j);
+    kb0 = i;
+    kb1 = nt;
+  } else {
+    const int h = g.h, hh2 = h * h, m = t / hh2, r = t % hh2, o = 2 * h * m;
+    i = o + h + r / h;
+    j = o + r % h;
+    if (i >= nt) return;  // (uniform: before any barrier)
+    if constexpr (MODE == kCiX) {
+      kb0 = j;
+      kb1 = o + h;
+    } else {
+      kb0 = o + h;
+      kb1 = i + 1;
+    }
+  }
+  const int nkb = kb1 - kb0;
+  // the scale of block pair kb: sA(kb) sB(kb)
+  const int64_t sl = (int64_t)l * nt * nt;
+  if (threadIdx.x < nkb) {
+    const int kb = kb0 + threadIdx.x;
+    float sa, sb;
+    if constexpr (MODE == kCiX) {
+      sa = S.lsc[sl + (int64_t)i * nt + kb];
+      sb = S.ysc[sl + (int64_t)kb * nt + j];
+    } else if constexpr (MODE == kCiY) {
+      sa = S.ysc[sl + (int64_t)i * nt + kb];
+      sb = S.xsc[sl + (int64_t)kb * nt + j];
+    } else {
+      sa = S.ysc[sl + (int64_t)kb * nt + i];
+      sb = S.ysc[sl + (int64_t)kb * nt + j];
+    }
+    sprod[threadIdx.x] = sa * sb;
+  }
+  if (threadIdx.x == 0) red = 0u;
+  const int64_t np2 = (int64_t)np_ * np_;
+  const int64_t oa = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)kb0 * kSwB;
+  const int64_t ob = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)kb0 * kSwB;
+  const _Float16* ah = g.ah + oa;
+  const _Float16* al = g.al + oa;
+  const _Float16* bh = g.bh + ob;
+  const _Float16* bl = g.bl + ob;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  constexpr int cpb = kSwB / kSxBK;  // K chunks per block
+  const int nk = nkb * cpb;
+  float scur = 1.f;
+  sx_issue(ah, al, bh, bl, np_, 0, lds);
+  for (int s = 0; s < nk; ++s) {
+    SX_WAIT_VM(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nk) sx_issue(ah, al, bh, bl, np_, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
+    if (s % cpb == 0) {  // a new block pair: move the accumulators to its units
+      const float snew = sprod[s / cpb];
+      if (s) {
+        const float ratio = snew / scur;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] *= ratio;
+      }
+      scur = snew;
+    }
+    __builtin_amdgcn_s_setprio(1);
+    sx_mma_stage(lds + (s & 1) * 4 * kSxPart, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  const float inv = 1.0f / scur;
+  if constexpr (MODE == kCiX) {
+    const float sx = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
+    const int64_t ot = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // X^T tile (j, i)
+    ci_transposed_out(acc, inv, lds, [&](int c, int r0, f32x4 v) {
+      ci_split4(v, sx, g.oth + ot + (int64_t)c * np_ + r0, g.otl + ot + (int64_t)c * np_ + r0);
+    });
+    if (threadIdx.x == 0) S.xsc[sl + (int64_t)i * nt + j] = sx;
+  } else if constexpr (MODE == kCiY) {
+    const float sy = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
+    const int64_t ot = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;   // Y tile (i, j)
+    const int64_t ott = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // Y^T tile (j, i)
+    ci_planes_out(acc, -inv, sy, g.oh + ot, g.ol + ot, np_);
+    ci_transposed_out(acc, -inv, lds, [&](int c, int r0, f32x4 v) {
+      ci_split4(v, sy, g.oth + ott + (int64_t)c * np_ + r0, g.otl + ott + (int64_t)c * np_ + r0);
+    });
+    if (threadIdx.x == 0) S.ysc[sl + (int64_t)i * nt + j] = sy;
+  } else {
+    float* O = g.Kinv + l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;
+    float* Ot = g.Kinv + l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(O, (short)0, 0x7fffffff, 0x00020000);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), ro, vo,
+                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+    if (i != j)
+      ci_transposed_out(acc, inv, lds, [&](int c, int r0, f32x4 v) {
+        *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
+      });
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host sequencing
+// ------------------------------------------------------------------------------------------
+// potrf lookahead schedules (the side stream has the highest priority):
+// (a) few latent dims (L <= kCiFuseMaxL): the pivots run back to back on the side stream, each applying
+//     the previous pass's update to its own block (ci_pending_update) and waiting only for U2(m-2), the
+//     last writer of its block before that:
+//       side:  pivot(0);  [wait ev_u2(m-1) (ev_c = prep0 for m = 0);  pivot(m+1);  record ev_piv(m+1)]...
+//       main:  prep0;  record ev_c;  [wait ev_piv(m);  panel(m);  U1(m) (without the pivot block);  U2(m);
+//              record ev_u2(m)]...
+// (b) many latent dims (the headline L = 16): the chain runs whole on the side stream beside U2:
+//       side:  prep0;  pivot(0);  panel(0);  record ev_prep
+//       main:  [wait ev_prep;  U1(k) (with the pivot block);  record ev_c;  U2(k)]...
+//       side:  [wait ev_c;  pivot(k+1);  panel(k+1);  record ev_prep]...
+// Buffers: U1(k) writes C planes (k+1) & 1, read by panel(k+1) (and pivot(k+2)'s pending update in (a));
+// their previous readers (panel(k-1), pivot(k)) precede U1(k) on the caller's stream.  The L planes of
+// column k are written once (panel(k)) and read by U1(k), U2(k), and trtri; D and the Y^T diagonal tiles
+// by the pivots only.  Then, on the caller's stream: the diagonal copy, trtri (2 launches per level),
+// lauum.
+size_t ci_scratch_bytes(int np_, int L) { return CiScratch(nullptr, np_, L).bytes; }
+
+int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
+                   int32_t* info, hipStream_t st) {
+  if (np_ <= 0 || np_ % kSwB || np_ / kSwB > 64) return -1;
+  if (L <= 0) return -2;
+  CiScratch S((char*)scratch, np_, L);
+  const int nt = S.nt;
+  const int64_t full = (int64_t)L * np_ * np_;
+  _Float16* YTh = YT;
+  _Float16* YTl = YT + full;
+  auto ok = [](hipError_t e) { return e == hipSuccess; };
+  {
+    ProfScope ps(LVAE_PH_POTRF, st);
+    std::lock_guard<std::mutex> lock(side_mutex());
+    SideStream* sd = nullptr;
+    LVAE_TRY(side_stream(sd));
+    (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
+    (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
+    if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
+    const bool fuse = L <= kCiFuseMaxL;
+    if (fuse) {
+      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, YTh, YTl, logdet, info, 0);
+      if (!ok(hipEventRecord(sd->piv[0], sd->s))) return LVAE_ERR_LAUNCH;
+      if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, st>>>(A, np_, S);
+      if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
+      for (int m = 0; m < nt; ++m) {
+        if (m + 1 < nt) {
+          if (!ok(hipStreamWaitEvent(sd->s, m == 0 ? sd->c : sd->u2p[(m - 1) & 1], 0))) return LVAE_ERR_LAUNCH;
+          ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, YTh, YTl, logdet, info, 1);
+          if (!ok(hipEventRecord(sd->piv[(m + 1) & 1], sd->s))) return LVAE_ERR_LAUNCH;
+        }
+        if (!ok(hipStreamWaitEvent(st, sd->piv[m & 1], 0))) return LVAE_ERR_LAUNCH;
+        if (m + 1 < nt) {
+          ci_panel_kernel<<<dim3(nt - m - 1, L), 512, 0, st>>>(S, np_, m);
+          const int n1 = nt - m - 2;  // column m+1 without the pivot block
+          if (n1 > 0) ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, m, n1, n1 * L);
+          const int n2 = (nt - m - 2) * (nt - m - 1) / 2;
+          if (n2 > 0) {
+            ProfScope pu(LVAE_PH_SWEEP_UPD, st);
+            ci_update_kernel<kCiU2><<<n2 * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L);
+          }
+          if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
+        }
+      }
+    } else {
+      if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
+      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, YTh, YTl, logdet, info, 0);
+      if (nt > 1) ci_panel_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(S, np_, 0);
+      if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+      for (int k = 0; k + 1 < nt; ++k) {
+        if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // panel(k)
+        const int n1 = nt - k - 1;  // column k+1 with the pivot block
+        ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, k, n1, n1 * L);
+        if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
+        if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
+        ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, YTh, YTl, logdet, info, 0);
+        if (k + 2 < nt) ci_panel_kernel<<<dim3(nt - k - 2, L), 512, 0, sd->s>>>(S, np_, k + 1);
+        if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
+        const int n2 = (nt - k - 2) * (nt - k - 1) / 2;
+        if (n2 > 0) {
+          ProfScope pu(LVAE_PH_SWEEP_UPD, st);
+          ci_update_kernel<kCiU2><<<n2 * L, 512, 0, st>>>(A, S, np_, k, n2, n2 * L);
+        }
+      }
+      if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // the last pivot
+    }
+  }
+  LVAE_CHECK_LAUNCH();
+  {
+    // trtri + lauum (the rest of potri)
+    ProfScope ps(LVAE_PH_POTRI, st);
+    _Float16* Yh = reinterpret_cast<_Float16*>(A);  // A is dead: the Y planes
+    _Float16* Yl = Yh + full;
+    _Float16* XTh = reinterpret_cast<_Float16*>(Kinv);  // Kinv is not written yet: the X^T planes
+    _Float16* XTl = XTh + full;
+    ci_diag_copy_kernel<<<dim3(nt, L), 256, 0, st>>>(S, np_, Yh, Yl);
+    for (int h = 1; h < nt; h *= 2) {
+      const int ninst = (nt + 2 * h - 1) / (2 * h), per = ninst * h * h, nwg = per * L;
+      CiGemmArgs gx{S.Lh, S.Ll, YTh, YTl, nullptr, nullptr, XTh, XTl, nullptr, np_, nt, h, per, nwg};
+      ci_gemm_kernel<kCiX><<<nwg, 512, 0, st>>>(gx, S);
+      CiGemmArgs gy{Yh, Yl, XTh, XTl, Yh, Yl, YTh, YTl, nullptr, np_, nt, h, per, nwg};
+      ci_gemm_kernel<kCiY><<<nwg, 512, 0, st>>>(gy, S);
+    }
+    const int per = nt * (nt + 1) / 2, nwg = per * L;
+    CiGemmArgs gl{YTh, YTl, YTh, YTl, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg};
+    ci_gemm_kernel<kCiLauum><<<nwg, 512, 0, st>>>(gl, S);
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace lvae
+
+extern "C" {
+size_t lvae_spd_inv_chol_scratch_size(int np_, int L) {
+  // the C-ABI form also needs the Y^T planes (the KL workspace lends its S-operand planes instead)
+  return lvae::ci_scratch_bytes(np_, L) + lvae::align256((size_t)L * np_ * np_ * 2 * sizeof(_Float16));
+}
+int lvae_spd_inv_chol_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
+                          void* stream) {
+  if (!A) return -3;
+  if (!scratch || ((uintptr_t)scratch & 255)) return -4;
+  if (!Ainv) return -5;
+  if (!logdet) return -6;
+  if (!info) return -7;
+  if (np_ <= 0 || np_ % lvae::kSwB) return -1;
+  char* yt = (char*)scratch + lvae::ci_scratch_bytes(np_, L);
+  return lvae::ci_inverse_f32(np_, L, A, scratch, (_Float16*)yt, Ainv, logdet, info, (hipStream_t)stream);
+}
+}

@@ -491,6 +491,172 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
     part[((int64_t)l * kBwdSlots + sl) * G + g0] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
 }
 
+// fp64 residual of the exact-KL solve, r = mu - K alpha0 (K = Gram + noise I, alpha0 = K^-1 mu from the
+// fp32 inverse), the matrix never materialised: every lower 64-tile's kernel values are evaluated in
+// fp64 (fp64 exp / sin, covariate tests and differences exact, as the reference's double arithmetic)
+// and contracted with alpha0 on both sides -- the row sums K_IJ a_J of block I and, off the diagonal,
+// the column sums K_IJ^T a_I of block J -- each written once to part[l][other block][row], summed in a
+// fixed order by kl_resid_reduce (deterministic).  Grid (G, L) over the tiles t = g, g + G, ...;
+// diagonal tiles are evaluated whole.  Components whose Cat / Bin gates are zero on a whole wave skip
+// their exp / sin factors.  Refining alpha = alpha0 + K^-1 r (kl_alpha_kernel) then makes K^-1 mu
+// (and mu^T K^-1 mu) fp64-accurate up to cond(K)^2 x the inverse's error (elbo_functions.py:27-30).
+__device__ inline void apply_factor64(int kind, int d, const double* __restrict__ pf, const double* __restrict__ sx1,
+                                      const double* __restrict__ sx2, int tr, int tc, double (&v)[4][4]) {
+  double xr[4], xc[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xc[c] = sx2[d * kGT + c * 16 + tc];
+  if (kind == LVAE_CAT) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] == xc[c]) ? v[a][c] : 0.0;
+  } else if (kind == LVAE_BIN) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] + xc[c] == 2.0) ? v[a][c] : 0.0;
+  } else if (kind == LVAE_RBF) {
+    const double cf = -0.5 / (pf[0] * pf[0]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double df = xr[a] - xc[c];
+        v[a][c] *= exp(cf * df * df);
+      }
+  } else if (kind == LVAE_PER) {
+    const double cf = -2.0 / (pf[0] * pf[0]), ip = M_PI / pf[1];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double sn = sin(fabs(xr[a] - xc[c]) * ip);
+        v[a][c] *= exp(cf * sn * sn);
+      }
+  } else {  // LVAE_LIN
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[a][c] *= xr[a] * xc[c];
+  }
+}
+
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void kl_resid_tiles(DevSpec s, const double* __restrict__ x, int ldx, int n, int np_,
+                                                      int qs, const double* __restrict__ params,
+                                                      const double* __restrict__ noise,
+                                                      const double* __restrict__ alpha, double* __restrict__ part,
+                                                      int ntiles) {
+  __shared__ double sx1[kGT * kMaxQB];
+  __shared__ double sx2[kGT * kMaxQB];
+  __shared__ double sp[64];
+  __shared__ double sa1[kGT], sa2[kGT];
+  __shared__ double cred[4][kGT];
+  const int G = gridDim.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  const int lane = tid & 63, wv = tid >> 6, nt = np_ / kGT;
+  if (tid < s.n_params) sp[tid] = params[(int64_t)l * s.n_params + tid];
+  const double nz = noise[l];
+  const double* al = alpha + (int64_t)l * np_;
+  for (int t = blockIdx.x; t < ntiles; t += G) {
+    int I, J;
+    tri_index(t, I, J);
+    const int i0 = I * kGT, j0 = J * kGT;
+    __syncthreads();  // the previous tile's LDS readers are done
+    stage_cov(x, ldx, n, qs, i0, j0, sx1, sx2);
+    if (tid < kGT) sa1[tid] = al[i0 + tid];
+    else if (tid < 2 * kGT) sa2[tid - kGT] = al[j0 + tid - kGT];
+    __syncthreads();
+    double k[4][4] = {};
+#pragma unroll 1
+    for (int r = 0; r < s.n_comp; ++r) {
+      double v[4][4];
+      const double sc = sp[s.scale_idx[r]];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[a][c] = sc;
+      // gates first (cheap, exact), then the transcendental factors unless the gates zeroed the wave
+#pragma unroll 1
+      for (int f = 0; f < s.n_fac[r]; ++f) {
+        const int kind = s.kind[r][f];
+        if (kind != LVAE_CAT && kind != LVAE_BIN) continue;
+        apply_factor64(kind, s.dim[r][f], sp, sx1, sx2, tr, tc, v);
+      }
+      bool any = false;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) any |= v[a][c] != 0.0;
+      if (!__any(any)) continue;
+#pragma unroll 1
+      for (int f = 0; f < s.n_fac[r]; ++f) {
+        const int kind = s.kind[r][f];
+        if (kind == LVAE_CAT || kind == LVAE_BIN) continue;
+        const int pi = s.param_idx[r][f];
+        apply_factor64(kind, s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) k[a][c] += v[a][c];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int i = i0 + 4 * tr + a, j = j0 + 4 * tc + c;
+        if (i >= n || j >= n) k[a][c] = 0.0;
+        else if (i == j) k[a][c] += nz;
+      }
+    // row sums of block I (this tile's share): reduce over the 16 lanes tc of each row group
+    double rs[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double v = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v += k[a][c] * sa2[4 * tc + c];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      rs[a] = v;
+    }
+    if (tc == 0) {
+      double* pr = part + ((int64_t)l * nt + J) * np_ + i0 + 4 * tr;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) pr[a] = rs[a];
+    }
+    if (I != J) {  // (uniform) column sums of block J: over tr (4 per wave, then the 4 waves)
+      double cs[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double v = 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) v += k[a][c] * sa1[4 * tr + a];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        cs[c] = v;
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cred[wv][4 * tc + c] = cs[c];
+      }
+      __syncthreads();
+      if (tid < kGT) part[((int64_t)l * nt + I) * np_ + j0 + tid] = cred[0][tid] + cred[1][tid] + cred[2][tid] + cred[3][tid];
+    }
+  }
+}
+
+// r[l][i] = mu[l][i] - sum_s part[l][s][i] (fixed order), 0 on the padding.  Grid (np / 256, L).
+__global__ __launch_bounds__(256) void kl_resid_reduce(const double* __restrict__ part, const double* __restrict__ muc,
+                                                       int n, int np_, double* __restrict__ res) {
+  const int i = blockIdx.x * 256 + threadIdx.x, l = blockIdx.y, nt = np_ / kGT;
+  if (i >= np_) return;
+  double acc = 0.0;
+  for (int s = 0; s < nt; ++s) acc += part[((int64_t)l * nt + s) * np_ + i];
+  res[(int64_t)l * np_ + i] = i < n ? muc[(int64_t)l * np_ + i] - acc : 0.0;
+}
+
 // per-parameter derivative constants of kl_gram_bwd_tiles' raw sums (host-built from the spec):
 // type 0 scale (1), 1 RBF lengthscale (1 / l^3), 2 PER lengthscale (4 / l^3), 3 PER period
 // (2 pi / (l^2 p^2), l at index ell[p])
@@ -575,6 +741,27 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
     gram_sq_fill_kernel<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles);
   else
     gram_sq_fill_kernel<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t kl_resid_partials_bytes(int np_, int L) { return (size_t)L * (np_ / kGT) * np_ * sizeof(double); }
+
+int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                  const double* params, const double* noise, const double* alpha0, const double* muc, double* part,
+                  double* res, hipStream_t st) {
+  const int bucket = spec_bucket(spec);
+  const int qs = spec_qs(spec);
+  if (!bucket || qs > kMaxQB || qs > ldx || spec->n_params > 64) return -1;
+  const DevSpec ds = to_dev(spec);
+  const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2;
+  int G = (2048 + L - 1) / L;
+  G = G < ntiles ? G : ntiles;
+  if (bucket == 1)
+    kl_resid_tiles<8, 2><<<dim3(G, L), 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, alpha0, part, ntiles);
+  else
+    kl_resid_tiles<16, 4><<<dim3(G, L), 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, alpha0, part, ntiles);
+  kl_resid_reduce<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(part, muc, n, np_, res);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -2,11 +2,15 @@
 // analytic backward, batched over the L latent dims (replaces the Python loop at training.py:515-522).
 //
 //   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
-//   K^-1, log|K|                                   (spd_sweep_f32: block symmetric sweep, f16 x3 MFMA)
-//   a = K^-1 mu, d = diag K^-1                    (kl_alpha_kernel, f64 accumulation; when a backward
-//                                                   follows, the same pass writes the S GEMM operand
-//                                                   B = K^-1 diag(sqrt v) as fp16 hi / lo planes with
-//                                                   a per-row power-of-two scale)
+//   K^-1, log|K|                                   (ci_inverse_f32: blocked Cholesky + trtri + lauum,
+//                                                   f16 x3 MFMA, chol_inv.hip)
+//   a0 = K^-1 mu                                   (kl_alpha_kernel, f64 accumulation)
+//   r = mu - K a0                                  (kl_gram_resid: fp64 Gram-free residual, gram.hip)
+//   a = a0 + K^-1 r, d = diag K^-1                 (kl_alpha_kernel again: one step of iterative
+//                                                   refinement in fp64; when a backward follows, the
+//                                                   same pass writes the S GEMM operand B = K^-1
+//                                                   diag(sqrt v) as fp16 hi / lo planes with a per-row
+//                                                   power-of-two scale)
 //   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
 // backward (dL/dkl_l = g_l):
 //   S = K^-1 V K^-1                                (syrk_x3_f32, f16 x3 MFMA, lower tiles)
@@ -27,9 +31,13 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
                 hipStream_t st);
 int syrk_x3_splits(int np_, int L);
 int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
-int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* logdet, int32_t* info,
-                  hipStream_t st);
-size_t spd_sweep_scratch_bytes(int np_, int L);
+int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
+                   int32_t* info, hipStream_t st);
+size_t ci_scratch_bytes(int np_, int L);
+size_t kl_resid_partials_bytes(int np_, int L);
+int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                  const double* params, const double* noise, const double* alpha0, const double* muc, double* part,
+                  double* res, hipStream_t st);
 
 struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
@@ -37,8 +45,8 @@ struct KLWorkspace {
   _Float16* planes;  // fp16 hi / lo planes of the S GEMM operand: 2 L np^2 halves
   float* rsc;        // [L, np] their per-row split scales
   float* gb;         // [L] max_j sqrt(Kinv_jj v_j) (kl_bdiag_kernel)
-  char* sweep;
-  double *mu, *alpha, *kdiag, *logdet, *part;
+  char* chol;         // ci_inverse_f32 scratch (its Y^T planes are `planes`, free until the reduce)
+  double *mu, *alpha, *res, *kdiag, *logdet, *part, *rpart;
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
     size_t off = 0;
@@ -57,10 +65,12 @@ struct KLWorkspace {
     gb = (float*)take((size_t)L * sizeof(float));
     mu = (double*)take((size_t)L * np_ * sizeof(double));
     alpha = (double*)take((size_t)L * np_ * sizeof(double));
+    res = (double*)take((size_t)L * np_ * sizeof(double));
     kdiag = (double*)take((size_t)L * np_ * sizeof(double));
     logdet = (double*)take((size_t)L * sizeof(double));
-    sweep = take(spd_sweep_scratch_bytes(np_, L));
+    chol = take(ci_scratch_bytes(np_, L));
     part = (double*)take(kl_gram_bwd_partials_bytes(np_, L));
+    rpart = (double*)take(kl_resid_partials_bytes(np_, L));
     Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
     bytes = off;
   }
@@ -95,24 +105,25 @@ __global__ __launch_bounds__(256) void kl_bdiag_kernel(const float* __restrict__
   if (tid == 0) g[l] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// one wave per row: a_i = sum_j Kinv[i][j] mu_j (f64 accumulate), d_i = Kinv[i][i]; with PLANES also
-// row i of the S GEMM operand B = K^-1 diag(sqrt v) as fp16 planes B_ij sc_i = hi + lo, sc_i =
-// x3_scale(sqrt(Kinv_ii) g[l]) (a bound on max_j |B_ij|, kl_bdiag_kernel): the backward's GEMM
-// reads its operand pre-split and nothing re-reads K^-1 for it.
+// one wave per row: a_i = base_i + sum_j Kinv[i][j] u_j (f64 accumulate; base may be NULL), and
+// d_i = Kinv[i][i] when kdiag != NULL; with PLANES also row i of the S GEMM operand B = K^-1 diag(sqrt v)
+// as fp16 planes B_ij sc_i = hi + lo, sc_i = x3_scale(sqrt(Kinv_ii) g[l]) (a bound on max_j |B_ij|,
+// kl_bdiag_kernel): the backward's GEMM reads its operand pre-split and nothing re-reads K^-1 for it.
 template <bool PLANES>
-__global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ muc,
+__global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ u,
                                                        const float* __restrict__ sv, int np_,
-                                                       const float* __restrict__ g, double* __restrict__ alpha,
-                                                       double* __restrict__ kdiag, float* __restrict__ rsc,
-                                                       _Float16* __restrict__ Bh, _Float16* __restrict__ Bl) {
+                                                       const float* __restrict__ g, const double* base,
+                                                       double* alpha, double* __restrict__ kdiag,
+                                                       float* __restrict__ rsc, _Float16* __restrict__ Bh,
+                                                       _Float16* __restrict__ Bl) {
   typedef _Float16 half4 __attribute__((ext_vector_type(4)));
   const int l = blockIdx.y, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= np_) return;
   const int64_t ro = (int64_t)l * np_ * np_ + (int64_t)i * np_;
   const float* row = Kinv + ro;
-  const double* m = muc + (int64_t)l * np_;
-  const float* s = sv + (int64_t)l * np_;
+  const double* m = u + (int64_t)l * np_;
+  const float* s = PLANES ? sv + (int64_t)l * np_ : nullptr;
   const float dii = row[i];
   const float sc = PLANES ? x3_scale(sqrtf(fabsf(dii)) * g[l]) : 0.f;
   double acc = 0.0;
@@ -134,9 +145,10 @@ __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__
   }
   acc = wave_sum(acc);
   if (lane == 0) {
-    alpha[(int64_t)l * np_ + i] = acc;
-    kdiag[(int64_t)l * np_ + i] = (double)dii;
-    if (PLANES) rsc[(int64_t)l * np_ + i] = sc;
+    const int64_t o = (int64_t)l * np_ + i;
+    alpha[o] = (base ? base[o] : 0.0) + acc;
+    if (kdiag) kdiag[o] = (double)dii;
+    if (PLANES) rsc[o] = sc;
   }
 }
 
@@ -202,36 +214,43 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
     ProfScope ps(LVAE_PH_GRAM, st);
     LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
   }
-  {
-    // K^-1 and log|K|: the block symmetric sweep (spd_sweep.hip: 16 rank-256 passes at np = 4096,
-    // pivot inverses overlapped on a second stream)
-    ProfScope ps(LVAE_PH_POTRF, st);
-    LVAE_TRY(spd_sweep_f32(np_, L, ws.A, ws.sweep, ws.Kinv, ws.logdet, info, st));
-  }
+  // K^-1 and log|K|: blocked Cholesky + trtri + lauum (chol_inv.hip; phases POTRF / POTRI inside),
+  // its Y^T planes in the S-operand planes (written only by the reduce, after this)
+  LVAE_TRY(ci_inverse_f32(np_, L, ws.A, ws.chol, ws.planes, ws.Kinv, ws.logdet, info, st));
   LVAE_CHECK_LAUNCH();
   return 0;
 }
 
-int lvae_kl_closed_reduce_f32(int n, int L, const double* mu, const double* logv, int ld_mu, double* kl,
-                              void* workspace, int need_bwd, void* stream) {
-  if (n <= 0) return -1;
-  if (L <= 0) return -2;
-  if (!mu || !logv || ld_mu < L) return -3;
-  if (!kl) return -6;
-  if (!workspace || ((uintptr_t)workspace & 255)) return -7;
+int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                              const double* params, const double* noise, const double* mu, const double* logv,
+                              int ld_mu, double* kl, void* workspace, int need_bwd, void* stream) {
+  if (!spec) return -1;
+  if (!x) return -2;
+  if (n <= 0) return -4;
+  if (L <= 0) return -5;
+  if (!params) return -6;
+  if (!noise) return -7;
+  if (!mu || !logv || ld_mu < L) return -8;
+  if (!kl) return -11;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -12;
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
   ProfScope ps(LVAE_PH_KL_REDUCE, st);
   kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v, ws.sv);
   const int64_t per = (int64_t)L * np_ * np_;
+  const dim3 rows(np_ / 4, L);
+  // a0 = K^-1 mu; r = mu - K a0 in fp64 from the covariates; a = a0 + K^-1 r (+ d, + the S planes)
+  kl_alpha_kernel<false><<<rows, 256, 0, st>>>(ws.Kinv, ws.mu, nullptr, np_, nullptr, nullptr, ws.alpha, nullptr,
+                                               nullptr, nullptr, nullptr);
+  LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res, st));
   if (need_bwd) {
     kl_bdiag_kernel<<<L, 256, 0, st>>>(ws.Kinv, ws.sv, np_, ws.gb);
-    kl_alpha_kernel<true><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, ws.gb, ws.alpha, ws.kdiag,
-                                                             ws.rsc, ws.planes, ws.planes + per);
+    kl_alpha_kernel<true><<<rows, 256, 0, st>>>(ws.Kinv, ws.res, ws.sv, np_, ws.gb, ws.alpha, ws.alpha, ws.kdiag,
+                                                ws.rsc, ws.planes, ws.planes + per);
   } else {
-    kl_alpha_kernel<false><<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.mu, ws.sv, np_, nullptr, ws.alpha,
-                                                              ws.kdiag, nullptr, nullptr, nullptr);
+    kl_alpha_kernel<false><<<rows, 256, 0, st>>>(ws.Kinv, ws.res, nullptr, np_, nullptr, ws.alpha, ws.alpha,
+                                                 ws.kdiag, nullptr, nullptr, nullptr);
   }
   kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   LVAE_CHECK_LAUNCH();
@@ -251,7 +270,7 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   if (!kl) return -11;
   if (!workspace || ((uintptr_t)workspace & 255)) return -13;
   LVAE_TRY(lvae_kl_closed_factor_f32(spec, x, ldx, n, L, params, noise, info, workspace, stream));
-  return lvae_kl_closed_reduce_f32(n, L, mu, logv, ld_mu, kl, workspace, need_bwd, stream);
+  return lvae_kl_closed_reduce_f32(spec, x, ldx, n, L, params, noise, mu, logv, ld_mu, kl, workspace, need_bwd, stream);
 }
 
 int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,

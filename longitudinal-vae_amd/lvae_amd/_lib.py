@@ -84,7 +84,8 @@ SIGNATURES = {
     "lvae_kl_closed_padded_n": (_I32, [_I32]),
     "lvae_kl_closed_workspace_size": (_SZ, [_I32, _I32]),
     "lvae_kl_closed_factor_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
-    "lvae_kl_closed_reduce_f32": (_I32, [_I32, _I32, _VP, _VP, _I32, _VP, _VP, _I32, _VP]),
+    "lvae_kl_closed_reduce_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32,
+                                         _VP]),
     "lvae_kl_closed_fwd_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _I32, _VP, _VP, _VP,
                                       _I32, _VP]),
     "lvae_kl_closed_bwd_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _I32, _VP, _VP, _VP, _VP,
@@ -113,6 +114,8 @@ SIGNATURES = {
     "lvae_conv3x3_pool_wgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "lvae_spd_inv_chol_scratch_size": (_SZ, [_I32, _I32]),
+    "lvae_spd_inv_chol_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),
     "lvae_predict_f64": (_I32, [_SPEC, _SPEC, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP, _VP,
                                 _VP, _VP, _D, _VP, _VP, _VP, _VP]),

@@ -67,14 +67,13 @@ class KLFactor:
         with torch.cuda.stream(stream):
             self.x64 = x.detach().to(torch.float64).contiguous()
             self.p = params.detach().to(torch.float64).contiguous()
-            nz = noise.detach().to(torch.float64).reshape(L).contiguous()
+            self.nz = noise.detach().to(torch.float64).reshape(L).contiguous()
             self.ws = torch.empty(int(lib.lvae_kl_closed_workspace_size(n, L)), dtype=torch.uint8, device=dev)
             self.info = torch.empty(L, dtype=torch.int32, device=dev)
             rc = lib.lvae_kl_closed_factor_f32(spec, _lib.ptr(self.x64), self.x64.shape[1], n, L, _lib.ptr(self.p),
-                                               _lib.ptr(nz), _lib.ptr(self.info), _lib.ptr(self.ws),
+                                               _lib.ptr(self.nz), _lib.ptr(self.info), _lib.ptr(self.ws),
                                                _lib.stream_ptr())
             _lib.check(rc, "kl_closed_factor")
-            nz.record_stream(stream)
         self.stream = stream
         self.n, self.L = n, L
 
@@ -82,13 +81,13 @@ class KLFactor:
         """Make the current stream wait for the factorisation (and own its buffers)."""
         cur = torch.cuda.current_stream(self.ws.device)
         cur.wait_stream(self.stream)
-        for t in (self.ws, self.info, self.x64, self.p):
+        for t in (self.ws, self.info, self.x64, self.p, self.nz):
             t.record_stream(cur)
 
 
 def kl_closed_prefactor(covar_modules, train_x, likelihoods, L, stream):
-    """Launch the (mu, logvar)-independent part of KL_closed_batched -- the Gram and its sweep
-    inverse -- on ``stream`` now; pass the result as KL_closed_batched(..., factor=)."""
+    """Launch the (mu, logvar)-independent part of KL_closed_batched -- the Gram and its blocked
+    Cholesky inverse -- on ``stream`` now; pass the result as KL_closed_batched(..., factor=)."""
     spec, params = _stack_modules(covar_modules)
     if params.shape[0] != L:
         raise ValueError(f"kernel batch {params.shape[0]} != latent dims {L}")
@@ -112,7 +111,8 @@ class _KLClosedFn(torch.autograd.Function):
                 raise ValueError(f"factor is for n={factor.n}, L={factor.L}; got n={n}, L={L}")
             factor.join()
             x64, p, ws, info = factor.x64, factor.p, factor.ws, factor.info
-            rc = lib.lvae_kl_closed_reduce_f32(n, L, _lib.ptr(mu64), _lib.ptr(lv64), L, _lib.ptr(kl), _lib.ptr(ws),
+            rc = lib.lvae_kl_closed_reduce_f32(spec, _lib.ptr(x64), x64.shape[1], n, L, _lib.ptr(p), _lib.ptr(factor.nz),
+                                               _lib.ptr(mu64), _lib.ptr(lv64), L, _lib.ptr(kl), _lib.ptr(ws),
                                                need_bwd, _lib.stream_ptr())
             _lib.check(rc, "kl_closed_reduce")
         else:

@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 OUT=gpurun_out
 mkdir -p $OUT
 echo "[$(date +%T)] pytest -m gpu ${K:+-k "$K"}"
-timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread \
+timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest tests -m gpu ${PYTEST_X:--x} -v -s --timeout 300 --timeout-method thread \
   -p no:cacheprovider ${K:+-k "$K"} > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR|rel err|errors|passed|failed|Error" $OUT/pytest_gpu.log | tail -60
 [ $rc -eq 0 ] || exit $rc

@@ -1,0 +1,180 @@
+"""The RCCL ("nccl" backend) branches of the multi-GPU steps, run for real in a world-size-1 process
+group on one GPU: LatentShardedClosedStep's all_gather_into_tensor + all-reduces (training.py:484-592)
+and the two-graph GraphedStep of the data-parallel Hensman step with its gradient / natural-gradient
+all-reduces between the graphs (training.py:90-140).  A world of one makes every collective an
+identity, so each result must equal the single-process step (the gloo tests in
+test_distributed_cpu.py cover the world-2 arithmetic).  Also: ClosedStep replayed as one HIP graph
+against its eager form (the factor's side streams and events inside the capture)."""
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import lvae_oracle as O
+from test_gpu_regime_b import CFG, DEV, _random_hypers, rel, set_raw
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+class _NcclWorld1:
+    def __enter__(self):
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        assert dist.get_backend() == "nccl"
+        return dist
+
+    def __exit__(self, *exc):
+        import torch.distributed as dist
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+        return False
+
+
+def test_rccl_world1_latent_sharded_closed_step(hip):
+    """LatentShardedClosedStep over RCCL (all_gather_into_tensor of (mu, logvar), SUM all-reduces of
+    d/d(mu, logvar), of the flat gradient bucket and of the loss terms) against the oracle's
+    whole-batch standard_training step: loss terms and every gradient."""
+    import lvae_amd as la
+    from lvae_amd.distributed import LatentShardedClosedStep
+    from lvae_amd.vae import ConvVAE
+    from lvae_amd.data import health_mnist_batch
+    L, P, T = 4, 32, 16
+    img, mask, X = health_mnist_batch(P, T, seed=19, dtype=torch.float64)
+    ref_vae = O.ConvVAE(L).double()
+    ref_vae.load_state_dict(O.vae_weights(ref_vae, 23))
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).double()
+    vae.load_state_dict(ref_vae.state_dict())
+    vae = vae.float().to(DEV)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    set_raw(k, _random_hypers(k, L, np.random.default_rng(19)))
+    raw = torch.stack([p.detach().clone() for _, p in k.named_parameters()], 1).requires_grad_()
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    eps = torch.randn(P * T, L, generator=torch.Generator().manual_seed(5), dtype=torch.float64)
+    loss, recon, gp = O.closed_step(ref_vae, O.spec_full(**CFG), raw, torch.ones(L, dtype=torch.float64), img, mask,
+                                    X, eps, 0.15)
+    with _NcclWorld1():
+        opt = torch.optim.SGD(list(vae.parameters()) + list(kd.parameters()), lr=0.0)
+        step = LatentShardedClosedStep(vae, kd, lik, opt, weight=0.15, loss_function="mse")
+        net, rl, _, g = step(img.float().to(DEV), mask.float().to(DEV), X.to(DEV), eps.float().to(DEV))
+        torch.cuda.synchronize()
+    assert rel(net, loss) < 1e-4
+    assert rel(rl, recon) < 1e-4
+    assert rel(g, gp) < 1e-4
+    assert rel(torch.stack([p.grad for _, p in kd.named_parameters()], 1), raw.grad) < 1e-4
+    for (name, p), (_, q) in zip(vae.named_parameters(), ref_vae.named_parameters()):
+        if q.grad is not None:
+            assert rel(p.grad, q.grad) < 1e-3, name
+
+
+def _hensman_setup(L=4, M=40, T=16, P=32):
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_batch
+    img, mask, X = health_mnist_batch(P, T, seed=16, device=DEV)
+    N = P * T
+    z = torch.stack([torch.cat([X[0:M // 2], X[N // 2:N // 2 + M // 2]])] * L)
+    batches = [torch.cat([torch.arange(s * T, (s + 1) * T) for s in ss]).to(DEV)
+               for ss in ([3, 9, 20, 1, 27], [4, 11, 30, 0, 7], [2, 5, 8, 13, 21], [6, 10, 12, 14, 15])]
+    eps = torch.randn(5 * T, L, generator=torch.Generator().manual_seed(4)).to(DEV)
+    return la, img, mask, X, z, batches, eps
+
+
+def test_rccl_world1_graphed_hensman_two_graphs(hip):
+    """The data-parallel Hensman step replayed as TWO HIP graphs with the RCCL all-reduces between
+    them (GradAllReduce of the Adam gradients, SUM all-reduce of the natural-gradient directions:
+    GraphedStep's comm path) against the eager single-process step, step after step."""
+    from lvae_amd.distributed import GradAllReduce, allreduce_tensors
+    from lvae_amd.steps import GraphedStep, HensmanStep
+    from lvae_amd.vae import ConvVAE
+    la, img, mask, X, z, batches, eps = _hensman_setup()
+    L, M, T, P = 4, 40, 16, 32
+
+    def make(hooks):
+        torch.manual_seed(3)
+        vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+        k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+        k0, k1 = k0.to(DEV), k1.to(DEV)
+        lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+        with torch.no_grad():
+            H = k0(z, z).evaluate() + 1e-6 * torch.eye(M, dtype=torch.float64, device=DEV)
+        m = torch.zeros(L, M, 1, dtype=torch.float64, device=DEV)
+        params = list(k0.parameters()) + list(k1.parameters()) + list(vae.parameters())
+        opt = torch.optim.Adam(params, lr=1e-3, capturable=True)
+        kw = {}
+        if hooks:
+            kw = dict(world=1, grad_hook=GradAllReduce(params, 1),
+                      ng_reduce=lambda ts: allreduce_tensors(ts, average=False))
+        return HensmanStep(vae, k0, k1, lik, opt, m, H, z, P, T, **kw), k0
+
+    la.set_sync_checks(False)
+    try:
+        eager, k0_e = make(False)
+        eager(img[batches[0]], mask[batches[0]], X[batches[0]], eps)  # = the graph's warm-up step
+        outs_e = [[float(v) for v in eager(img[b], mask[b], X[b], eps)] for b in batches]
+        with _NcclWorld1():
+            graph_step, k0_g = make(True)
+            s = (img[batches[0]].clone(), mask[batches[0]].clone(), X[batches[0]].clone(), eps)
+            g = GraphedStep(graph_step, s, warmup=1)
+            assert g.comm and g.g2 is not None
+            outs_g = []
+            for b in batches:
+                torch.index_select(img, 0, b, out=s[0])
+                torch.index_select(mask, 0, b, out=s[1])
+                torch.index_select(X, 0, b, out=s[2])
+                outs_g.append([float(v) for v in g()])
+            g.check()
+    finally:
+        la.set_sync_checks(True)
+    for a, b in zip(outs_e, outs_g):
+        assert np.allclose(a, b, rtol=1e-6), (a, b)
+    # (m, H) after five natural-gradient steps: the fp32 ConvVAE backward (MIOpen, run-to-run
+    # reduction order) moves grad_m at ~1e-7, which the updates carry into m at ~1e-6 of its size
+    assert rel(graph_step.m, eager.m) < 1e-5 and rel(graph_step.H, eager.H) < 1e-6
+    for (n, p), (_, q) in zip(k0_g.named_parameters(), k0_e.named_parameters()):
+        assert rel(p, q) < 1e-9, n
+
+
+def test_graphed_closed_step_matches_eager(hip):
+    """ClosedStep (the bench's exact-KL step: the factorisation on the caller's stream with the inverse's
+    own side stream, the ConvVAE on a second stream joined by events) captured as ONE HIP graph and
+    replayed, against the same step run eagerly: per-step loss terms and the parameters after three
+    Adam steps."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_batch
+    from lvae_amd.steps import ClosedStep, GraphedStep
+    from lvae_amd.vae import ConvVAE
+    L, P, T = 4, 32, 16
+    img, mask, X = health_mnist_batch(P, T, seed=12, device=DEV)
+    eps = torch.randn(P * T, L, generator=torch.Generator().manual_seed(6)).to(DEV)
+
+    def make():
+        torch.manual_seed(11)
+        vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+        k = la.generate_kernel(**CFG, latent_dim=L).to(DEV)
+        lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+        opt = torch.optim.Adam(list(k.parameters()) + list(vae.parameters()), lr=1e-3, capturable=True)
+        return ClosedStep(vae, k, lik, opt, weight=0.15), k
+
+    la.set_sync_checks(False)
+    try:
+        eager, k_e = make()
+        eager(img, mask, X, eps)  # = the graph's warm-up step
+        outs_e = [[float(v) for v in eager(img, mask, X, eps)] for _ in range(3)]
+        graph_step, k_g = make()
+        g = GraphedStep(graph_step, (img, mask, X, eps), warmup=1)
+        outs_g = [[float(v) for v in g()] for _ in range(3)]
+        g.check()
+    finally:
+        la.set_sync_checks(True)
+    for a, b in zip(outs_e, outs_g):
+        assert np.allclose(a, b, rtol=1e-6), (a, b)
+    for (n, p), (_, q) in zip(k_g.named_parameters(), k_e.named_parameters()):
+        assert rel(p, q) < 1e-6, n
