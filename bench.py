@@ -44,22 +44,25 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2s_pmc_summary.json")
-U2_NAME = "sw_update_kernel<0,2>"       # the sweep's interior rank-256 update U2 (spd_sweep.hip, MODE kSwU2)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3_pmc_summary.json")
+U2_NAME = "ci_update_kernel<0>"         # the Cholesky's trailing rank-256 update U2 (chol_inv.hip, MODE kCiU2)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernels):
-    """Sum over the named kernels (one dispatch each) of FETCH_SIZE x 2 + WRITE_SIZE, bytes."""
+def pmc_traffic(kernels, per_step=False):
+    """FETCH_SIZE x 2 + WRITE_SIZE (bytes) of the named kernels from the committed PMC summary: per
+    dispatch (mean), or per step (the summary's per-step total, for kernels launched several times
+    a step with different sizes)."""
     try:
         d = json.load(open(PMC_SUMMARY))
+        key = "per_step" if per_step else "mean"
         tot = 0.0
         for name in kernels:
-            f = [v["mean"] for k, v in d["FETCH_SIZE"].items() if name in k.replace(" ", "")]
-            w = [v["mean"] for k, v in d["WRITE_SIZE"].items() if name in k.replace(" ", "")]
+            f = [v[key] for k, v in d["FETCH_SIZE"].items() if name in k.replace(" ", "")]
+            w = [v[key] for k, v in d["WRITE_SIZE"].items() if name in k.replace(" ", "")]
             if not (f and w):
                 return None
             tot += (2 * f[0] + w[0]) * 1024
@@ -88,9 +91,25 @@ def setup_dist():
     return world, rank, dev
 
 
+def cpu_share():
+    """The host CPUs this process may use: the affinity mask, the cgroup v2 quota (cpu.max) and the
+    OMP_NUM_THREADS the box sets (the harness assigns each GPU a 16-CPU share; os.cpu_count() is the
+    whole machine's)."""
+    share = {"sched_getaffinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+             "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        share["cgroup_cpu_max"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        share["cgroup_cpu_max"] = "unreadable"
+    return share
+
+
 def host_info():
-    """lscpu model / sockets / physical cores, and the NUMA node of GPU0 if sysfs shows it."""
-    info = {"threads_used": torch.get_num_threads(), "os_cpu_count": os.cpu_count(), "machine": platform.machine()}
+    """lscpu model / sockets / physical cores, the NUMA node of GPU0 if sysfs shows it, and the CPU
+    share (cpu_share) the timed threads come from."""
+    info = {"threads_used": torch.get_num_threads(), "os_cpu_count": os.cpu_count(), "machine": platform.machine(),
+            "cpu_share": cpu_share()}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         kv = {k.strip(): v.strip() for k, v in (ln.split(":", 1) for ln in out.splitlines() if ":" in ln)}
@@ -272,38 +291,48 @@ def run_closed(args, world, rank, dev):
                                       f"split {N // world}/rank, 1 all-gather + 2 all-reduces per step")}}
     if phase and Lr > 0:
         np_ = _lib.load().lvae_kl_closed_padded_n(N)
-        inv_ms = phase["potrf"][0] / args.steps
+        potrf_ms = phase["potrf"][0] / args.steps
+        potri_ms = phase.get("potri", (0.0, 0))[0] / args.steps
         syrk_ms = phase["syrk"][0] / args.steps
-        res["gp_cholesky_gflops"] = Lr * N ** 3 / 3 / (inv_ms * 1e-3) / 1e9 if inv_ms > 0 else None
-        res["gp_cholesky_gflops_basis"] = (f"L*N^3/3 (the LAPACK potrf count, SURVEY.md §8(d)) / time of the whole "
-                                           f"inverse phase (block-sweep K^-1 + log|K|, {inv_ms:.2f} ms/step on rank 0)")
+        res["gp_cholesky_gflops"] = Lr * N ** 3 / 3 / (potrf_ms * 1e-3) / 1e9 if potrf_ms > 0 else None
+        res["gp_cholesky_gflops_basis"] = (f"L*N^3/3 (the LAPACK potrf count, SURVEY.md §8(d)) / time of the blocked "
+                                           f"Cholesky factorisation phase (potrf: {potrf_ms:.2f} ms/step on rank 0; the "
+                                           f"triangular inverse + product, trtri + lauum, take {potri_ms:.2f} ms more)")
         res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
-        # dominant kernel: the sweep's interior rank-256 update U2 (nt - 1 launches per step; row /
-        # column k+1 go to the short U1 launch ahead of it).  Algorithmic bytes per launch: every
-        # updated lower 256-tile read and written once in fp32 -> 2 x 4 B x 256^2 per tile,
-        # (nt-2) (nt-1) / 2 tiles per dim (I, J not in {k, k+1}), x the dims of this rank.
+        # dominant kernel by GPU time: the S GEMM S = K^-1 V K^-1 (one launch per step), L np^2 (np + 1)
+        # fp32-equivalent flop (lower 256-tiles incl. the diagonal ones, whole), each a 3-product f16 split:
+        # 3 x that in f16 MFMA flop against the dense f16 peak
+        flops = Lr * np_ * np_ * (np_ + 1)
+        if syrk_ms > 0:
+            ach = X3_PRODUCTS * flops / (syrk_ms * 1e-3) / 1e12
+            res["roofline"] = {"kernel": "syrk_x3_kernel (S = K^-1 V K^-1, syrk_x3.hip; the largest GPU-time share of the step)",
+                               "bound": "mfma", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": ach / F16_MFMA_PEAK_TFLOPS,
+                               "traffic": pmc_traffic(("syrk_x3_kernel",)) if world == 1 else None,
+                               "traffic_source": os.path.basename(PMC_SUMMARY),
+                               "algorithmic_flop_per_launch": X3_PRODUCTS * flops,
+                               "fp32_equivalent_tflops": flops / (syrk_ms * 1e-3) / 1e12,
+                               "avg_launch_us": syrk_ms * 1e3,
+                               "engine": "f16 MFMA (v_mfma_f32_32x32x16_f16), 3-product split: achieved counts the 3 "
+                                         "f16 products per fp32-equivalent product"}
+        # secondary: the trailing rank-256 update of the Cholesky (U2, HBM-streaming); per step the passes
+        # k = 0 .. nt-3 update (nt-k-2)(nt-k-1)/2 tiles per dim, each read and written once in fp32
         nt = np_ // 256
         upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
-        tiles = (nt - 2) * (nt - 1) // 2 * Lr
+        tiles = sum((nt - k - 2) * (nt - k - 1) // 2 for k in range(nt - 2)) * Lr
         upd_bytes = 2 * 4 * 256 * 256 * tiles
         if upd_n:
-            avg_s = upd_ms / upd_n * 1e-3
-            ach = upd_bytes / avg_s / 1e9
-            res["roofline"] = {"kernel": "sw_update_kernel<0, 2> (sweep interior rank-256 update U2, spd_sweep.hip)",
-                               "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic((U2_NAME,)) if world == 1 else None,
-                               "algorithmic_bytes_per_launch": upd_bytes, "avg_launch_us": avg_s * 1e6,
-                               "launches_per_step": upd_n / args.steps, "padded_n": int(np_)}
-        # secondary: S = K^-1 V K^-1 (one launch per step): L N^2 (N+1) flop (lower triangle incl.
-        # the diagonal); engine: 3-product f16 split -> the f16 dense peak / 3
-        flops = Lr * np_ * np_ * (np_ + 1)
-        ach = flops / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
-        peak = F16_MFMA_PEAK_TFLOPS / X3_PRODUCTS
-        res["roofline_secondary"] = {"kernel": "syrk_x3_kernel (S = K^-1 V K^-1; operand planes written by the forward's kl_alpha_kernel)", "bound": "mfma",
-                                     "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                                     "frac": (ach / peak) if ach else None,
-                                     "traffic": pmc_traffic(("syrk_x3_kernel",)) if world == 1 else None,
-                                     "engine": "f16 MFMA, 3-product split (fp32-equivalent peak = 2.5 PF / 3)"}
+            ach = upd_bytes / (upd_ms / args.steps * 1e-3) / 1e9
+            launches = upd_n / args.steps
+            res["roofline_secondary"] = {"kernel": "ci_update_kernel<0> (potrf trailing rank-256 update U2, chol_inv.hip)",
+                                         "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                         "frac": ach / HBM_PEAK_GBS,
+                                         "traffic": pmc_traffic((U2_NAME,), per_step=True) if world == 1 else None,
+                                         "traffic_source": os.path.basename(PMC_SUMMARY),
+                                         "algorithmic_bytes_per_step": upd_bytes,
+                                         "algorithmic_bytes_per_launch": upd_bytes / launches,
+                                         "avg_launch_us": upd_ms / upd_n * 1e3, "launches_per_step": launches,
+                                         "padded_n": int(np_)}
     return res
 
 

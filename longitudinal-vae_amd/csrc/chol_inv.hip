@@ -85,8 +85,8 @@ struct CiScratch {
 };
 
 // ------------------------------------------------------------------------------------------
-// pivot(kb): A_kk (lower triangle) -> L_kk in LDS -> Y_kk = L_kk^-1; out: Y_kk planes (D, row-major; Y^T
-// tile (kb, kb), transposed) with the split scale of max |Y_kk|, log|A_kk|, info.  One 1024-thread
+// pivot(kb): A_kk (lower triangle) -> L_kk in LDS -> Y_kk = L_kk^-1; out: Y_kk planes (D, row-major)
+// with the split scale of max |Y_kk|, log|A_kk|, info.  One 1024-thread
 // workgroup per dim.  With `pending` (schedule (a), kb > 0) the block still lacks pass kb-1's update,
 // applied here: X = L_{kb,kb-1} = C_kb Y_{kb-1}^T (C planes of pass kb-1, block kb; D of kb-1), split
 // at its exact max into Xh / Xl, then A_kk - X X^T.
@@ -167,7 +167,6 @@ __device__ inline void ci_pending_update(const float* __restrict__ T, int64_t np
 }
 
 __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict__ Aall, int np_, int kb, CiScratch S,
-                                                        _Float16* __restrict__ YTh, _Float16* __restrict__ YTl,
                                                         double* __restrict__ logdet, int32_t* __restrict__ info,
                                                         int pending) {
   __shared__ float lf[kPvBlocks * kPvBlk];
@@ -275,9 +274,9 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
     __syncthreads();
   }
 
-  // 3. max |Y_kk| -> its split scale; out: D (row-major planes) and the transposed planes into tile
-  //    (kb, kb) of Y^T.  Thread (r0 = tid >> 6, c = 4 (tid & 63)) covers rows r0, r0 + 16, ... (a wave
-  //    writes one whole row of each: half4 runs).
+  // 3. max |Y_kk| -> its split scale; out: D (row-major planes; the diagonal copy puts them into the
+  //    Y and Y^T planes after potrf).  Thread (r0 = tid >> 6, c = 4 (tid & 63)) covers rows r0, r0 + 16,
+  //    ... (a wave writes one whole row: half4 runs).
   {
     float m = 0.f;
     for (int e = tid; e < kPvBlocks * 1024; e += 1024) {
@@ -292,29 +291,21 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
   const float sY = x3_scale(__uint_as_float(ymax_s));
   const int c = 4 * (tid & 63);
   const int64_t od = ((int64_t)l * S.nt + kb) * kSwBB;
-  const int64_t np2 = (int64_t)np_ * np_;
   _Float16* dh = S.Dh + od;
   _Float16* dl = S.Dl + od;
-  _Float16* th = YTh + l * np2 + (int64_t)kb * kSwB * np_ + kb * kSwB;
-  _Float16* tl = YTl + l * np2 + (int64_t)kb * kSwB * np_ + kb * kSwB;
   for (int r = tid >> 6; r < kSwB; r += 16) {
-    x3_half4 h4, l4, ht4, lt4;
+    x3_half4 h4, l4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int cq = c + q;
-      const float v = r >= cq ? pv_blk(lf, r >> 5, cq >> 5)[(r & 31) * kPvL + (cq & 31)] : 0.f;       // Y(r, cq)
-      const float vt = cq >= r ? pv_blk(lf, cq >> 5, r >> 5)[(cq & 31) * kPvL + (r & 31)] : 0.f;      // Y(cq, r)
-      const float y = v * sY, yt = vt * sY;
-      const _Float16 yh = (_Float16)y, yth = (_Float16)yt;
+      const float v = r >= cq ? pv_blk(lf, r >> 5, cq >> 5)[(r & 31) * kPvL + (cq & 31)] : 0.f;  // Y(r, cq)
+      const float y = v * sY;
+      const _Float16 yh = (_Float16)y;
       h4[q] = yh;
       l4[q] = (_Float16)(y - (float)yh);
-      ht4[q] = yth;
-      lt4[q] = (_Float16)(yt - (float)yth);
     }
     *reinterpret_cast<x3_half4*>(dh + r * kSwB + c) = h4;
     *reinterpret_cast<x3_half4*>(dl + r * kSwB + c) = l4;
-    *reinterpret_cast<x3_half4*>(th + (int64_t)r * np_ + c) = ht4;
-    *reinterpret_cast<x3_half4*>(tl + (int64_t)r * np_ + c) = lt4;
   }
   if (w == 0 && lane == 0) bad_s = bad;
   __syncthreads();
@@ -460,7 +451,7 @@ __global__ __launch_bounds__(512) void ci_panel_kernel(CiScratch S, int np_, int
 //   kCiU2  the trailing tiles I >= J >= k+2, in place
 // ------------------------------------------------------------------------------------------
 constexpr int kCiU2 = 0, kCiU1 = 1;
-constexpr int kCiFuseMaxL = 8;  // latent dims per call up to which the pivot updates its own block
+constexpr int kCiFuseMaxL = 16; // latent dims per call up to which the pivot updates its own block
 template <int MODE>
 __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall, CiScratch S, int np_, int k,
                                                         int ntl, int nwg) {
@@ -550,17 +541,42 @@ __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall
 }
 
 // D (the pivots' Y_kk planes) -> the diagonal tiles of the row-major Y planes (after potrf: the Y
-// planes alias A).  grid (nt, L), 256 threads.
+// planes alias A) and, transposed through LDS in 64 x 64 pieces, of the Y^T planes.  grid (nt, L),
+// 256 threads.
 __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_, _Float16* __restrict__ Yh,
-                                                           _Float16* __restrict__ Yl) {
-  const int k = blockIdx.x, l = blockIdx.y;
+                                                           _Float16* __restrict__ Yl, _Float16* __restrict__ YTh,
+                                                           _Float16* __restrict__ YTl) {
+  __shared__ _Float16 tp[2][64][66];
+  const int k = blockIdx.x, l = blockIdx.y, t = threadIdx.x;
   const int64_t od = ((int64_t)l * S.nt + k) * kSwBB;
   const int64_t ot = (int64_t)l * np_ * np_ + (int64_t)k * kSwB * np_ + k * kSwB;
-  for (int e = threadIdx.x; e < kSwBB / 8; e += 256) {
+  for (int e = t; e < kSwBB / 8; e += 256) {
     const int r = e >> 5, c = (e & 31) * 8;
     *reinterpret_cast<x3_half8*>(Yh + ot + (int64_t)r * np_ + c) = *reinterpret_cast<const x3_half8*>(S.Dh + od + r * kSwB + c);
     *reinterpret_cast<x3_half8*>(Yl + ot + (int64_t)r * np_ + c) = *reinterpret_cast<const x3_half8*>(S.Dl + od + r * kSwB + c);
   }
+  for (int pr = 0; pr < 4; ++pr)
+    for (int pc = 0; pc <= pr; ++pc) {  // the nonzero 64 x 64 pieces (pr, pc) of the lower-triangular Y_kk
+      __syncthreads();
+      for (int e = t; e < 64 * 64; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        tp[0][r][c] = S.Dh[od + (64 * pr + r) * kSwB + 64 * pc + c];
+        tp[1][r][c] = S.Dl[od + (64 * pr + r) * kSwB + 64 * pc + c];
+      }
+      __syncthreads();
+      for (int e = t; e < 64 * 64; e += 256) {  // Y^T (64 pc + c, 64 pr + r) = Y (64 pr + r, 64 pc + c)
+        const int c = e >> 6, r = e & 63;
+        YTh[ot + (int64_t)(64 * pc + c) * np_ + 64 * pr + r] = tp[0][r][c];
+        YTl[ot + (int64_t)(64 * pc + c) * np_ + 64 * pr + r] = tp[1][r][c];
+      }
+      if (pr != pc) {  // the mirrored piece of Y^T is zero (Y_kk is lower triangular)
+        for (int e = t; e < 64 * 64; e += 256) {
+          const int c = e >> 6, r = e & 63;
+          YTh[ot + (int64_t)(64 * pr + c) * np_ + 64 * pc + r] = (_Float16)0.f;
+          YTl[ot + (int64_t)(64 * pr + c) * np_ + 64 * pc + r] = (_Float16)0.f;
+        }
+      }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -745,14 +761,14 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
     if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
     const bool fuse = L <= kCiFuseMaxL;
     if (fuse) {
-      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, YTh, YTl, logdet, info, 0);
+      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
       if (!ok(hipEventRecord(sd->piv[0], sd->s))) return LVAE_ERR_LAUNCH;
       if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, st>>>(A, np_, S);
       if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
       for (int m = 0; m < nt; ++m) {
         if (m + 1 < nt) {
           if (!ok(hipStreamWaitEvent(sd->s, m == 0 ? sd->c : sd->u2p[(m - 1) & 1], 0))) return LVAE_ERR_LAUNCH;
-          ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, YTh, YTl, logdet, info, 1);
+          ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1);
           if (!ok(hipEventRecord(sd->piv[(m + 1) & 1], sd->s))) return LVAE_ERR_LAUNCH;
         }
         if (!ok(hipStreamWaitEvent(st, sd->piv[m & 1], 0))) return LVAE_ERR_LAUNCH;
@@ -770,7 +786,7 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
       }
     } else {
       if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
-      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, YTh, YTl, logdet, info, 0);
+      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
       if (nt > 1) ci_panel_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(S, np_, 0);
       if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
       for (int k = 0; k + 1 < nt; ++k) {
@@ -779,7 +795,7 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
         ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, k, n1, n1 * L);
         if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
         if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
-        ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, YTh, YTl, logdet, info, 0);
+        ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0);
         if (k + 2 < nt) ci_panel_kernel<<<dim3(nt - k - 2, L), 512, 0, sd->s>>>(S, np_, k + 1);
         if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
         const int n2 = (nt - k - 2) * (nt - k - 1) / 2;
@@ -799,7 +815,7 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
     _Float16* Yl = Yh + full;
     _Float16* XTh = reinterpret_cast<_Float16*>(Kinv);  // Kinv is not written yet: the X^T planes
     _Float16* XTl = XTh + full;
-    ci_diag_copy_kernel<<<dim3(nt, L), 256, 0, st>>>(S, np_, Yh, Yl);
+    ci_diag_copy_kernel<<<dim3(nt, L), 256, 0, st>>>(S, np_, Yh, Yl, YTh, YTl);
     for (int h = 1; h < nt; h *= 2) {
       const int ninst = (nt + 2 * h - 1) / (2 * h), per = ninst * h * h, nwg = per * L;
       CiGemmArgs gx{S.Lh, S.Ll, YTh, YTl, nullptr, nullptr, XTh, XTl, nullptr, np_, nt, h, per, nwg};

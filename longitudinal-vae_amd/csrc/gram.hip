@@ -500,51 +500,73 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
 // diagonal tiles are evaluated whole.  Components whose Cat / Bin gates are zero on a whole wave skip
 // their exp / sin factors.  Refining alpha = alpha0 + K^-1 r (kl_alpha_kernel) then makes K^-1 mu
 // (and mu^T K^-1 mu) fp64-accurate up to cond(K)^2 x the inverse's error (elbo_functions.py:27-30).
+// exp(x) for x <= 0 to ~1e-15 relative with a 64-entry table: 2^y = 2^m 2^(i/64) 2^f, y = x log2 e,
+// f in [0, 1/64) by a degree-5 polynomial (truncation (f ln 2)^6 / 720 < 3e-15) -- about half the fp64
+// instructions of the library exp.  tab[i] = 2^(i/64) in LDS.
+__device__ inline double exp_nonpos64(double x, const double* __restrict__ tab) {
+  constexpr double kLog2e = 1.4426950408889634074;
+  constexpr double kLn2 = 0.69314718055994530942;
+  const double y = fmax(x * kLog2e, -1100.0);
+  const double k = floor(y * 64.0);
+  const double f = (y - k * (1.0 / 64.0)) * kLn2;  // in [0, ln2 / 64)
+  const int ki = (int)k;
+  double p = 1.0 / 120.0;
+  p = fma(p, f, 1.0 / 24.0);
+  p = fma(p, f, 1.0 / 6.0);
+  p = fma(p, f, 0.5);
+  p = fma(p, f, 1.0);
+  p = fma(p, f, 1.0);
+  return ldexp(tab[ki & 63] * p, ki >> 6);
+}
+
+// Covariates are often integer-coded (time points, disease times): an RBF / periodic factor of an
+// integer distance |d| < kIntTab is read from a per-(component, factor) table of its fp64 values (the
+// same function of the same argument), and evaluated directly otherwise.
+constexpr int kIntTab = 64;
+__device__ inline double factor64_at(int kind, double ad, const double* __restrict__ pf,
+                                     const double* __restrict__ tab) {
+  if (kind == LVAE_RBF) return exp_nonpos64(-0.5 / (pf[0] * pf[0]) * ad * ad, tab);
+  const double sn = sin(ad * (M_PI / pf[1]));
+  return exp_nonpos64(-2.0 / (pf[0] * pf[0]) * sn * sn, tab);
+}
+
 __device__ inline void apply_factor64(int kind, int d, const double* __restrict__ pf, const double* __restrict__ sx1,
-                                      const double* __restrict__ sx2, int tr, int tc, double (&v)[4][4]) {
-  double xr[4], xc[4];
+                                      const double* __restrict__ sx2, int tr, int tc, int hf, double (&v)[2][4],
+                                      const double* __restrict__ tab, const double* __restrict__ itab) {
+  double xr[2], xc[4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
+  for (int a = 0; a < 2; ++a) xr[a] = sx1[d * kGT + (2 * hf + a) * 16 + tr];
 #pragma unroll
   for (int c = 0; c < 4; ++c) xc[c] = sx2[d * kGT + c * 16 + tc];
   if (kind == LVAE_CAT) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] == xc[c]) ? v[a][c] : 0.0;
   } else if (kind == LVAE_BIN) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] + xc[c] == 2.0) ? v[a][c] : 0.0;
-  } else if (kind == LVAE_RBF) {
-    const double cf = -0.5 / (pf[0] * pf[0]);
+  } else if (kind == LVAE_RBF || kind == LVAE_PER) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const double df = xr[a] - xc[c];
-        v[a][c] *= exp(cf * df * df);
-      }
-  } else if (kind == LVAE_PER) {
-    const double cf = -2.0 / (pf[0] * pf[0]), ip = M_PI / pf[1];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const double sn = sin(fabs(xr[a] - xc[c]) * ip);
-        v[a][c] *= exp(cf * sn * sn);
+        const double ad = fabs(xr[a] - xc[c]);
+        const bool hit = ad < (double)kIntTab && ad == floor(ad);
+        v[a][c] *= hit ? itab[hit ? (int)ad : 0] : factor64_at(kind, ad, pf, tab);
       }
   } else {  // LVAE_LIN
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[a][c] *= xr[a] * xc[c];
   }
 }
 
 template <int MC, int MF>
-__global__ __launch_bounds__(256) void kl_resid_tiles(DevSpec s, const double* __restrict__ x, int ldx, int n, int np_,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void kl_resid_tiles(DevSpec s, const double* __restrict__ x, int ldx, int n, int np_,
                                                       int qs, const double* __restrict__ params,
                                                       const double* __restrict__ noise,
                                                       const double* __restrict__ alpha, double* __restrict__ part,
@@ -554,9 +576,20 @@ __global__ __launch_bounds__(256) void kl_resid_tiles(DevSpec s, const double* _
   __shared__ double sp[64];
   __shared__ double sa1[kGT], sa2[kGT];
   __shared__ double cred[4][kGT];
+  __shared__ double tab[64];
+  __shared__ double itab[MC * MF * kIntTab];  // integer-distance tables, slot r * MF + f
   const int G = gridDim.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  if (tid < 64) tab[tid] = exp2((double)tid / 64.0);
   const int lane = tid & 63, wv = tid >> 6, nt = np_ / kGT;
   if (tid < s.n_params) sp[tid] = params[(int64_t)l * s.n_params + tid];
+  __syncthreads();
+  for (int e = tid; e < MC * MF * kIntTab; e += 256) {
+    const int r = e / (MF * kIntTab), f = (e / kIntTab) % MF, m = e % kIntTab;
+    double val = 0.0;
+    if (r < s.n_comp && f < s.n_fac[r] && (s.kind[r][f] == LVAE_RBF || s.kind[r][f] == LVAE_PER))
+      val = factor64_at(s.kind[r][f], (double)m, sp + s.param_idx[r][f], tab);
+    itab[e] = val;
+  }
   const double nz = noise[l];
   const double* al = alpha + (int64_t)l * np_;
   for (int t = blockIdx.x; t < ntiles; t += G) {
@@ -568,58 +601,68 @@ __global__ __launch_bounds__(256) void kl_resid_tiles(DevSpec s, const double* _
     if (tid < kGT) sa1[tid] = al[i0 + tid];
     else if (tid < 2 * kGT) sa2[tid - kGT] = al[j0 + tid - kGT];
     __syncthreads();
-    double k[4][4] = {};
+    // the 4 x 4 micro-tile in two halves of 2 rows (fewer live fp64 registers): row sums of block I
+    // (this tile's share, reduced over the 16 lanes tc of each row group) and the column sums of block
+    // J accumulated over both halves
+    double rs[4], cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
-    for (int r = 0; r < s.n_comp; ++r) {
-      double v[4][4];
-      const double sc = sp[s.scale_idx[r]];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[a][c] = sc;
-      // gates first (cheap, exact), then the transcendental factors unless the gates zeroed the wave
+    for (int hf = 0; hf < 2; ++hf) {
+      double k[2][4] = {};
 #pragma unroll 1
-      for (int f = 0; f < s.n_fac[r]; ++f) {
-        const int kind = s.kind[r][f];
-        if (kind != LVAE_CAT && kind != LVAE_BIN) continue;
-        apply_factor64(kind, s.dim[r][f], sp, sx1, sx2, tr, tc, v);
-      }
-      bool any = false;
+      for (int r = 0; r < s.n_comp; ++r) {
+        double v[2][4];
+        const double sc = sp[s.scale_idx[r]];
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) any |= v[a][c] != 0.0;
-      if (!__any(any)) continue;
+          for (int c = 0; c < 4; ++c) v[a][c] = sc;
+        // gates first (cheap, exact), then the transcendental factors unless the gates zeroed the wave
 #pragma unroll 1
-      for (int f = 0; f < s.n_fac[r]; ++f) {
-        const int kind = s.kind[r][f];
-        if (kind == LVAE_CAT || kind == LVAE_BIN) continue;
-        const int pi = s.param_idx[r][f];
-        apply_factor64(kind, s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
+        for (int f = 0; f < s.n_fac[r]; ++f) {
+          const int kind = s.kind[r][f];
+          if (kind != LVAE_CAT && kind != LVAE_BIN) continue;
+          apply_factor64(kind, s.dim[r][f], sp, sx1, sx2, tr, tc, hf, v, tab, itab);
+        }
+        bool any = false;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) any |= v[a][c] != 0.0;
+        if (!__any(any)) continue;
+#pragma unroll 1
+        for (int f = 0; f < s.n_fac[r]; ++f) {
+          const int kind = s.kind[r][f];
+          if (kind == LVAE_CAT || kind == LVAE_BIN) continue;
+          const int pi = s.param_idx[r][f];
+          apply_factor64(kind, s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, hf, v, tab,
+                         itab + (r * MF + f) * kIntTab);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) k[a][c] += v[a][c];
       }
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) k[a][c] += v[a][c];
-    }
+        for (int c = 0; c < 4; ++c) {
+          const int i = i0 + 4 * tr + 2 * hf + a, j = j0 + 4 * tc + c;
+          if (i >= n || j >= n) k[a][c] = 0.0;
+          else if (i == j) k[a][c] += nz;
+        }
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 2; ++a) {
+        double v = 0.0;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int i = i0 + 4 * tr + a, j = j0 + 4 * tc + c;
-        if (i >= n || j >= n) k[a][c] = 0.0;
-        else if (i == j) k[a][c] += nz;
+        for (int c = 0; c < 4; ++c) v += k[a][c] * sa2[4 * tc + c];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        rs[2 * hf + a] = v;
       }
-    // row sums of block I (this tile's share): reduce over the 16 lanes tc of each row group
-    double rs[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      double v = 0.0;
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v += k[a][c] * sa2[4 * tc + c];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-      rs[a] = v;
+        for (int a = 0; a < 2; ++a) cs[c] += k[a][c] * sa1[4 * tr + 2 * hf + a];
     }
     if (tc == 0) {
       double* pr = part + ((int64_t)l * nt + J) * np_ + i0 + 4 * tr;
@@ -627,15 +670,10 @@ __global__ __launch_bounds__(256) void kl_resid_tiles(DevSpec s, const double* _
       for (int a = 0; a < 4; ++a) pr[a] = rs[a];
     }
     if (I != J) {  // (uniform) column sums of block J: over tr (4 per wave, then the 4 waves)
-      double cs[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        double v = 0.0;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) v += k[a][c] * sa1[4 * tr + a];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        cs[c] = v;
+        cs[c] += __shfl_xor(cs[c], 16, 64);
+        cs[c] += __shfl_xor(cs[c], 32, 64);
       }
       if (lane < 16) {
 #pragma unroll

@@ -21,6 +21,7 @@
 // of one latent dim: neighbouring tiles share 256-row panels in that XCD's L2.  (The blocked order
 // of the sweep's update measured 10% slower here: with K = 4096 the panels stream through L2.)
 #include "x3_dma.hpp"
+#include "x3_gemm4.hpp"
 
 namespace lvae {
 
@@ -71,6 +72,45 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
     }
 }
 
+// The same S tiles on the 4-wave, 4-stage core (x3_gemm4.hpp): 256 threads, one wave per SIMD with
+// 128 x 128 each, 16-deep K chunks with three in flight across every barrier.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void syrk_x4_kernel(
+    const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl, const float* __restrict__ rsc, float* __restrict__ S,
+    float* __restrict__ Sx, int np_, int ntl, int nwg, int L, int kspan) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[kG4Lds];  // 128 KB, the only LDS object
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int sp = wgid / (ntl * L), l = (wgid / ntl) % L;
+  int I, J;
+  sx_tri(wgid % ntl, I, J);
+  const int64_t ld = np_;
+  const int64_t base = (int64_t)l * np_ * np_, k0 = (int64_t)sp * kspan;
+  const _Float16* ah = Bh + base + (int64_t)I * kG4T * ld + k0;
+  const _Float16* al = Bl + base + (int64_t)I * kG4T * ld + k0;
+  const _Float16* bh = Bh + base + (int64_t)J * kG4T * ld + k0;
+  const _Float16* bl = Bl + base + (int64_t)J * kG4T * ld + k0;
+  sx_f32x16 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = sx_f32x16{};
+  g4_gemm(ah, al, bh, bl, ld, kspan, lds, acc, [](int, sx_f32x16(&)[4][4]) {});
+  const float* rs = rsc + (int64_t)l * np_;
+  float* C = (sp == 0 ? S : Sx + (int64_t)(sp - 1) * L * np_ * np_) + base + (int64_t)(I * kG4T) * ld + J * kG4T;
+  float icol[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) icol[b] = 1.0f / rs[J * kG4T + g4_col(b)];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = g4_row(a, e);
+      const float irow = 1.0f / rs[I * kG4T + row];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) C[(int64_t)row * ld + g4_col(b)] = acc[a][b][e] * (irow * icol[b]);
+    }
+}
+
 // K splits of the S GEMM: a 256-CU chip holds one 512-thread workgroup per CU (128 KB of LDS), so
 // L * nt (nt + 1) / 2 tiles run in ceil(tiles / 256) rounds; with few latent dims per GPU (latent-dim
 // sharding) the last round is mostly empty (L = 2: 272 tiles = 2 rounds for 1.06 rounds of work).
@@ -103,4 +143,22 @@ int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float*
   return 0;
 }
 
+// dev A/B (not in the C ABI): the S GEMM on the 8-wave 2-stage core (variant 0) or the 4-wave 4-stage
+// core (variant 1), no K split
+int syrk_dev_variant(int variant, int np_, int L, const float* rsc, const _Float16* planes, float* S, hipStream_t st) {
+  if (np_ % kSxT) return -1;
+  const int64_t per = (int64_t)np_ * np_;
+  const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L;
+  if (variant == 0)
+    syrk_x3_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
+  else
+    syrk_x4_kernel<<<nwg, 256, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace lvae
+
+extern "C" int lvae_dev_syrk(int variant, int np_, int L, const float* rsc, const void* planes, float* S, void* stream) {
+  return lvae::syrk_dev_variant(variant, np_, L, rsc, (const _Float16*)planes, S, (hipStream_t)stream);
+}

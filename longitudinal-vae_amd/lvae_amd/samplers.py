@@ -44,10 +44,32 @@ def subject_rows(subjects, T):
     return (s[:, None] * T + torch.arange(T, dtype=torch.int64, device=s.device)[None, :]).reshape(-1)
 
 
-def hensman_batches(perm, P_b, T, rank=0, world=1):
+def _check_same_permutation(perm, group=None):
+    """Raise if the ranks of an initialised process group hold different subject orders (a sampler
+    built without a seed draws from each process's own NumPy global state): one MIN / MAX all-reduce
+    of a checksum of the order."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    p = np.asarray(perm, dtype=np.int64)
+    w = (np.arange(len(p), dtype=np.int64) * 2654435761) % 2147483647 + 1
+    h = int(((p + 1) * w).sum() % 2305843009213693951)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([h, -h], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    if int(t[0]) != h or int(t[1]) != -h:
+        raise ValueError("hensman_batches: ranks hold different subject orders -- build the SubjectSampler "
+                         "with the same explicit seed on every rank (or broadcast rank 0's permutation)")
+
+
+def hensman_batches(perm, P_b, T, rank=0, world=1, check=True, group=None):
     """Batches of one epoch for one rank: the global batch of world*P_b consecutive subjects of the
     permutation is split into contiguous per-rank slices of P_b subjects (the last global batch may be
-    short, as with drop_last=False; ranks whose slice is empty get no batch in that step)."""
+    short, as with drop_last=False; ranks whose slice is empty get no batch in that step).  With
+    world > 1 inside an initialised process group (and check=True) the ranks' orders are compared
+    first: different orders would silently give overlapping / missing subjects."""
+    if world > 1 and check:
+        _check_same_permutation(perm, group)
     perm = np.asarray(perm)
     G = world * P_b
     out = []

@@ -164,9 +164,18 @@ class _Deconv2Sigmoid(torch.autograd.Function):
         return gz, dw, db
 
 
+def _deconv2_lds_ok(cin, hi, wi):
+    """The LDS bounds lvae_deconv2_sigmoid_fwd / _bwd_f32 enforce (64 KB each; rc -3 beyond):
+    forward Cin ((Hi+2)(Wi+2) | 1) floats, backward (2Hi+2)(2Wi+2) + Cin Hi Wi floats."""
+    return (4 * cin * (((hi + 2) * (wi + 2)) | 1) <= 65536
+            and 4 * ((2 * hi + 2) * (2 * wi + 2) + cin * hi * wi) <= 65536)
+
+
 def deconv_sigmoid(deconv, z):
-    """sigmoid(deconv(z)) for the decoder's last layer: fused HIP path for CUDA fp32."""
+    """sigmoid(deconv(z)) for the decoder's last layer: fused HIP path for CUDA fp32 (torch's
+    transposed conv + sigmoid when the geometry or the kernel's LDS bound rules it out)."""
     if (z.is_cuda and z.dtype == torch.float32 and deconv.weight.dtype == torch.float32 and deconv.bias is not None
+            and z.dim() == 4 and _deconv2_lds_ok(z.shape[1], z.shape[2], z.shape[3])
             and deconv.out_channels == 1 and deconv.in_channels <= 16 and tuple(deconv.kernel_size) == (4, 4)
             and tuple(deconv.stride) == (2, 2) and tuple(deconv.padding) == (1, 1)
             and tuple(deconv.output_padding) == (0, 0) and tuple(deconv.dilation) == (1, 1) and deconv.groups == 1):

@@ -21,8 +21,9 @@ def main(out_dir):
                 a = acc[(name, counter)]
                 a[0] += v
                 a[1] += 1
+        steps = int(os.environ.get("PMC_STEPS", "3"))  # bench steps + warm-up steps of each pass
         for (name, c), (s, n) in acc.items():
-            res.setdefault(c, {})[name] = {"mean": s / n, "dispatches": n}
+            res.setdefault(c, {})[name] = {"mean": s / n, "dispatches": n, "per_step": s / steps}
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as f:
         json.dump(res, f, indent=1)
     keys = os.environ.get("PMC_KERNELS", "").split(",")

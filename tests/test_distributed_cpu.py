@@ -67,6 +67,16 @@ def _worker(rank, world, port, q):
         b = torch.full((2, 2), float(10 * (rank + 1)))
         allreduce_tensors([a, b], average=False)
         q.put(("sum", rank, a.numpy().copy(), b.numpy().copy()))
+        # --- hensman_batches refuses per-rank subject orders that differ ---
+        from lvae_amd.samplers import SubjectSampler, hensman_batches
+        same = SubjectSampler(P_tot, T, seed=4).permutation()
+        hensman_batches(same, P_b, T, rank, world)  # agreeing orders pass
+        own = SubjectSampler(P_tot, T, seed=100 + rank).permutation()
+        try:
+            hensman_batches(own, P_b, T, rank, world)
+            q.put(("perm", rank, False))
+        except ValueError:
+            q.put(("perm", rank, True))
     finally:
         dist.destroy_process_group()
 
@@ -78,7 +88,7 @@ def test_gloo_world2_dp_contract():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in range(2 * world)]
+    res = [q.get(timeout=300) for _ in range(3 * world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -115,6 +125,7 @@ def test_gloo_world2_dp_contract():
     assert abs(hens[0][4] - kld.item()) <= 1e-10 * abs(kld.item())
     for _, _, a, b in sums:
         assert np.allclose(a, 3.0) and np.allclose(b, 30.0)
+    assert all(r[2] for r in res if r[0] == "perm")  # every rank detected the mismatch
 
 
 def test_hensman_batch_sharding():
