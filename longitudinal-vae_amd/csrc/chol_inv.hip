@@ -541,42 +541,34 @@ __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall
 }
 
 // D (the pivots' Y_kk planes) -> the diagonal tiles of the row-major Y planes (after potrf: the Y
-// planes alias A) and, transposed through LDS in 64 x 64 pieces, of the Y^T planes.  grid (nt, L),
-// 256 threads.
+// planes alias A) and, transposed through LDS, of the Y^T planes.  grid (16 nt, L): one 256-thread
+// workgroup per 64 x 64 piece (a, b) of a diagonal tile, Y (a, b) = D (a, b) and Y^T (b, a) = D (a, b)^T.
 __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_, _Float16* __restrict__ Yh,
                                                            _Float16* __restrict__ Yl, _Float16* __restrict__ YTh,
                                                            _Float16* __restrict__ YTl) {
   __shared__ _Float16 tp[2][64][66];
-  const int k = blockIdx.x, l = blockIdx.y, t = threadIdx.x;
-  const int64_t od = ((int64_t)l * S.nt + k) * kSwBB;
+  const int k = blockIdx.x >> 4, pa = (blockIdx.x >> 2) & 3, pb = blockIdx.x & 3, l = blockIdx.y, t = threadIdx.x;
+  const int64_t od = ((int64_t)l * S.nt + k) * kSwBB + (int64_t)(64 * pa) * kSwB + 64 * pb;
   const int64_t ot = (int64_t)l * np_ * np_ + (int64_t)k * kSwB * np_ + k * kSwB;
-  for (int e = t; e < kSwBB / 8; e += 256) {
-    const int r = e >> 5, c = (e & 31) * 8;
-    *reinterpret_cast<x3_half8*>(Yh + ot + (int64_t)r * np_ + c) = *reinterpret_cast<const x3_half8*>(S.Dh + od + r * kSwB + c);
-    *reinterpret_cast<x3_half8*>(Yl + ot + (int64_t)r * np_ + c) = *reinterpret_cast<const x3_half8*>(S.Dl + od + r * kSwB + c);
-  }
-  for (int pr = 0; pr < 4; ++pr)
-    for (int pc = 0; pc <= pr; ++pc) {  // the nonzero 64 x 64 pieces (pr, pc) of the lower-triangular Y_kk
-      __syncthreads();
-      for (int e = t; e < 64 * 64; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        tp[0][r][c] = S.Dh[od + (64 * pr + r) * kSwB + 64 * pc + c];
-        tp[1][r][c] = S.Dl[od + (64 * pr + r) * kSwB + 64 * pc + c];
-      }
-      __syncthreads();
-      for (int e = t; e < 64 * 64; e += 256) {  // Y^T (64 pc + c, 64 pr + r) = Y (64 pr + r, 64 pc + c)
-        const int c = e >> 6, r = e & 63;
-        YTh[ot + (int64_t)(64 * pc + c) * np_ + 64 * pr + r] = tp[0][r][c];
-        YTl[ot + (int64_t)(64 * pc + c) * np_ + 64 * pr + r] = tp[1][r][c];
-      }
-      if (pr != pc) {  // the mirrored piece of Y^T is zero (Y_kk is lower triangular)
-        for (int e = t; e < 64 * 64; e += 256) {
-          const int c = e >> 6, r = e & 63;
-          YTh[ot + (int64_t)(64 * pr + c) * np_ + 64 * pc + r] = (_Float16)0.f;
-          YTl[ot + (int64_t)(64 * pr + c) * np_ + 64 * pc + r] = (_Float16)0.f;
-        }
-      }
+  const int64_t oy = ot + (int64_t)(64 * pa) * np_ + 64 * pb, oyt = ot + (int64_t)(64 * pb) * np_ + 64 * pa;
+  for (int e = t; e < 64 * 8; e += 256) {  // rows of 8-half vectors: direct copy + LDS image
+    const int r = e >> 3, c = (e & 7) * 8;
+    const x3_half8 h = *reinterpret_cast<const x3_half8*>(S.Dh + od + r * kSwB + c);
+    const x3_half8 lo = *reinterpret_cast<const x3_half8*>(S.Dl + od + r * kSwB + c);
+    *reinterpret_cast<x3_half8*>(Yh + oy + (int64_t)r * np_ + c) = h;
+    *reinterpret_cast<x3_half8*>(Yl + oy + (int64_t)r * np_ + c) = lo;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      tp[0][r][c + q] = h[q];
+      tp[1][r][c + q] = lo[q];
     }
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * 64; e += 256) {  // Y^T (b, a) row c, column r = D (a, b) (r, c)
+    const int c = e >> 6, r = e & 63;
+    YTh[oyt + (int64_t)c * np_ + r] = tp[0][r][c];
+    YTl[oyt + (int64_t)c * np_ + r] = tp[1][r][c];
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -599,6 +591,7 @@ struct CiGemmArgs {
   _Float16 *oh, *ol, *oth, *otl;      // outputs: row-major planes (kCiY), transposed planes (kCiX, kCiY)
   float* Kinv;                         // kCiLauum
   int np_, nt, h, per_dim, nwg;        // per_dim: workgroups per latent dim
+  int inst0;                           // trtri: first recursive-doubling instance of the launch
 };
 
 template <int MODE>
@@ -606,18 +599,32 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   __shared__ float sprod[64];
   __shared__ uint32_t red;
-  const int orig = blockIdx.x, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int l = wgid / g.per_dim, t = wgid % g.per_dim, nt = g.nt, np_ = g.np_;
-  int i, j, kb0, kb1;
+  const int nt = g.nt, np_ = g.np_;
+  int l, i, j, kb0, kb1;
   if constexpr (MODE == kCiLauum) {
-    sx_tri(t, i, j);
+    // XCD-contiguous remap, 4 x 8 blocks of tiles sharing their Y^T panels in an XCD's L2 (small I,
+    // the longest K ranges, first)
+    const int orig = blockIdx.x, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    l = wgid / g.per_dim;
+    sx_tri_blocked(wgid % g.per_dim, nt, i, j);
     kb0 = i;
     kb1 = nt;
   } else {
-    const int h = g.h, hh2 = h * h, m = t / hh2, r = t % hh2, o = 2 * h * m;
-    i = o + h + r / h;
-    j = o + r % h;
+    // longest K first over the whole launch (the tiles of a level span K = 1 .. h blocks): block b
+    // takes latent dim b % L (an XCD then keeps the dims b % 8 selects, and their panels) and the
+    // t = b / L-th tile of a K-descending order -- X: K = o + h - j, so j_off = j - o ascending; Y:
+    // K = i - o - h + 1, so i_off = i - o - h descending; then the instance, then the other index
+    const int L = g.nwg / g.per_dim, t = blockIdx.x / L, h = g.h, ninst = g.per_dim / (h * h);
+    l = blockIdx.x % L;
+    const int slow = t / (ninst * h), rem = t % (ninst * h), m = g.inst0 + rem / h, fast = rem % h, o = 2 * h * m;
+    if constexpr (MODE == kCiX) {
+      j = o + slow;
+      i = o + h + fast;
+    } else {
+      i = o + h + (h - 1 - slow);
+      j = o + fast;
+    }
     if (i >= nt) return;  // (uniform: before any barrier)
     if constexpr (MODE == kCiX) {
       kb0 = j;
@@ -736,9 +743,12 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
 //       side:  [wait ev_c;  pivot(k+1);  panel(k+1);  record ev_prep]...
 // Buffers: U1(k) writes C planes (k+1) & 1, read by panel(k+1) (and pivot(k+2)'s pending update in (a));
 // their previous readers (panel(k-1), pivot(k)) precede U1(k) on the caller's stream.  The L planes of
-// column k are written once (panel(k)) and read by U1(k), U2(k), and trtri; D and the Y^T diagonal tiles
-// by the pivots only.  Then, on the caller's stream: the diagonal copy, trtri (2 launches per level),
-// lauum.
+// column k are written once (panel(k)) and read by U1(k), U2(k), and trtri; D by the pivots, the panels
+// and the diagonal copies.
+// Then, on the caller's stream: the diagonal copy, trtri (2 launches per level), lauum.  (Launching each
+// recursive-doubling instance as soon as potrf had produced its blocks -- 2 small launches per
+// instance on the caller's stream between the passes -- measured 15.1 vs 14.2 ms per closed step at
+// L = 16: the small launches slowed the passes more than the overlap saved.)
 size_t ci_scratch_bytes(int np_, int L) { return CiScratch(nullptr, np_, L).bytes; }
 
 int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
@@ -750,6 +760,10 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
   const int64_t full = (int64_t)L * np_ * np_;
   _Float16* YTh = YT;
   _Float16* YTl = YT + full;
+  _Float16* Yh = reinterpret_cast<_Float16*>(A);  // A is dead after potrf: the Y planes
+  _Float16* Yl = Yh + full;
+  _Float16* XTh = reinterpret_cast<_Float16*>(Kinv);  // Kinv is written last (lauum): the X^T planes until then
+  _Float16* XTl = XTh + full;
   auto ok = [](hipError_t e) { return e == hipSuccess; };
   {
     ProfScope ps(LVAE_PH_POTRF, st);
@@ -790,7 +804,7 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
       if (nt > 1) ci_panel_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(S, np_, 0);
       if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
       for (int k = 0; k + 1 < nt; ++k) {
-        if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // panel(k)
+        if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // pivot(k), panel(k)
         const int n1 = nt - k - 1;  // column k+1 with the pivot block
         ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, k, n1, n1 * L);
         if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
@@ -809,22 +823,18 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
   }
   LVAE_CHECK_LAUNCH();
   {
-    // trtri + lauum (the rest of potri)
+    // trtri (recursive doubling, 2 launches per level) + lauum: the rest of potri
     ProfScope ps(LVAE_PH_POTRI, st);
-    _Float16* Yh = reinterpret_cast<_Float16*>(A);  // A is dead: the Y planes
-    _Float16* Yl = Yh + full;
-    _Float16* XTh = reinterpret_cast<_Float16*>(Kinv);  // Kinv is not written yet: the X^T planes
-    _Float16* XTl = XTh + full;
-    ci_diag_copy_kernel<<<dim3(nt, L), 256, 0, st>>>(S, np_, Yh, Yl, YTh, YTl);
+    ci_diag_copy_kernel<<<dim3(16 * nt, L), 256, 0, st>>>(S, np_, Yh, Yl, YTh, YTl);
     for (int h = 1; h < nt; h *= 2) {
       const int ninst = (nt + 2 * h - 1) / (2 * h), per = ninst * h * h, nwg = per * L;
-      CiGemmArgs gx{S.Lh, S.Ll, YTh, YTl, nullptr, nullptr, XTh, XTl, nullptr, np_, nt, h, per, nwg};
+      CiGemmArgs gx{S.Lh, S.Ll, YTh, YTl, nullptr, nullptr, XTh, XTl, nullptr, np_, nt, h, per, nwg, 0};
       ci_gemm_kernel<kCiX><<<nwg, 512, 0, st>>>(gx, S);
-      CiGemmArgs gy{Yh, Yl, XTh, XTl, Yh, Yl, YTh, YTl, nullptr, np_, nt, h, per, nwg};
+      CiGemmArgs gy{Yh, Yl, XTh, XTl, Yh, Yl, YTh, YTl, nullptr, np_, nt, h, per, nwg, 0};
       ci_gemm_kernel<kCiY><<<nwg, 512, 0, st>>>(gy, S);
     }
     const int per = nt * (nt + 1) / 2, nwg = per * L;
-    CiGemmArgs gl{YTh, YTl, YTh, YTl, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg};
+    CiGemmArgs gl{YTh, YTl, YTh, YTl, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg, 0};
     ci_gemm_kernel<kCiLauum><<<nwg, 512, 0, st>>>(gl, S);
   }
   LVAE_CHECK_LAUNCH();

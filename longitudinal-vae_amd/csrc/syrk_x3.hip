@@ -18,13 +18,16 @@
 // per-lane GLOBAL address of the DMA (its LDS side is lane-linear).
 //
 // Blocks are remapped so that each XCD (blockIdx % 8) works through a contiguous range of tiles
-// of one latent dim: neighbouring tiles share 256-row panels in that XCD's L2.  (The blocked order
-// of the sweep's update measured 10% slower here: with K = 4096 the panels stream through L2.)
+// of one latent dim, in the blocked order of sx_tri_blocked (row blocks of 4, inside a block by
+// column): the 32 tiles an XCD runs at once form a 4 x 8 block sharing 4 A and 8 B panels in its L2
+// (r3, scripts/gemm_ab.py: 3.19 vs 3.46 ms at np = 4096, L = 16 against the row-major order; 51.1 vs
+// 55.9 ms at np = 16384, L = 4).
 #include "x3_dma.hpp"
 #include "x3_gemm4.hpp"
 
 namespace lvae {
 
+template <int ORDER = 0>
 __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
                                                       const float* __restrict__ rsc, float* __restrict__ S,
                                                       float* __restrict__ Sx, int np_, int ntl, int nwg, int L,
@@ -35,7 +38,10 @@ __global__ __launch_bounds__(512) void syrk_x3_kernel(const _Float16* __restrict
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int sp = wgid / (ntl * L), l = (wgid / ntl) % L;  // K split, latent dim
   int I, J;
-  sx_tri(wgid % ntl, I, J);
+  if constexpr (ORDER == 0)
+    sx_tri(wgid % ntl, I, J);
+  else
+    sx_tri_blocked(wgid % ntl, np_ / kSxT, I, J);
   const int64_t ld = np_;
   const int64_t base = (int64_t)l * np_ * np_, k0 = (int64_t)sp * kspan;
   const _Float16* ah = Bh + base + (int64_t)I * kSxT * ld + k0;
@@ -111,6 +117,114 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
 }
 
+// Variant: 256 x 128 half tiles, TWO independent 256-thread workgroups per CU (72 KB of LDS each),
+// each 4 waves of 128 x 64 and a 3-stage ring of 16-deep K chunks (one in flight across each barrier):
+// when one workgroup waits at its barrier the other one's MFMAs run.
+constexpr int kH2BK = 16, kH2NS = 3;
+constexpr int kH2A = 256 * kH2BK, kH2B = 128 * kH2BK;   // halves per A / B plane and stage
+constexpr int kH2Stage = 2 * kH2A + 2 * kH2B;          // 24 KB
+__device__ inline void h2_issue(const _Float16* __restrict__ ah, const _Float16* __restrict__ al,
+                                const _Float16* __restrict__ bh, const _Float16* __restrict__ bl, int64_t ld, int k0,
+                                _Float16* __restrict__ stage) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // 24 wave-instructions of 32 rows x 2 chunks: A hi / lo 8 each, B hi / lo 4 each; wave w takes 6
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int ins = 6 * w + q;
+    const _Float16* src;
+    _Float16* dst;
+    int blk;
+    if (ins < 16) {
+      src = ins < 8 ? ah : al;
+      blk = ins & 7;
+      dst = stage + (ins < 8 ? 0 : kH2A);
+    } else {
+      src = ins < 20 ? bh : bl;
+      blk = (ins - 16) & 3;
+      dst = stage + 2 * kH2A + (ins < 20 ? 0 : kH2B);
+    }
+    const int row = 32 * blk + (lane >> 1);
+    const int c = (lane & 1) ^ ((row >> 3) & 1);
+    __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)row * ld + k0 + 8 * c), (void*)(dst + blk * 512), 16,
+                                     0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void syrk_h2_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
+                                                         const float* __restrict__ rsc, float* __restrict__ S, int np_,
+                                                         int nth, int nwg, int L) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[kH2NS * kH2Stage];  // 72 KB, the only LDS object
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int l = wgid / nth, t = wgid % nth;
+  // half tiles (I, J2), J2 <= 2 I + 1, in blocks of 4 tile rows (all half columns of a row block first)
+  int I, J2;
+  {
+    int r, c;
+    sx_tri(t >> 1, r, c);  // whole-tile lower index, two halves each
+    I = r;
+    J2 = 2 * c + (t & 1);
+  }
+  const int ld = np_;
+  const int64_t base = (int64_t)l * np_ * np_;
+  const _Float16* ah = Bh + base + (int64_t)I * 256 * ld;
+  const _Float16* al = Bl + base + (int64_t)I * 256 * ld;
+  const _Float16* bh = Bh + base + (int64_t)J2 * 128 * ld;
+  const _Float16* bl = Bl + base + (int64_t)J2 * 128 * ld;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * 128, wn = (w & 1) * 64;
+  const int r32 = lane & 31, kh = lane >> 5;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  const int nk = np_ / kH2BK;
+  h2_issue(ah, al, bh, bl, ld, 0, lds);
+  if (nk > 1) h2_issue(ah, al, bh, bl, ld, kH2BK, lds + kH2Stage);
+  for (int s = 0; s < nk; ++s) {
+    if (s + 1 < nk) __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6): stage s landed, s + 1 in flight
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < nk) h2_issue(ah, al, bh, bl, ld, (s + 2) * kH2BK, lds + ((s + 2) % kH2NS) * kH2Stage);
+    const _Float16* cur = lds + (s % kH2NS) * kH2Stage;
+    __builtin_amdgcn_s_setprio(1);
+    sx_half8 bH[2], bL[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      bH[b] = g4_frag(cur + 2 * kH2A, wn + 32 * b + r32, kh);
+      bL[b] = g4_frag(cur + 2 * kH2A + kH2B, wn + 32 * b + r32, kh);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const sx_half8 aH = g4_frag(cur, wm + 32 * a + r32, kh);
+      const sx_half8 aL = g4_frag(cur + kH2A, wm + 32 * a + r32, kh);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH[b], acc[a][b], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  const float* rs = rsc + (int64_t)l * np_;
+  float* C = S + base + (int64_t)(I * 256 + wm) * ld + J2 * 128 + wn;
+  float icol[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) icol[b] = 1.0f / rs[J2 * 128 + wn + 32 * b + r32];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = 32 * a + (e & 3) + 8 * (e >> 2) + 4 * kh;
+      const float irow = 1.0f / rs[I * 256 + wm + row];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) C[(int64_t)row * ld + 32 * b + r32] = acc[a][b][e] * (irow * icol[b]);
+    }
+}
+
 // K splits of the S GEMM: a 256-CU chip holds one 512-thread workgroup per CU (128 KB of LDS), so
 // L * nt (nt + 1) / 2 tiles run in ceil(tiles / 256) rounds; with few latent dims per GPU (latent-dim
 // sharding) the last round is mostly empty (L = 2: 272 tiles = 2 rounds for 1.06 rounds of work).
@@ -138,7 +252,7 @@ int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float*
   const int ns = syrk_x3_splits(np_, L);
   if (ns > 1 && !Sx) return -2;
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L * ns;
-  syrk_x3_kernel<<<nwg, 512, 0, st>>>(Bh, Bl, rsc, S, Sx, np_, ntl, nwg, L, np_ / ns);
+  syrk_x3_kernel<1><<<nwg, 512, 0, st>>>(Bh, Bl, rsc, S, Sx, np_, ntl, nwg, L, np_ / ns);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -150,7 +264,11 @@ int syrk_dev_variant(int variant, int np_, int L, const float* rsc, const _Float
   const int64_t per = (int64_t)np_ * np_;
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L;
   if (variant == 0)
-    syrk_x3_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
+    syrk_x3_kernel<0><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
+  else if (variant == 2)
+    syrk_x3_kernel<1><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
+  else if (variant == 3)
+    syrk_h2_kernel<<<2 * nwg, 256, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, np_, 2 * ntl, 2 * nwg, L);
   else
     syrk_x4_kernel<<<nwg, 256, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
   LVAE_CHECK_LAUNCH();

@@ -1,5 +1,6 @@
 """A/B of the S-GEMM cores (lvae_dev_syrk: variant 0 = 8-wave 2-stage x3_dma core, 1 = 4-wave 4-stage
-x3_gemm4 core) on random pre-split planes: time per launch and agreement of the lower tiles."""
+x3_gemm4 core, 2 = variant 0 with the 4-row-block tile order) on random pre-split planes: time per
+launch and agreement of the lower tiles."""
 import ctypes
 import os
 import sys
@@ -23,7 +24,7 @@ def run(np_, L, reps=5):
     planes = torch.cat([hi.reshape(-1), lo.reshape(-1)]).contiguous()
     rsc = torch.ones(L, np_, device="cuda")
     out = {}
-    for v in (0, 1):
+    for v in VARIANTS:
         S = torch.zeros(L, np_, np_, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
         for _ in range(2):
@@ -41,9 +42,11 @@ def run(np_, L, reps=5):
         print(f"np={np_} L={L} variant {v}: {ms:.3f} ms  {flops / ms / 1e9:.1f} TF (fp32-equiv), "
               f"{flops / ms / 1e9 / 833.3:.3f} of x3 peak", flush=True)
     tril = torch.tril(torch.ones(np_, np_, device="cuda", dtype=torch.bool))
-    a, b = out[0][1][:, tril], out[1][1][:, tril]
+    a, b = out[VARIANTS[0]][1][:, tril], out[VARIANTS[-1]][1][:, tril]
     print(f"  max rel diff {float((a - b).abs().max() / b.abs().max()):.2e}", flush=True)
 
+
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,2").split(",")]
 
 if __name__ == "__main__":
     run(4096, 16)
