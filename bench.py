@@ -305,10 +305,10 @@ def run_closed(args, world, rank, dev):
         flops = Lr * np_ * np_ * (np_ + 1)
         if syrk_ms > 0:
             ach = X3_PRODUCTS * flops / (syrk_ms * 1e-3) / 1e12
-            res["roofline"] = {"kernel": "syrk_x3_kernel (S = K^-1 V K^-1, syrk_x3.hip; the largest GPU-time share of the step)",
+            res["roofline"] = {"kernel": "syrk_tiles_kernel (S = K^-1 V K^-1, syrk_x3.hip; the largest GPU-time share of the step)",
                                "bound": "mfma", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                               "traffic": pmc_traffic(("syrk_x3_kernel",)) if world == 1 else None,
+                               "traffic": pmc_traffic(("syrk_tiles_kernel",)) if world == 1 else None,
                                "traffic_source": os.path.basename(PMC_SUMMARY),
                                "algorithmic_flop_per_launch": X3_PRODUCTS * flops,
                                "fp32_equivalent_tflops": flops / (syrk_ms * 1e-3) / 1e12,

@@ -585,23 +585,97 @@ __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_,
 // trtri launches cover every (instance m, ii, jj) of level h: i = o + h + ii, j = o + jj, o = 2 h m
 // (workgroups with i >= nt exit at once); lauum the L nt (nt + 1) / 2 lower tiles.
 // ------------------------------------------------------------------------------------------
-constexpr int kCiX = 0, kCiY = 1, kCiLauum = 2;
+constexpr int kCiX = 0, kCiY = 1, kCiLauum = 2, kCiLauumKL = 3;
 struct CiGemmArgs {
   const _Float16 *ah, *al, *bh, *bl;  // full plane arrays
   _Float16 *oh, *ol, *oth, *otl;      // outputs: row-major planes (kCiY), transposed planes (kCiX, kCiY)
-  float* Kinv;                         // kCiLauum
+  float* Kinv;                         // kCiLauum(KL)
   int np_, nt, h, per_dim, nwg;        // per_dim: workgroups per latent dim
   int inst0;                           // trtri: first recursive-doubling instance of the launch
+  // kCiLauumKL (the exact KL's reduce, kl_closed.hip): mu [L, np] fp64 and sqrt v [L, np] in; out the
+  // partials of K^-1 mu, apart[l][s][p] = sum over column block s of Kinv(p, .) mu (every (s, p) once),
+  // and -- if bh -- the fp16 hi / lo planes of B = K^-1 diag(sqrt v) (row stride np) split with the
+  // dim's scale bsc[l] (ci_bscale_kernel)
+  const double* mu;
+  const float* sv;
+  float* apart;
+  _Float16 *bh_out, *bl_out;
+  float* bsc;
 };
+
+// one halving butterfly step over lane bit D (D <= 16): the lane keeps the half of its N partial sums
+// its bit selects and adds the partner's copy of that half
+template <int D, int N>
+__device__ inline void ci_bfly(float (&x)[32], int lane) {
+  const bool up = (lane & D) != 0;
+#pragma unroll
+  for (int q = 0; q < N / 2; ++q) {
+    const float send = up ? x[q] : x[q + N / 2];
+    const float keep = up ? x[q + N / 2] : x[q];
+    x[q] = keep + __shfl_xor(send, D, 64);
+  }
+}
+
+// kCiLauumKL: the partials of K^-1 mu from the tile T = acc * inv = (K^-1)_ij (i >= j): the rows,
+// apart[l][j][256 i + r] = sum_c T(r, c) mu_j(c), and for i != j the mirror's rows,
+// apart[l][i][256 j + c] = sum_r T(r, c) mu_i(r).  smu = mu_i (0..255), mu_j (256..511); spart 6 x 256
+// floats of LDS.  Row sums: each lane's 2 columns, then per pair of 32-row blocks a halving butterfly
+// over the 32 lanes of a half-wave (31 shuffles; lane t ends with the t-th of the pair's 32 rows of its
+// half-wave), then the 4 column waves in a fixed order in LDS; column sums: each lane's 64 rows, the
+// other half-wave, the 2 row waves.  fp32: the KL refines K^-1 mu in fp64 after (kl_closed.hip).
+__device__ inline void ci_kl_partials(const sx_f32x16 (&acc)[4][2], float inv, const CiGemmArgs& g, int l, int i,
+                                      int j, const float* smu, float* spart) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, kh = lane >> 5;
+  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
+  const float m0 = smu[kSwB + wn + r32], m1 = smu[kSwB + wn + 32 + r32];
+#pragma unroll
+  for (int a2 = 0; a2 < 4; a2 += 2) {
+    float x[32];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) x[16 * a + e] = acc[a2 + a][0][e] * m0 + acc[a2 + a][1][e] * m1;
+    ci_bfly<16, 32>(x, lane);
+    ci_bfly<8, 16>(x, lane);
+    ci_bfly<4, 8>(x, lane);
+    ci_bfly<2, 4>(x, lane);
+    ci_bfly<1, 2>(x, lane);
+    const int a = a2 + (r32 >> 4), e = r32 & 15;
+    spart[(w & 3) * kSwB + wm + 32 * a + (e & 3) + 8 * (e >> 2) + 4 * kh] = x[0];
+  }
+  if (i != j) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float cs = 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cs += acc[a][b][e] * smu[sx_row(a, e)];
+      cs += __shfl_xor(cs, 32, 64);
+      if (kh == 0) spart[(4 + (w >> 2)) * kSwB + wn + 32 * b + r32] = cs;
+    }
+  }
+  __syncthreads();
+  const int np_ = g.np_, nt = g.nt;
+  float* ap = g.apart + (int64_t)l * nt * np_;
+  if (tid < kSwB) {
+    const float s = ((spart[tid] + spart[kSwB + tid]) + spart[2 * kSwB + tid]) + spart[3 * kSwB + tid];
+    ap[(int64_t)j * np_ + i * kSwB + tid] = s * inv;
+  } else if (i != j) {
+    const int c = tid - kSwB;
+    ap[(int64_t)i * np_ + j * kSwB + c] = (spart[4 * kSwB + c] + spart[5 * kSwB + c]) * inv;
+  }
+}
 
 template <int MODE>
 __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   __shared__ float sprod[64];
   __shared__ uint32_t red;
+  __shared__ float kl_mu[2 * kSwB], kl_sv[2 * kSwB], kl_part[6 * kSwB];  // (kCiLauumKL only)
   const int nt = g.nt, np_ = g.np_;
   int l, i, j, kb0, kb1;
-  if constexpr (MODE == kCiLauum) {
+  if constexpr (MODE == kCiLauum || MODE == kCiLauumKL) {
     // XCD-contiguous remap, 4 x 8 blocks of tiles sharing their Y^T panels in an XCD's L2 (small I,
     // the longest K ranges, first)
     const int orig = blockIdx.x, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
@@ -665,31 +739,13 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
-  constexpr int cpb = kSwB / kSxBK;  // K chunks per block
-  const int nk = nkb * cpb;
-  float scur = 1.f;
-  sx_issue(ah, al, bh, bl, np_, 0, lds);
-  for (int s = 0; s < nk; ++s) {
-    SX_WAIT_VM(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 1 < nk) sx_issue(ah, al, bh, bl, np_, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
-    if (s % cpb == 0) {  // a new block pair: move the accumulators to its units
-      const float snew = sprod[s / cpb];
-      if (s) {
-        const float ratio = snew / scur;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b) acc[a][b] *= ratio;
-      }
-      scur = snew;
-    }
-    __builtin_amdgcn_s_setprio(1);
-    sx_mma_stage(lds + (s & 1) * 4 * kSxPart, acc);
-    __builtin_amdgcn_s_setprio(0);
+  if constexpr (MODE == kCiLauumKL) {  // mu and sqrt v of row block i (0..255) and column block j
+    const int t = threadIdx.x, blk = t < kSwB ? i : j;
+    const int64_t p = (int64_t)l * np_ + (int64_t)blk * kSwB + (t & (kSwB - 1));
+    kl_mu[t] = (float)g.mu[p];
+    kl_sv[t] = g.sv[p];
   }
-  const float inv = 1.0f / scur;
+  const float inv = 1.0f / sx_gemm_scaled(ah, al, bh, bl, np_, nkb, sprod, lds, acc);
   if constexpr (MODE == kCiX) {
     const float sx = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
     const int64_t ot = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // X^T tile (j, i)
@@ -707,6 +763,14 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     });
     if (threadIdx.x == 0) S.ysc[sl + (int64_t)i * nt + j] = sy;
   } else {
+    // (kCiLauumKL: the tile is scaled in place once -- the epilogue has no registers for a scaled copy)
+    if constexpr (MODE == kCiLauumKL) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] *= inv;
+    }
+    const float osc = MODE == kCiLauumKL ? 1.f : inv;
     float* O = g.Kinv + l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;
     float* Ot = g.Kinv + l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(O, (short)0, 0x7fffffff, 0x00020000);
@@ -718,12 +782,48 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
       for (int e = 0; e < 16; ++e)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), ro, vo,
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * osc), ro, vo,
                                                 ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
-    if (i != j)
+    if constexpr (MODE == kCiLauumKL) {
+      ci_kl_partials(acc, 1.f, g, l, i, j, kl_mu, kl_part);
+      const int64_t tb = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;   // B tile (i, j)
+      const int64_t tbt = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // B tile (j, i)
+      const float sb = g.bh_out ? g.bsc[l] : 0.f;  // the dim's split scale of B (ci_bscale_kernel)
+      if (g.bh_out) {
+        // B(i, j) = T diag(sqrt v_j): column-scaled, straight from the registers
+        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(g.bh_out + tb, (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(g.bl_out + tb, (short)0, 0x7fffffff, 0x00020000);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const int vb = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 2;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float mc = sb * kl_sv[kSwB + sx_col(b)];
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const float y = acc[a][b][e] * mc;
+              const _Float16 yh = (_Float16)y;
+              const _Float16 yl = (_Float16)(y - (float)yh);
+              const int so = ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 2;
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yh), rh, vb, so, 0);
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yl), rl, vb, so, 0);
+            }
+        }
+      }
+      if (i != j)
+        ci_transposed_out(acc, 1.f, lds, [&](int c, int r0, f32x4 v) {
+          *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
+          if (g.bh_out) {
+            const f32x4 s4 = *reinterpret_cast<const f32x4*>(&kl_sv[r0]);
+            ci_split4(v * s4, sb, g.bh_out + tbt + (int64_t)c * np_ + r0, g.bl_out + tbt + (int64_t)c * np_ + r0);
+          }
+        });
+    } else if (i != j) {
       ci_transposed_out(acc, inv, lds, [&](int c, int r0, f32x4 v) {
         *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
       });
+    }
   }
 }
 
@@ -745,14 +845,16 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
 // their previous readers (panel(k-1), pivot(k)) precede U1(k) on the caller's stream.  The L planes of
 // column k are written once (panel(k)) and read by U1(k), U2(k), and trtri; D by the pivots, the panels
 // and the diagonal copies.
-// Then, on the caller's stream: the diagonal copy, trtri (2 launches per level), lauum.  (Launching each
+// Then, on the caller's stream: the diagonal copy, trtri (2 launches per level); lauum is ci_lauum_f32.  (Launching each
 // recursive-doubling instance as soon as potrf had produced its blocks -- 2 small launches per
 // instance on the caller's stream between the passes -- measured 15.1 vs 14.2 ms per closed step at
 // L = 16: the small launches slowed the passes more than the overlap saved.)
 size_t ci_scratch_bytes(int np_, int L) { return CiScratch(nullptr, np_, L).bytes; }
 
-int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
-                   int32_t* info, hipStream_t st) {
+// potrf + trtri: Y = L^-1 as the Y^T planes YT (+ the per-tile scales in the scratch); A and Kinv are
+// overwritten (Kinv holds the X^T planes)
+int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
+                  int32_t* info, hipStream_t st) {
   if (np_ <= 0 || np_ % kSwB || np_ / kSwB > 64) return -1;
   if (L <= 0) return -2;
   CiScratch S((char*)scratch, np_, L);
@@ -823,7 +925,7 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
   }
   LVAE_CHECK_LAUNCH();
   {
-    // trtri (recursive doubling, 2 launches per level) + lauum: the rest of potri
+    // trtri (recursive doubling, 2 launches per level): with lauum (ci_lauum_f32) the rest of potri
     ProfScope ps(LVAE_PH_POTRI, st);
     ci_diag_copy_kernel<<<dim3(16 * nt, L), 256, 0, st>>>(S, np_, Yh, Yl, YTh, YTl);
     for (int h = 1; h < nt; h *= 2) {
@@ -833,12 +935,70 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
       CiGemmArgs gy{Yh, Yl, XTh, XTl, Yh, Yl, YTh, YTl, nullptr, np_, nt, h, per, nwg, 0};
       ci_gemm_kernel<kCiY><<<nwg, 512, 0, st>>>(gy, S);
     }
-    const int per = nt * (nt + 1) / 2, nwg = per * L;
-    CiGemmArgs gl{YTh, YTl, YTh, YTl, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg, 0};
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// bsc[l] = x3_scale(a bound on max |B|), B = K^-1 diag(sqrt v), known BEFORE lauum so that every tile
+// of B is split with one scale per dim (the S GEMM then needs no rescaling between K blocks, which cost
+// it 10%): |K^-1_ij| <= max_j K^-1_jj = max_j sum_{i >= j} Y_ij^2 <= max_J sum_{I >= J} 256 m_IJ^2, m_IJ <
+// 2^14 / ysc(I, J) the max of Y's tile (x3_scale puts it in [2^13, 2^14) ysc^-1).  The bound may be loose
+// by ~256 nt: that only moves the lo plane's subnormal floor, an absolute error <= 2^-38 bound per entry
+// (far below the split's 2^-22 relative error).  One workgroup of 64 threads per dim.
+__global__ __launch_bounds__(64) void ci_bscale_kernel(CiScratch S, const float* __restrict__ sv, int np_,
+                                                       float* __restrict__ bsc) {
+  const int l = blockIdx.x, t = threadIdx.x, nt = S.nt;
+  const float* ys = S.ysc + (int64_t)l * nt * nt;
+  float d = 0.f;  // column blocks J = t, t + 64, ...
+  for (int J = t; J < nt; J += 64) {
+    float c = 0.f;
+    for (int I = J; I < nt; ++I) {
+      const float m = 16384.f / ys[I * nt + J];
+      c += 256.f * m * m;
+    }
+    d = fmaxf(d, c);
+  }
+  float v = 0.f;
+  for (int i = t; i < np_; i += 64) v = fmaxf(v, sv[(int64_t)l * np_ + i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    d = fmaxf(d, __shfl_xor(d, o, 64));
+    v = fmaxf(v, __shfl_xor(v, o, 64));
+  }
+  if (t == 0) bsc[l] = x3_scale(d * v);
+}
+
+// lauum, K^-1 = Y^T Y from ci_factor_f32's Y^T planes.  With mu (the exact KL's reduce): also the
+// partials of K^-1 mu (apart) and, if Bh, the planes of B = K^-1 diag(sqrt v) with their scale bsc[L].
+int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const double* mu, const float* sv,
+                 float* apart, _Float16* Bh, float* bsc, hipStream_t st) {
+  if (np_ <= 0 || np_ % kSwB || np_ / kSwB > 64) return -1;
+  CiScratch S((char*)scratch, np_, L);
+  const int nt = S.nt, per = nt * (nt + 1) / 2, nwg = per * L;
+  const int64_t full = (int64_t)L * np_ * np_;
+  ProfScope ps(LVAE_PH_POTRI, st);
+  CiGemmArgs gl{YT, YT + full, YT, YT + full, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg, 0};
+  if (mu) {
+    gl.mu = mu;
+    gl.sv = sv;
+    gl.apart = apart;
+    gl.bh_out = Bh;
+    gl.bl_out = Bh ? Bh + full : nullptr;
+    gl.bsc = bsc;
+    if (Bh) ci_bscale_kernel<<<L, 64, 0, st>>>(S, sv, np_, bsc);
+    ci_gemm_kernel<kCiLauumKL><<<nwg, 512, 0, st>>>(gl, S);
+  } else {
     ci_gemm_kernel<kCiLauum><<<nwg, 512, 0, st>>>(gl, S);
   }
   LVAE_CHECK_LAUNCH();
   return 0;
+}
+
+int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
+                   int32_t* info, hipStream_t st) {
+  LVAE_TRY(ci_factor_f32(np_, L, A, scratch, YT, Kinv, logdet, info, st));
+  return ci_lauum_f32(np_, L, scratch, YT, Kinv, nullptr, nullptr, nullptr, nullptr, nullptr, st);
 }
 
 }  // namespace lvae

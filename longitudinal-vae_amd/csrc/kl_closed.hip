@@ -1,21 +1,24 @@
 // kl_closed.hip -- exact GP-prior KL of the Longitudinal-VAE (elbo_functions.py:8-34), forward and
 // analytic backward, batched over the L latent dims (replaces the Python loop at training.py:515-522).
 //
+// factor (needs only the covariates and hyper-parameters: launched before the encoder has run):
 //   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
-//   K^-1, log|K|                                   (ci_inverse_f32: blocked Cholesky + trtri + lauum,
-//                                                   f16 x3 MFMA, chol_inv.hip)
-//   a0 = K^-1 mu                                   (kl_alpha_kernel, f64 accumulation)
+//   Y = L^-1, log|K|                               (ci_factor_f32: blocked Cholesky + trtri, f16 x3 MFMA,
+//                                                   chol_inv.hip)
+// reduce (needs mu, log v):
+//   K^-1 = Y^T Y, the partials of a0 = K^-1 mu,    (ci_lauum_f32 with the KL epilogue: one pass over the
+//   and B = K^-1 diag(sqrt v) as fp16 hi / lo       K^-1 tiles while they are in registers; B only when a
+//   planes, one power-of-two scale per dim          backward follows)
+//   a0, d = diag K^-1                              (kl_alpha0_kernel: fixed-order sum of the partials)
 //   r = mu - K a0                                  (kl_gram_resid: fp64 Gram-free residual, gram.hip)
-//   a = a0 + K^-1 r, d = diag K^-1                 (kl_alpha_kernel again: one step of iterative
-//                                                   refinement in fp64; when a backward follows, the
-//                                                   same pass writes the S GEMM operand B = K^-1
-//                                                   diag(sqrt v) as fp16 hi / lo planes with a per-row
-//                                                   power-of-two scale)
+//   a = a0 + K^-1 r                                (kl_alpha_kernel, f64 accumulation: one step of
+//                                                   iterative refinement)
 //   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
 // backward (dL/dkl_l = g_l):
-//   S = K^-1 V K^-1                                (syrk_x3_f32, f16 x3 MFMA, lower tiles)
+//   S = K^-1 V K^-1 = B B^T                        (syrk_tiles_f32, f16 x3 MFMA, lower tiles)
 //   G = 1/2 (K^-1 - S - a a^T) -> dtheta, dnoise   (kl_gram_bwd, fused, never materialised)
 //   dmu = g a,  dlogv = g/2 (v d - 1)
+// One reduce per factor: the backward's S overwrites the Y^T planes.
 #include "common.hpp"
 #include "prof.hpp"
 
@@ -30,9 +33,11 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
                 const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
                 hipStream_t st);
 int syrk_x3_splits(int np_, int L);
-int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
-int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
-                   int32_t* info, hipStream_t st);
+int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
+int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
+                  int32_t* info, hipStream_t st);
+int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const double* mu, const float* sv,
+                 float* apart, _Float16* Bh, float* bsc, hipStream_t st);
 size_t ci_scratch_bytes(int np_, int L);
 size_t kl_resid_partials_bytes(int np_, int L);
 int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
@@ -42,10 +47,11 @@ int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n,
 struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
   float* Sx;         // K-split partials 1.. of the S GEMM (syrk_x3_splits(np, L) - 1 matrices; few dims only)
-  _Float16* planes;  // fp16 hi / lo planes of the S GEMM operand: 2 L np^2 halves
-  float* rsc;        // [L, np] their per-row split scales
-  float* gb;         // [L] max_j sqrt(Kinv_jj v_j) (kl_bdiag_kernel)
-  char* chol;         // ci_inverse_f32 scratch (its Y^T planes are `planes`, free until the reduce)
+  _Float16* planes;  // 2 L np^2 halves: the factor's Y^T planes, then (backward) S = K^-1 V K^-1 in fp32
+  _Float16* Bp;      // the planes of B = K^-1 diag(sqrt v) (reduce -> backward): = A, dead after trtri
+  float* bsc;        // [L] their split scale per dim
+  float* apart;      // [L, nt, np] the partials of K^-1 mu (lauum epilogue)
+  char* chol;        // ci_factor_f32 scratch
   double *mu, *alpha, *res, *kdiag, *logdet, *part, *rpart;
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
@@ -57,12 +63,13 @@ struct KLWorkspace {
     };
     const size_t mat = (size_t)L * np_ * np_ * sizeof(float);
     A = (float*)take(mat);
+    Bp = reinterpret_cast<_Float16*>(A);
     planes = (_Float16*)take(mat);
     Kinv = (float*)take(mat);
     v = (float*)take((size_t)L * np_ * sizeof(float));
     sv = (float*)take((size_t)L * np_ * sizeof(float));
-    rsc = (float*)take((size_t)L * np_ * sizeof(float));
-    gb = (float*)take((size_t)L * sizeof(float));
+    bsc = (float*)take((size_t)L * sizeof(float));
+    apart = (float*)take((size_t)L * (np_ / 256) * np_ * sizeof(float));  // nt = np / 256 slots
     mu = (double*)take((size_t)L * np_ * sizeof(double));
     alpha = (double*)take((size_t)L * np_ * sizeof(double));
     res = (double*)take((size_t)L * np_ * sizeof(double));
@@ -88,67 +95,37 @@ __global__ void kl_prep_kernel(const double* __restrict__ mu, const double* __re
   sv[(int64_t)l * np_ + i] = (float)sqrt(vv);
 }
 
-// g[l] = max_j sqrt(Kinv_jj) sqrt(v_j): with |Kinv_ij| <= sqrt(Kinv_ii Kinv_jj) (K^-1 SPD), row i of
-// B = K^-1 diag(sqrt v) is bounded by sqrt(Kinv_ii) g[l] -- the split bound kl_alpha_kernel needs
-// BEFORE it streams the row (one pass over K^-1 instead of two)
-__global__ __launch_bounds__(256) void kl_bdiag_kernel(const float* __restrict__ Kinv, const float* __restrict__ sv,
-                                                       int np_, float* __restrict__ g) {
-  __shared__ float red[4];
-  const int l = blockIdx.x, tid = threadIdx.x;
-  float m = 0.f;
-  for (int j = tid; j < np_; j += 256)
-    m = fmaxf(m, sqrtf(fabsf(Kinv[(int64_t)l * np_ * np_ + (int64_t)j * np_ + j])) * sv[(int64_t)l * np_ + j]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((tid & 63) == 0) red[tid >> 6] = m;
-  __syncthreads();
-  if (tid == 0) g[l] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+// a0 = sum_s apart[l][s] (fixed order, fp64) and d = diag K^-1; grid (np / 256, L)
+__global__ __launch_bounds__(256) void kl_alpha0_kernel(const float* __restrict__ apart, const float* __restrict__ Kinv,
+                                                        int np_, double* __restrict__ alpha,
+                                                        double* __restrict__ kdiag) {
+  const int l = blockIdx.y, nt = np_ / 256;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const float* ap = apart + (int64_t)l * nt * np_ + p;
+  double s = 0.0;
+  for (int q = 0; q < nt; ++q) s += (double)ap[(int64_t)q * np_];
+  const int64_t o = (int64_t)l * np_ + p;
+  alpha[o] = s;
+  kdiag[o] = (double)Kinv[(int64_t)l * np_ * np_ + (int64_t)p * np_ + p];
 }
 
-// one wave per row: a_i = base_i + sum_j Kinv[i][j] u_j (f64 accumulate; base may be NULL), and
-// d_i = Kinv[i][i] when kdiag != NULL; with PLANES also row i of the S GEMM operand B = K^-1 diag(sqrt v)
-// as fp16 planes B_ij sc_i = hi + lo, sc_i = x3_scale(sqrt(Kinv_ii) g[l]) (a bound on max_j |B_ij|,
-// kl_bdiag_kernel): the backward's GEMM reads its operand pre-split and nothing re-reads K^-1 for it.
-template <bool PLANES>
+// alpha = base + K^-1 u (one wave per row, fp64 accumulation of the fp32 K^-1 row times the fp64 u)
 __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__ Kinv, const double* __restrict__ u,
-                                                       const float* __restrict__ sv, int np_,
-                                                       const float* __restrict__ g, const double* base,
-                                                       double* alpha, double* __restrict__ kdiag,
-                                                       float* __restrict__ rsc, _Float16* __restrict__ Bh,
-                                                       _Float16* __restrict__ Bl) {
-  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+                                                       int np_, const double* base, double* alpha) {
   const int l = blockIdx.y, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= np_) return;
-  const int64_t ro = (int64_t)l * np_ * np_ + (int64_t)i * np_;
-  const float* row = Kinv + ro;
+  const float* row = Kinv + (int64_t)l * np_ * np_ + (int64_t)i * np_;
   const double* m = u + (int64_t)l * np_;
-  const float* s = PLANES ? sv + (int64_t)l * np_ : nullptr;
-  const float dii = row[i];
-  const float sc = PLANES ? x3_scale(sqrtf(fabsf(dii)) * g[l]) : 0.f;
   double acc = 0.0;
   for (int j = lane * 4; j < np_; j += 256) {
     const float4 k4 = *reinterpret_cast<const float4*>(row + j);
     acc += (double)k4.x * m[j] + (double)k4.y * m[j + 1] + (double)k4.z * m[j + 2] + (double)k4.w * m[j + 3];
-    if constexpr (PLANES) {
-      const float4 s4 = *reinterpret_cast<const float4*>(s + j);
-      const float y[4] = {k4.x * s4.x * sc, k4.y * s4.y * sc, k4.z * s4.z * sc, k4.w * s4.w * sc};
-      half4 h, lo;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        h[q] = (_Float16)y[q];
-        lo[q] = (_Float16)(y[q] - (float)h[q]);
-      }
-      *reinterpret_cast<half4*>(Bh + ro + j) = h;
-      *reinterpret_cast<half4*>(Bl + ro + j) = lo;
-    }
   }
   acc = wave_sum(acc);
   if (lane == 0) {
     const int64_t o = (int64_t)l * np_ + i;
-    alpha[o] = (base ? base[o] : 0.0) + acc;
-    if (kdiag) kdiag[o] = (double)dii;
-    if (PLANES) rsc[o] = sc;
+    alpha[o] = base[o] + acc;
   }
 }
 
@@ -214,9 +191,9 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
     ProfScope ps(LVAE_PH_GRAM, st);
     LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
   }
-  // K^-1 and log|K|: blocked Cholesky + trtri + lauum (chol_inv.hip; phases POTRF / POTRI inside),
-  // its Y^T planes in the S-operand planes (written only by the reduce, after this)
-  LVAE_TRY(ci_inverse_f32(np_, L, ws.A, ws.chol, ws.planes, ws.Kinv, ws.logdet, info, st));
+  // Y = L^-1 and log|K|: blocked Cholesky + trtri (chol_inv.hip; phases POTRF / POTRI inside); lauum
+  // runs in the reduce
+  LVAE_TRY(ci_factor_f32(np_, L, ws.A, ws.chol, ws.planes, ws.Kinv, ws.logdet, info, st));
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -238,20 +215,13 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
   KLWorkspace ws((char*)workspace, np_, L);
   ProfScope ps(LVAE_PH_KL_REDUCE, st);
   kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v, ws.sv);
-  const int64_t per = (int64_t)L * np_ * np_;
-  const dim3 rows(np_ / 4, L);
-  // a0 = K^-1 mu; r = mu - K a0 in fp64 from the covariates; a = a0 + K^-1 r (+ d, + the S planes)
-  kl_alpha_kernel<false><<<rows, 256, 0, st>>>(ws.Kinv, ws.mu, nullptr, np_, nullptr, nullptr, ws.alpha, nullptr,
-                                               nullptr, nullptr, nullptr);
+  // K^-1 (+ the partials of a0 = K^-1 mu, + the B planes); a0, d; r = mu - K a0 in fp64 from the
+  // covariates; a = a0 + K^-1 r
+  LVAE_TRY(ci_lauum_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.mu, ws.sv, ws.apart, need_bwd ? ws.Bp : nullptr,
+                        ws.bsc, st));
+  kl_alpha0_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.apart, ws.Kinv, np_, ws.alpha, ws.kdiag);
   LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res, st));
-  if (need_bwd) {
-    kl_bdiag_kernel<<<L, 256, 0, st>>>(ws.Kinv, ws.sv, np_, ws.gb);
-    kl_alpha_kernel<true><<<rows, 256, 0, st>>>(ws.Kinv, ws.res, ws.sv, np_, ws.gb, ws.alpha, ws.alpha, ws.kdiag,
-                                                ws.rsc, ws.planes, ws.planes + per);
-  } else {
-    kl_alpha_kernel<false><<<rows, 256, 0, st>>>(ws.Kinv, ws.res, nullptr, np_, nullptr, ws.alpha, ws.alpha,
-                                                 ws.kdiag, nullptr, nullptr, nullptr);
-  }
+  kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.alpha, ws.alpha);
   kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   LVAE_CHECK_LAUNCH();
   return 0;
@@ -282,15 +252,16 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
-  // S = K^-1 V K^-1 into the (no longer needed) Gram buffer, from the fp16 hi / lo planes of
-  // K^-1 diag(sqrt v) the forward wrote (need_bwd; np is a multiple of 256: lvae_kl_closed_padded_n)
+  // S = K^-1 V K^-1 = B B^T into the (no longer needed) Y^T plane buffer, from the fp16 hi / lo planes
+  // of B = K^-1 diag(sqrt v) the forward wrote (need_bwd; np is a multiple of 256: lvae_kl_closed_padded_n)
+  float* S = reinterpret_cast<float*>(ws.planes);
   {
     ProfScope ps(LVAE_PH_SYRK, st);
-    LVAE_TRY(syrk_x3_f32(np_, L, ws.rsc, ws.planes, ws.A, ws.Sx, st));
+    LVAE_TRY(syrk_tiles_f32(np_, L, ws.bsc, ws.Bp, S, ws.Sx, st));
   }
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);
-    LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, ws.A, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
+    LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, S, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
                          gkl, ws.part, dparams, dnoise, st));
   }
   {

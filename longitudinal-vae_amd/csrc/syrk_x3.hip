@@ -2,10 +2,11 @@
 // on the f16 matrix cores with the fp32-accurate 3-product split (see mfma_x3.hpp for the error
 // argument), specialised for throughput:
 //
-//   split : row i of B = K^-1 diag(sqrt v), times sc_i = x3_scale(bound on max_j |B_ij|), is split
-//           ONCE into fp16 hi / lo planes by the forward's kl_alpha_kernel (which reads K^-1 anyway); the
-//           epilogue divides by sc_i sc_j (the generic x3 tile GEMM would re-split every operand
-//           chunk for every output tile);
+//   split : B = K^-1 diag(sqrt v) is split ONCE into fp16 hi / lo planes, with one power-of-two scale
+//           per latent dim from a bound (ci_bscale_kernel), by the forward's lauum epilogue (which holds
+//           the K^-1 tiles in registers anyway: chol_inv.hip, kCiLauumKL); the epilogue divides by its
+//           square (the generic x3 tile GEMM would re-split every operand chunk for every output tile).  (r1-r2: one scale per row from a bound, written by a separate pass
+//           over K^-1 -- syrk_x3_kernel below, kept for the dev A/B harness);
 //   syrk  : 256 x 256 output tiles, 512 threads = 8 waves (2 along M x 4 along N, 128 x 64 each,
 //           4 x 2 blocks of v_mfma_f32_32x32x16_f16, three products per block and k-step);
 //           operands staged global -> LDS directly (global_load_lds_dwordx4, no VGPR round trip)
@@ -241,18 +242,55 @@ int syrk_x3_splits(int np_, int L) {
   return best;
 }
 
-// S (lower 256-tiles of [L, np, np] fp32) = K^-1 diag(v) K^-1 from the fp16 hi / lo planes of
-// B = K^-1 diag(sqrt v) (2 L np^2 halves: hi then lo), row i scaled by rsc[l][i] (kl_alpha_kernel).
-// With s = syrk_x3_splits(np, L) > 1 the K-split partials go to S (split 0) and Sx[j - 1] (split j).
-int syrk_x3_f32(int np_, int L, const float* rsc, const _Float16* planes, float* S, float* Sx, hipStream_t st) {
+// The product S GEMM: B's planes split with ONE power-of-two scale per latent dim, bsc[l] (written by the
+// exact KL's lauum epilogue, chol_inv.hip), so S = acc / bsc[l]^2.  (Per-tile scales with the
+// accumulators rescaled at every K block cost 10% here, scripts/gemm_ab.py.  So did the 8-wave core with
+// 16-deep chunks in a 4-stage ring, two chunks in flight across each barrier: 3.55 vs 3.18 ms at
+// np = 4096, L = 16 and 87 vs 51 ms at np = 16384, L = 4 -- its 32-B row segments per chunk double the
+// L2 traffic.)  Same tile order and K split.
+__global__ __launch_bounds__(512) void syrk_tiles_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
+                                                         const float* __restrict__ bsc, float* __restrict__ S,
+                                                         float* __restrict__ Sx, int np_, int ntl, int nwg, int L, int ns) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int sp = wgid / (ntl * L), l = (wgid / ntl) % L, nt = np_ / kSxT;
+  int I, J;
+  sx_tri_blocked(wgid % ntl, nt, I, J);
+  const int kb0 = sp * nt / ns, kb1 = (sp + 1) * nt / ns;
+  const int64_t ld = np_;
+  const int64_t base = (int64_t)l * np_ * np_, k0 = (int64_t)kb0 * kSxT;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  if (kb1 > kb0)
+    sx_gemm(Bh + base + (int64_t)I * kSxT * ld + k0, Bl + base + (int64_t)I * kSxT * ld + k0,
+            Bh + base + (int64_t)J * kSxT * ld + k0, Bl + base + (int64_t)J * kSxT * ld + k0, ld, (kb1 - kb0) * kSxT,
+            lds, acc);
+  const float sc = bsc[l], inv = 1.0f / (sc * sc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* C = (sp == 0 ? S : Sx + (int64_t)(sp - 1) * L * np_ * np_) + base + (int64_t)I * kSxT * ld + J * kSxT;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+  const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), rc, vo,
+                                              ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+}
+
+int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st) {
   if (np_ % kSxT) return -1;
   const int64_t per = (int64_t)np_ * np_;
-  const _Float16* Bh = planes;
-  const _Float16* Bl = planes + (int64_t)L * per;
   const int ns = syrk_x3_splits(np_, L);
   if (ns > 1 && !Sx) return -2;
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L * ns;
-  syrk_x3_kernel<1><<<nwg, 512, 0, st>>>(Bh, Bl, rsc, S, Sx, np_, ntl, nwg, L, np_ / ns);
+  syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -267,6 +305,8 @@ int syrk_dev_variant(int variant, int np_, int L, const float* rsc, const _Float
     syrk_x3_kernel<0><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
   else if (variant == 2)
     syrk_x3_kernel<1><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
+  else if (variant == 4)  // the product kernel (rsc[l * np] read as the dims' scales: ones)
+    syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
   else if (variant == 3)
     syrk_h2_kernel<<<2 * nwg, 256, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, np_, 2 * ntl, 2 * nwg, L);
   else

@@ -134,6 +134,41 @@ __device__ inline void sx_gemm(const _Float16* __restrict__ ah, const _Float16* 
   }
 }
 
+// sx_gemm over nkb whole 256-deep K blocks whose operand planes carry per-block split scales:
+// sprod[kb] = sA(kb) sB(kb) (LDS, written before the first barrier here).  The accumulators move to
+// the units of each new block at its first chunk (ratios of powers of two: exact); returns the units
+// of the last block (value = acc / returned).
+__device__ inline float sx_gemm_scaled(const _Float16* __restrict__ ah, const _Float16* __restrict__ al,
+                                       const _Float16* __restrict__ bh, const _Float16* __restrict__ bl, int64_t ld,
+                                       int nkb, const float* sprod, _Float16* __restrict__ lds,
+                                       sx_f32x16 (&acc)[4][2]) {
+  constexpr int cpb = 256 / kSxBK;  // K chunks per block
+  const int nk = nkb * cpb;
+  float scur = 1.f;
+  sx_issue(ah, al, bh, bl, ld, 0, lds);
+  for (int s = 0; s < nk; ++s) {
+    SX_WAIT_VM(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nk) sx_issue(ah, al, bh, bl, ld, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kSxPart);
+    if (s % cpb == 0) {
+      const float snew = sprod[s / cpb];
+      if (s) {
+        const float ratio = snew / scur;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] *= ratio;
+      }
+      scur = snew;
+    }
+    __builtin_amdgcn_s_setprio(1);
+    sx_mma_stage(lds + (s & 1) * 4 * kSxPart, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  return scur;
+}
+
 // accumulator element e of block (a, b) in lane: row / column inside the 256 x 256 tile
 __device__ inline int sx_row(int a, int e) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

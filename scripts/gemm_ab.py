@@ -1,6 +1,7 @@
 """A/B of the S-GEMM cores (lvae_dev_syrk: variant 0 = 8-wave 2-stage x3_dma core, 1 = 4-wave 4-stage
-x3_gemm4 core, 2 = variant 0 with the 4-row-block tile order) on random pre-split planes: time per
-launch and agreement of the lower tiles."""
+x3_gemm4 core, 2 = variant 0 with the 4-row-block tile order, 3 = half tiles with two workgroups per CU,
+4 = the product syrk_tiles_kernel: one split scale per dim) on random pre-split planes: time per launch
+and agreement of the lower tiles."""
 import ctypes
 import os
 import sys

@@ -28,7 +28,7 @@ for name in ${CFGS:-headline c5rank}; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/$name -o run --output-format csv -- \
     python3 $ROOT/bench.py --regime closed $args --steps 5 --warmup 2 --no-cpu-baseline --no-phase-timing --no-c2 \
     > $OUT/$name.json 2> $OUT/$name.err || { tail -20 $OUT/$name.err; exit 1; }
-  grep -h "ci_gemm\|ci_pivot\|ci_update\|ci_panel\|syrk" $OUT/$name/run_kernel_trace.csv > $OUT/$name.trace_ci.csv 2>/dev/null
+  grep -h "ci_gemm\|ci_pivot\|ci_update\|ci_panel\|syrk\|kl_" $OUT/$name/run_kernel_trace.csv > $OUT/$name.trace_ci.csv 2>/dev/null
   rm -f $OUT/$name/run_kernel_trace.csv
   cat $OUT/$name.json
   summ $OUT/$name/run_kernel_stats.csv 7 | tee $OUT/$name.summary.txt
