@@ -45,7 +45,10 @@ DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3_pmc_summary.json")
-U2_NAME = "ci_update_kernel<0>"         # the Cholesky's trailing rank-256 update U2 (chol_inv.hip, MODE kCiU2)
+# the Cholesky's trailing rank-256 update (chol_inv.hip): U2 alone (MODE kCiU2) when the lookahead chain
+# runs on the side stream (schedule (b), > CI_FUSE_MAX_L dims per call), else fused with U1 (kCiU12)
+CI_FUSE_MAX_L = 16
+U2_NAMES = {False: "ci_update_kernel<0>", True: "ci_update_kernel<2>"}
 
 
 def log(*a):
@@ -316,18 +319,22 @@ def run_closed(args, world, rank, dev):
                                "engine": "f16 MFMA (v_mfma_f32_32x32x16_f16), 3-product split: achieved counts the 3 "
                                          "f16 products per fp32-equivalent product"}
         # secondary: the trailing rank-256 update of the Cholesky (U2, HBM-streaming); per step the passes
-        # k = 0 .. nt-3 update (nt-k-2)(nt-k-1)/2 tiles per dim, each read and written once in fp32
+        # k = 0 .. nt-3 update (nt-k-2)(nt-k-1)/2 tiles per dim, each read and written once in fp32 (at
+        # <= CI_FUSE_MAX_L dims the same launch also turns column k+1's nt-k-2 tiles into the next pass's
+        # planes: read fp32, write 2 fp16 planes, the same 8 bytes per element)
         nt = np_ // 256
+        fused = Lr <= CI_FUSE_MAX_L
         upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
-        tiles = sum((nt - k - 2) * (nt - k - 1) // 2 for k in range(nt - 2)) * Lr
+        tiles = sum((nt - k - 2) * (nt - k - 1) // 2 + (nt - k - 2 if fused else 0) for k in range(nt - 2)) * Lr
         upd_bytes = 2 * 4 * 256 * 256 * tiles
+        u2_name = U2_NAMES[fused]
         if upd_n:
             ach = upd_bytes / (upd_ms / args.steps * 1e-3) / 1e9
             launches = upd_n / args.steps
-            res["roofline_secondary"] = {"kernel": "ci_update_kernel<0> (potrf trailing rank-256 update U2, chol_inv.hip)",
+            res["roofline_secondary"] = {"kernel": f"{u2_name} (potrf trailing rank-256 update U2{' + U1' if fused else ''}, chol_inv.hip)",
                                          "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                          "frac": ach / HBM_PEAK_GBS,
-                                         "traffic": pmc_traffic((U2_NAME,), per_step=True) if world == 1 else None,
+                                         "traffic": pmc_traffic((u2_name,), per_step=True) if world == 1 else None,
                                          "traffic_source": os.path.basename(PMC_SUMMARY),
                                          "algorithmic_bytes_per_step": upd_bytes,
                                          "algorithmic_bytes_per_launch": upd_bytes / launches,

@@ -166,15 +166,24 @@ __device__ inline void ci_pending_update(const float* __restrict__ T, int64_t np
   }
 }
 
+// dev: phase timestamps of the pivots (s_memrealtime, 100 MHz) into prof[(kb * L + l) * 8 + phase] when
+// lvae_dev_pivot_prof set a buffer (scripts/pivot_prof.py); nullptr in the product
+static unsigned long long* g_pivot_prof = nullptr;
+#define CI_STAMP(q)                                                                     \
+  do {                                                                                  \
+    if (prof && threadIdx.x == 0) prof[((int64_t)kb * gridDim.x + l) * 8 + (q)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict__ Aall, int np_, int kb, CiScratch S,
                                                         double* __restrict__ logdet, int32_t* __restrict__ info,
-                                                        int pending) {
+                                                        int pending, unsigned long long* __restrict__ prof) {
   __shared__ float lf[kPvBlocks * kPvBlk];
-  __shared__ uint32_t ymax_s, xmax_s;
+  __shared__ uint32_t ymax_s, xmax_s, dmax_s;
   __shared__ float bsc[kPvBlocks];
   __shared__ int bad_s;
   const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
+  CI_STAMP(0);
   if (tid == 0) {
     bad_s = INT_MAX;
     ymax_s = 0u;
@@ -194,15 +203,30 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
     for (int b = 0; b < kPvBlocks; ++b) lf[b * kPvBlk + r * kPvL + c] = v[b];
   }
   __syncthreads();
+  CI_STAMP(1);
   double ld = 0.0;
   int bad = INT_MAX;
 
-  // 1. Cholesky A_kk = L L^T, panel by panel, then the trailing update A_ij -= L_iq L_jq^T
+  // 1. Cholesky A_kk = L L^T, panel by panel (two elimination steps per MFMA, pv_panel2), then the
+  //    trailing update A_ij -= L_iq L_jq^T on the f16 cores with the x3 split (pv_mma3): every entry of
+  //    L obeys |L_ij| <= sqrt(A_ii), so one split scale from the block's largest diagonal entry serves
+  //    every panel block
+  {
+    float m = 0.f;
+    if (tid < kSwB) m = fabsf(pv_blk(lf, tid >> 5, tid >> 5)[(tid & 31) * kPvL + (tid & 31)]);
+    dmax_s = 0u;  // (after the loads' barrier: nobody reads it before the one below)
+    __syncthreads();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) atomicMax(&dmax_s, __float_as_uint(m));
+    __syncthreads();
+  }
+  const float sL = x3_scale(sqrtf(__uint_as_float(dmax_s)));
   for (int q = 0; q < 8; ++q) {
     if (w <= 7 - q) {
-      pv_panel(lf, q, w, lane, ld, bad);
+      pv_panel2(lf, q, w, lane, ld, bad);
     } else {
-      __syncthreads();  // pv_panel's barrier
+      __syncthreads();  // pv_panel2's barrier
     }
     __syncthreads();
     const int m = 7 - q, nb = m * (m + 1) / 2;
@@ -216,13 +240,15 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
       pv_f32x16 acc;
       float* Bij = pv_blk(lf, i, j);
       pv_load(acc, Bij, rl, hh);
-      pv_mma<false, false>(acc, pv_blk(lf, i, q), pv_blk(lf, j, q), rl, hh, -1.f);
+      pv_mma3<false, false>(acc, pv_blk(lf, i, q), pv_blk(lf, j, q), sL, sL, rl, hh, -1.f);
       pv_store(acc, Bij, rl, hh);
     }
     __syncthreads();
   }
+  CI_STAMP(2);
   if (w < 8) pv_trinv(pv_blk(lf, w, w), lane);
   __syncthreads();
+  CI_STAMP(3);
 
   // 2. L^-1 in place by recursive doubling (levels of 64, 128, 256 rows; see spd_sweep.hip's pivot)
   if (w < 4) {
@@ -274,6 +300,7 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
     __syncthreads();
   }
 
+  CI_STAMP(4);
   // 3. max |Y_kk| -> its split scale; out: D (row-major planes; the diagonal copy puts them into the
   //    Y and Y^T planes after potrf).  Thread (r0 = tid >> 6, c = 4 (tid & 63)) covers rows r0, r0 + 16,
   //    ... (a wave writes one whole row: half4 runs).
@@ -309,6 +336,7 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
   }
   if (w == 0 && lane == 0) bad_s = bad;
   __syncthreads();
+  CI_STAMP(5);
   if (tid == 0) {
     S.ysc[((int64_t)l * S.nt + kb) * S.nt + kb] = sY;
     logdet[l] += ld;
@@ -450,25 +478,37 @@ __global__ __launch_bounds__(512) void ci_panel_kernel(CiScratch S, int np_, int
 //          written as the planes of pass k+1's C operand (the diagonal tile in fp32, for the pivot)
 //   kCiU2  the trailing tiles I >= J >= k+2, in place
 // ------------------------------------------------------------------------------------------
-constexpr int kCiU2 = 0, kCiU1 = 1;
+constexpr int kCiU2 = 0, kCiU1 = 1, kCiU12 = 2;  // kCiU12: U1 (without the pivot block) + U2, one launch
 constexpr int kCiFuseMaxL = 16; // latent dims per call up to which the pivot updates its own block
 template <int MODE>
 __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall, CiScratch S, int np_, int k,
-                                                        int ntl, int nwg) {
+                                                        int ntl, int nwg, int n1 = 0) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   __shared__ uint32_t red;
-  if (MODE == kCiU1 && threadIdx.x == 0) red = 0u;
-  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int l = wgid / ntl, t = wgid % ntl, nt = np_ / kSwB;
-  int I, J;
-  if constexpr (MODE == kCiU1) {
-    I = (ntl == nt - k - 1) ? k + 1 + t : k + 2 + t;  // with / without the pivot block
+  if (MODE != kCiU2 && threadIdx.x == 0) red = 0u;
+  const int nt = np_ / kSwB;
+  // kCiU12: workgroups [0, n1 L) are column k+1's tiles (dispatched first: the next pass's C operand),
+  // the rest the trailing tiles; ntl / nwg describe the trailing part
+  const bool u1 = MODE == kCiU1 || (MODE == kCiU12 && (int)blockIdx.x < n1 * (nwg / max(ntl, 1)));
+  int l, I, J;
+  if (MODE == kCiU12 && u1) {
+    l = blockIdx.x / n1;
+    I = k + 2 + blockIdx.x % n1;
     J = k + 1;
   } else {
-    sx_tri_blocked(t, nt - k - 2, I, J);
-    I += k + 2;
-    J += k + 2;
+    const int orig = MODE == kCiU12 ? blockIdx.x - n1 * (nwg / ntl) : blockIdx.x;
+    const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    l = wgid / ntl;
+    const int t = wgid % ntl;
+    if constexpr (MODE == kCiU1) {
+      I = (ntl == nt - k - 1) ? k + 1 + t : k + 2 + t;  // with / without the pivot block
+      J = k + 1;
+    } else {
+      sx_tri_blocked(t, nt - k - 2, I, J);
+      I += k + 2;
+      J += k + 2;
+    }
   }
   const int64_t np2 = (int64_t)np_ * np_;
   float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
@@ -522,7 +562,7 @@ __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall
       const int i = 16 * j + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
       acc[a][b][e] += cv[j & 1][q] * ncs;
     }
-  if (MODE == kCiU1 && I != J) {
+  if (u1 && I != J) {
     // a block of column k+1 = block I of the next pass's C operand: straight to its planes
     const float sc = x3_scale(sw_block_max(ci_acc_absmax(acc) * fabsf(ninv), &red));
     const int64_t on = (int64_t)l * np_ * kSwB + (int64_t)I * kSwBB;
@@ -835,7 +875,7 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
 //     the previous pass's update to its own block (ci_pending_update) and waiting only for U2(m-2), the
 //     last writer of its block before that:
 //       side:  pivot(0);  [wait ev_u2(m-1) (ev_c = prep0 for m = 0);  pivot(m+1);  record ev_piv(m+1)]...
-//       main:  prep0;  record ev_c;  [wait ev_piv(m);  panel(m);  U1(m) (without the pivot block);  U2(m);
+//       main:  prep0;  record ev_c;  [wait ev_piv(m);  panel(m);  U1(m) (without the pivot block) + U2(m), one launch;
 //              record ev_u2(m)]...
 // (b) many latent dims (the headline L = 16): the chain runs whole on the side stream beside U2:
 //       side:  prep0;  pivot(0);  panel(0);  record ev_prep
@@ -877,32 +917,31 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
     const bool fuse = L <= kCiFuseMaxL;
     if (fuse) {
-      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
+      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, g_pivot_prof);
       if (!ok(hipEventRecord(sd->piv[0], sd->s))) return LVAE_ERR_LAUNCH;
       if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, st>>>(A, np_, S);
       if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
       for (int m = 0; m < nt; ++m) {
         if (m + 1 < nt) {
           if (!ok(hipStreamWaitEvent(sd->s, m == 0 ? sd->c : sd->u2p[(m - 1) & 1], 0))) return LVAE_ERR_LAUNCH;
-          ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1);
+          ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1, g_pivot_prof);
           if (!ok(hipEventRecord(sd->piv[(m + 1) & 1], sd->s))) return LVAE_ERR_LAUNCH;
         }
         if (!ok(hipStreamWaitEvent(st, sd->piv[m & 1], 0))) return LVAE_ERR_LAUNCH;
         if (m + 1 < nt) {
           ci_panel_kernel<<<dim3(nt - m - 1, L), 512, 0, st>>>(S, np_, m);
-          const int n1 = nt - m - 2;  // column m+1 without the pivot block
-          if (n1 > 0) ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, m, n1, n1 * L);
-          const int n2 = (nt - m - 2) * (nt - m - 1) / 2;
+          // column m+1 without the pivot block + the trailing tiles, one launch
+          const int n1 = nt - m - 2, n2 = (nt - m - 2) * (nt - m - 1) / 2;
           if (n2 > 0) {
             ProfScope pu(LVAE_PH_SWEEP_UPD, st);
-            ci_update_kernel<kCiU2><<<n2 * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L);
+            ci_update_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
           }
           if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
         }
       }
     } else {
       if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
-      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
+      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, g_pivot_prof);
       if (nt > 1) ci_panel_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(S, np_, 0);
       if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
       for (int k = 0; k + 1 < nt; ++k) {
@@ -911,7 +950,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
         ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, k, n1, n1 * L);
         if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
         if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
-        ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0);
+        ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0, g_pivot_prof);
         if (k + 2 < nt) ci_panel_kernel<<<dim3(nt - k - 2, L), 512, 0, sd->s>>>(S, np_, k + 1);
         if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
         const int n2 = (nt - k - 2) * (nt - k - 1) / 2;
@@ -1004,6 +1043,8 @@ int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float*
 }  // namespace lvae
 
 extern "C" {
+// dev only (not in the C ABI header): the pivots' phase timestamps into buf (nt L 8 u64; nullptr: off)
+void lvae_dev_pivot_prof(void* buf) { lvae::g_pivot_prof = (unsigned long long*)buf; }
 size_t lvae_spd_inv_chol_scratch_size(int np_, int L) {
   // the C-ABI form also needs the Y^T planes (the KL workspace lends its S-operand planes instead)
   return lvae::ci_scratch_bytes(np_, L) + lvae::align256((size_t)L * np_ * np_ * 2 * sizeof(_Float16));

@@ -71,7 +71,8 @@ __device__ inline void pv_mma(pv_f32x16& acc, const float* X, const float* Y, in
 // v_mfma_f32_32x32x2f32: ~5x the MFMA rate) accumulated in a temporary and unscaled into acc.
 // The f16 32x32x16 accumulator layout is that of the 32x32x2 f32 MFMA (pv_row).
 template <bool TX, bool TY>
-__device__ inline void pv_mma3(pv_f32x16& acc, const float* X, const float* Y, float sX, float sY, int rl, int hh) {
+__device__ inline void pv_mma3(pv_f32x16& acc, const float* X, const float* Y, float sX, float sY, int rl, int hh,
+                               float sgn = 1.f) {
   pv_f32x16 t = {};
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -91,7 +92,7 @@ __device__ inline void pv_mma3(pv_f32x16& acc, const float* X, const float* Y, f
     t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL, t, 0, 0, 0);
     t = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH, t, 0, 0, 0);
   }
-  acc += t * (1.0f / (sX * sY));
+  acc += t * (sgn / (sX * sY));
 }
 
 // As pv_mma3 on blocks already split IN PLACE (pv_pack_blocks: each fp32 word replaced by the packed
@@ -203,6 +204,72 @@ __device__ inline void pv_panel(float* lf, int q, int w, int lane, double& ld, i
       if (lane == p) dp = d;
     }
     X = __builtin_amdgcn_mfma_f32_32x32x2f32(-u, u * id, X, 0, 0, 0);
+  }
+  if (w == 0) {
+    const double lv = (lane < 32) ? log((double)dp) : 0.0;
+    ld += wave_sum(lv);
+    const unsigned long long nb = __ballot(lane < 32 && !(dp > 0.0f && isfinite(dp)));
+    if (nb) bad = min(bad, 32 * q + (int)__builtin_ctzll(nb));
+  }
+}
+
+// the value v of lane (rl, h) in every lane (rl, .): v_permlane32_swap of v with itself gives the lower
+// half's values in both halves (first result) and the upper half's (second)
+__device__ inline float pv_from_half(float v, int h) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(h ? r[1] : r[0]);
+}
+
+// pv_panel with TWO elimination steps per MFMA: rows p and p+1 (p even) sit in the same half of the
+// accumulator lanes, so step p+1's vectors follow from step p's by one FMA per lane
+//   u1 = X[p+1, :] - X[p, p+1] u0 / d_p,   d_{p+1} = X[p+1, p+1] - X[p, p+1]^2 / d_p   (b1 likewise)
+// and the MFMA carries step p in k-slot h(p) and step p+1 in the other one (its operands moved across
+// by v_permlane32_swap): 16 MFMAs per panel and block instead of 32 on the dependent chain.
+__device__ inline void pv_panel2(float* lf, int q, int w, int lane, double& ld, int& bad) {
+  const int rl = lane & 31, hh = lane >> 5, i = q + w;
+  float* Dq = pv_blk(lf, q, q);
+  float* Bi = pv_blk(lf, i, q);
+  pv_f32x16 X, Bt;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = pv_row(e, hh);
+    X[e] = r >= rl ? Dq[r * kPvL + rl] : Dq[rl * kPvL + r];
+    Bt[e] = (w > 0) ? Bi[rl * kPvL + r] : 0.0f;
+  }
+  float dp = 0.f;  // lane p: pivot d_p
+  __syncthreads();  // every panel wave has its copy of A_qq before wave 0 overwrites it with L_qq
+#pragma unroll
+  for (int p = 0; p < 32; p += 2) {
+    const int e0 = pv_e(p), e1 = e0 + 1, hp = pv_hh(p);  // row p + 1: element e0 + 1, same half
+    const int lp = p + 32 * hp;
+    const float d0 = pv_rl(X[e0], lp), x01 = pv_rl(X[e0], lp + 1), x11 = pv_rl(X[e1], lp + 1);
+    const float id0 = __builtin_amdgcn_rcpf(d0), is0 = __builtin_amdgcn_rsqf(d0);
+    const float c01 = x01 * id0;
+    const float d1 = x11 - x01 * c01;
+    const float id1 = __builtin_amdgcn_rcpf(d1), is1 = __builtin_amdgcn_rsqf(d1);
+    const bool mine = (hh == hp);
+    const float u0 = (mine && rl >= p) ? X[e0] : 0.0f;
+    const float u1 = (mine && rl > p) ? X[e1] - c01 * u0 : 0.0f;
+    const float u1s = pv_from_half(u1, hp);
+    const float a = mine ? u0 : u1s;
+    if (w > 0) {
+      const float b0 = mine ? Bt[e0] : 0.0f;
+      const float b1 = mine ? Bt[e1] - c01 * b0 : 0.0f;
+      if (mine) {
+        Bi[rl * kPvL + p] = b0 * is0;
+        Bi[rl * kPvL + p + 1] = b1 * is1;
+      }
+      const float b1s = pv_from_half(b1, hp);
+      Bt = __builtin_amdgcn_mfma_f32_32x32x2f32(-a, mine ? b0 * id0 : b1s * id1, Bt, 0, 0, 0);
+    } else {
+      if (mine) {
+        Dq[rl * kPvL + p] = u0 * is0;
+        Dq[rl * kPvL + p + 1] = u1 * is1;
+      }
+      if (lane == p) dp = d0;
+      if (lane == p + 1) dp = d1;
+    }
+    X = __builtin_amdgcn_mfma_f32_32x32x2f32(-a, mine ? u0 * id0 : u1s * id1, X, 0, 0, 0);
   }
   if (w == 0) {
     const double lv = (lane < 32) ? log((double)dp) : 0.0;
