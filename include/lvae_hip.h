@@ -113,7 +113,7 @@ size_t lvae_kl_closed_workspace_size(int n, int L);
  * params [L, n_params] fp64; noise [L] fp64; kl [L] fp64; info [L] int32.
  * workspace: lvae_kl_closed_workspace_size(n, L) bytes, 256-B aligned.
  * need_bwd != 0 also writes the backward's S-GEMM operand (fp16 planes of K^-1 diag(sqrt v),
- * per-row scales) into the workspace; lvae_kl_closed_bwd_f32 requires a need_bwd forward.      */
+ * one power-of-two scale per dim) into the workspace; the backward requires a need_bwd forward. */
 int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
                            const double* params, const double* noise, const double* mu, const double* logv,
                            int ld_mu, double* kl, int32_t* info, void* workspace, int need_bwd,
@@ -142,6 +142,14 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
                            const double* params, const double* mu, const double* logv, int ld_mu,
                            const double* gkl, double* dmu, double* dlogv, double* dparams, double* dnoise,
                            void* workspace, void* stream);
+/* The same backward in its two independent halves (lvae_kl_closed_bwd_f32 = _latent then _hyper), for
+ * callers that start the encoder's backward on d/d(mu, logv) while the hyper-parameter half (the
+ * S = K^-1 V K^-1 GEMM and the Gram adjoint: ~all of the backward's time) still runs. Either order. */
+int lvae_kl_closed_bwd_latent_f32(int n, int L, const double* logv, int ld_mu, const double* gkl, double* dmu,
+                                  double* dlogv, void* workspace, void* stream);
+int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                                 const double* params, const double* gkl, double* dparams, double* dnoise,
+                                 void* workspace, void* stream);
 
 /* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
  * 256-wide pivot blocks -- the default Regime B inverse of lvae_kl_closed_fwd_f32: per pivot block k,

@@ -243,10 +243,10 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   return lvae_kl_closed_reduce_f32(spec, x, ldx, n, L, params, noise, mu, logv, ld_mu, kl, workspace, need_bwd, stream);
 }
 
-int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,
-                           const double* mu, const double* logv, int ld_mu, const double* gkl, double* dmu,
-                           double* dlogv, double* dparams, double* dnoise, void* workspace, void* stream) {
-  (void)mu;
+// d kl / d (params, noise): S = K^-1 V K^-1, then the fused Gram adjoint
+int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
+                                 const double* params, const double* gkl, double* dparams, double* dnoise,
+                                 void* workspace, void* stream) {
   if (!spec) return -1;
   if (!workspace || ((uintptr_t)workspace & 255)) return -15;
   hipStream_t st = (hipStream_t)stream;
@@ -264,14 +264,34 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
     LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, S, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
                          gkl, ws.part, dparams, dnoise, st));
   }
-  {
-    ProfScope ps(LVAE_PH_BWD_ELEM, st);
-    const int64_t tot = (int64_t)n * L;
-    kl_bwd_elem_kernel<<<cdiv(tot, 256), 256, 0, st>>>(logv, ld_mu, n, np_, L, ws.alpha, ws.kdiag, gkl, dmu,
-                                                        dlogv);
-  }
   LVAE_CHECK_LAUNCH();
   return 0;
+}
+
+// d kl / d (mu, logv): elementwise from K^-1 mu and diag K^-1 (the forward's)
+int lvae_kl_closed_bwd_latent_f32(int n, int L, const double* logv, int ld_mu, const double* gkl, double* dmu,
+                                  double* dlogv, void* workspace, void* stream) {
+  if (n <= 0) return -4;
+  if (L <= 0) return -5;
+  if (!logv || ld_mu < L) return -8;
+  if (!gkl || !dmu || !dlogv) return -10;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -15;
+  hipStream_t st = (hipStream_t)stream;
+  const int np_ = lvae_kl_closed_padded_n(n);
+  KLWorkspace ws((char*)workspace, np_, L);
+  ProfScope ps(LVAE_PH_BWD_ELEM, st);
+  const int64_t tot = (int64_t)n * L;
+  kl_bwd_elem_kernel<<<cdiv(tot, 256), 256, 0, st>>>(logv, ld_mu, n, np_, L, ws.alpha, ws.kdiag, gkl, dmu, dlogv);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L, const double* params,
+                           const double* mu, const double* logv, int ld_mu, const double* gkl, double* dmu,
+                           double* dlogv, double* dparams, double* dnoise, void* workspace, void* stream) {
+  (void)mu;
+  LVAE_TRY(lvae_kl_closed_bwd_latent_f32(n, L, logv, ld_mu, gkl, dmu, dlogv, workspace, stream));
+  return lvae_kl_closed_bwd_hyper_f32(spec, x, ldx, n, L, params, gkl, dparams, dnoise, workspace, stream);
 }
 
 const char* lvae_version(void) { return "lvae_hip 0.1.0 gfx950"; }

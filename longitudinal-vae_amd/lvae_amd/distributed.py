@@ -69,8 +69,8 @@ def shard_bounds(n, world, rank):
 
 
 def _hip_kl(spec, params, noise, mu, logv, x):
-    from .elbo import _KLClosedFn
-    return _KLClosedFn.apply(params, noise, mu, logv, x, spec)
+    from .elbo import _kl_closed_apply
+    return _kl_closed_apply(params, noise, mu, logv, x, spec, None)
 
 
 class LatentShardedClosedStep:

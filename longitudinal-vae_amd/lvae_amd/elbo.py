@@ -95,17 +95,52 @@ def kl_closed_prefactor(covar_modules, train_x, likelihoods, L, stream):
     return KLFactor(spec, params, noise, train_x, stream)
 
 
-class _KLClosedFn(torch.autograd.Function):
+class _KLState:
+    """What the hyper-parameter half of the backward needs from the forward (filled by _KLClosedFn)."""
+    ws = p = x64 = spec = None
+    n = L = 0
+
+
+class _KLHyperFn(torch.autograd.Function):
+    """A zero-valued [L] term carrying d kl / d (params, noise) (lvae_kl_closed_bwd_hyper_f32: the S GEMM
+    and the Gram adjoint, ~all of the KL backward's time) as a node of its own.  Created before the
+    (mu, logvar) node, it runs after it in the backward (autograd runs later-created ready nodes first),
+    so the encoder's backward gets d kl / d (mu, logvar) from the cheap elementwise half and runs on its
+    stream beside this one's GEMMs."""
+
     @staticmethod
-    def forward(ctx, params, noise, mu, logv, x, spec, factor=None):
+    def forward(ctx, params, noise, state, L):
+        ctx.state = state
+        ctx.in_dtypes = (params.dtype, noise.dtype, noise.shape)
+        return torch.zeros(L, dtype=torch.float64, device=params.device)
+
+    @staticmethod
+    def backward(ctx, gkl):
+        lib = _lib.lib()
+        st = ctx.state
+        g = gkl.detach().to(torch.float64).reshape(st.L).contiguous()
+        dp = torch.empty_like(st.p)
+        dnz = torch.empty(st.L, dtype=torch.float64, device=st.p.device)
+        rc = lib.lvae_kl_closed_bwd_hyper_f32(st.spec, _lib.ptr(st.x64), st.x64.shape[1], st.n, st.L, _lib.ptr(st.p),
+                                              _lib.ptr(g), _lib.ptr(dp), _lib.ptr(dnz), _lib.ptr(st.ws),
+                                              _lib.stream_ptr())
+        _lib.check(rc, "kl_closed_bwd_hyper")
+        pd, nd, nshape = ctx.in_dtypes
+        return dp.to(pd), dnz.to(nd).reshape(nshape), None, None
+
+
+class _KLClosedFn(torch.autograd.Function):
+    """kl [L] from (mu, logvar) (and the detached hyper-parameters); backward: d kl / d (mu, logvar)
+    only (lvae_kl_closed_bwd_latent_f32), the hyper-parameter half is _KLHyperFn's."""
+
+    @staticmethod
+    def forward(ctx, params, noise, mu, logv, x, spec, factor, state, need_bwd):
         lib = _lib.lib()
         n, L = mu.shape
         dev = mu.device
         mu64 = mu.detach().to(torch.float64).contiguous()
         lv64 = logv.detach().to(torch.float64).contiguous()
         kl = torch.empty(L, dtype=torch.float64, device=dev)
-        # the backward's S GEMM operand is written by the forward only when a backward can follow
-        need_bwd = int(any(t.requires_grad for t in (params, noise, mu, logv)))
         if factor is not None:
             if factor.n != n or factor.L != L:
                 raise ValueError(f"factor is for n={factor.n}, L={factor.L}; got n={n}, L={L}")
@@ -126,27 +161,35 @@ class _KLClosedFn(torch.autograd.Function):
                                             _lib.ptr(ws), need_bwd, _lib.stream_ptr())
             _lib.check(rc, "kl_closed_fwd")
         _check_info(info, "KL_closed cholesky")
-        ctx.save_for_backward(p, mu64, lv64, x64, ws)
-        ctx.spec = spec
-        ctx.in_dtypes = (params.dtype, noise.dtype, noise.shape, mu.dtype, logv.dtype)
+        state.ws, state.p, state.x64, state.spec, state.n, state.L = ws, p, x64, spec, n, L
+        ctx.save_for_backward(lv64, ws)
+        ctx.in_dtypes = (mu.dtype, logv.dtype)
         return kl
 
     @staticmethod
     def backward(ctx, gkl):
         lib = _lib.lib()
-        p, mu64, lv64, x64, ws = ctx.saved_tensors
-        n, L = mu64.shape
+        lv64, ws = ctx.saved_tensors
+        n, L = lv64.shape
         g = gkl.detach().to(torch.float64).reshape(L).contiguous()
-        dmu = torch.empty_like(mu64)
+        dmu = torch.empty_like(lv64)
         dlv = torch.empty_like(lv64)
-        dp = torch.empty_like(p)
-        dnz = torch.empty(L, dtype=torch.float64, device=p.device)
-        rc = lib.lvae_kl_closed_bwd_f32(ctx.spec, _lib.ptr(x64), x64.shape[1], n, L, _lib.ptr(p), _lib.ptr(mu64),
-                                        _lib.ptr(lv64), L, _lib.ptr(g), _lib.ptr(dmu), _lib.ptr(dlv), _lib.ptr(dp),
-                                        _lib.ptr(dnz), _lib.ptr(ws), _lib.stream_ptr())
-        _lib.check(rc, "kl_closed_bwd")
-        pd, nd, nshape, md, ld = ctx.in_dtypes
-        return dp.to(pd), dnz.to(nd).reshape(nshape), dmu.to(md), dlv.to(ld), None, None, None
+        rc = lib.lvae_kl_closed_bwd_latent_f32(n, L, _lib.ptr(lv64), L, _lib.ptr(g), _lib.ptr(dmu), _lib.ptr(dlv),
+                                               _lib.ptr(ws), _lib.stream_ptr())
+        _lib.check(rc, "kl_closed_bwd_latent")
+        md, ld = ctx.in_dtypes
+        return None, None, dmu.to(md), dlv.to(ld), None, None, None, None, None
+
+
+def _kl_closed_apply(params, noise, mu, log_var, train_x, spec, factor):
+    L = mu.shape[1]
+    need_bwd = int(torch.is_grad_enabled() and any(t.requires_grad for t in (params, noise, mu, log_var)))
+    state = _KLState()
+    hyper = None
+    if torch.is_grad_enabled() and (params.requires_grad or noise.requires_grad):
+        hyper = _KLHyperFn.apply(params, noise, state, L)  # (first: its node runs after the (mu, logvar) one)
+    kl = _KLClosedFn.apply(params.detach(), noise.detach(), mu, log_var, train_x, spec, factor, state, need_bwd)
+    return kl if hyper is None else kl + hyper
 
 
 def _stack_modules(covar_modules):
@@ -170,12 +213,12 @@ def KL_closed_batched(covar_modules, train_x, likelihoods, mu, log_var, factor=N
     inverse were launched ahead (its hyperparameters are the ones differentiated)."""
     L = mu.shape[1]
     if factor is not None:
-        return _KLClosedFn.apply(factor.params, factor.noise, mu, log_var, train_x, factor.spec, factor)
+        return _kl_closed_apply(factor.params, factor.noise, mu, log_var, train_x, factor.spec, factor)
     spec, params = _stack_modules(covar_modules)
     if params.shape[0] != L:
         raise ValueError(f"kernel batch {params.shape[0]} != latent dims {L}")
     noise = _noise_vector(likelihoods, L).to(params.device)
-    return _KLClosedFn.apply(params, noise, mu, log_var, train_x, spec)
+    return _kl_closed_apply(params, noise, mu, log_var, train_x, spec, None)
 
 
 def KL_closed(covar_module, train_x, likelihoods, data, mu, log_var):

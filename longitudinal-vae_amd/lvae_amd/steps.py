@@ -38,9 +38,10 @@ class ClosedStep:
             # enqueued first, on the caller's stream, and the whole ConvVAE runs on one second stream
             # beside them -- the encoder (its (mu, logvar) join the KL through an event), then the
             # decoder and recon loss, which do not depend on the KL at all.  Autograd runs each
-            # backward op on its forward's stream: the decoder backward beside the KL backward (S
-            # GEMM + Gram adjoint), the encoder backward after both.  (Two extra streams at most: the
-            # box exposes 4 hardware queues, and the sweep keeps one side stream of its own.)
+            # backward op on its forward's stream: the decoder backward beside the KL reduce, the
+            # encoder backward (once d kl / d (mu, logvar) is out: elbo._KLClosedFn) beside the KL's
+            # hyper-parameter half (S GEMM + Gram adjoint, elbo._KLHyperFn).  (Two extra streams at
+            # most: the box exposes 4 hardware queues, and the inverse keeps one side stream of its own.)
             main = torch.cuda.current_stream(img.device)
             vst = self._stream("_vae_stream", img.device)
             vst.wait_stream(main)  # the previous step's updates, before the factorisation is queued
@@ -57,9 +58,24 @@ class ClosedStep:
             mu.record_stream(main)
             log_var.record_stream(main)
             kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var, factor=factor)
+            L = mu.shape[1]
+            if self.loss_function == "mse":
+                gp = kl.sum() / L
+                rec_term, gp_term = recon_loss, self.weight * gp
+            else:
+                gp = kl.sum()
+                rec_term, gp_term = nll_loss, gp
+            # The backward from the two loss terms as separate roots, called on the ConvVAE's stream:
+            # the decoder's backward then starts as soon as its forward is done, beside the KL reduce
+            # on the caller's stream, instead of behind it (a root summed on the caller's stream
+            # would hand the decoder its gradient only after everything queued there).
+            with torch.cuda.stream(vst):
+                torch.autograd.backward([rec_term, gp_term])
             main.wait_stream(vst)
-            recon_loss.record_stream(main)
-            nll_loss.record_stream(main)
+            for t in (recon_loss, nll_loss, rec_term):
+                t.record_stream(main)
+            net = rec_term.detach() + gp_term.detach()
+            return net, recon_loss.detach(), nll_loss.detach(), gp.detach()
         else:
             recon, mu, log_var = self.vae(img, eps)
             mse, nll = self.vae.loss_function(recon, img, mask)
