@@ -254,7 +254,8 @@ def run_closed(args, world, rank, dev):
         inputs = (img[lo:hi].contiguous(), mask[lo:hi].contiguous(), X, eps[lo:hi].contiguous())
         d0, d1 = shard_bounds(L, world, rank)
     else:
-        step = ClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True)
+        step = ClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True,
+                          vae_stream_priority=args.vae_stream_priority)
         inputs = (img, mask, X, eps)
         d0, d1 = 0, L
 
@@ -506,6 +507,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-timing", action="store_true")
     ap.add_argument("--no-c2", action="store_true")
+    ap.add_argument("--vae-stream-priority", dest="vae_stream_priority", type=int, default=-1,
+                    help="priority of the ConvVAE's stream in the closed step (lower = higher; 0 = default)")
     args = ap.parse_args()
 
     world, rank, local = setup_dist()

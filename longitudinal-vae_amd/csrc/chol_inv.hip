@@ -40,6 +40,7 @@
 #include "prof.hpp"
 #include "pv_lds.hpp"
 #include "side_stream.hpp"
+#include "x3_c16.hpp"
 
 namespace lvae {
 
@@ -829,7 +830,34 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
       const int64_t tb = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;   // B tile (i, j)
       const int64_t tbt = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // B tile (j, i)
       const float sb = g.bh_out ? g.bsc[l] : 0.f;  // the dim's split scale of B (ci_bscale_kernel)
-      if (g.bh_out) {
+      if (g.bh_out && kCiBC16) {
+        // B(i, j) = T diag(sqrt v_j), column-scaled, straight from the registers into the chunk-major
+        // planes (x3_c16.hpp): tile (i, j) is the 128 KB run of chunks 16 j .. 16 j + 15 of row block i;
+        // lane (w, lane): chunk (w & 3) * 4 + 2 b + (lane & 31) / 16, row (w >> 2) 128 + 32 a + .. + 4 (lane
+        // >> 5), half (lane & 15) ^ 8 (bit 3 of the row = bit 0 of e >> 2: a compile-time choice per e)
+        const int64_t tc = c16_off(l, np_, i * kSwB, j * kSwB);
+        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(g.bh_out + tc, (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(g.bl_out + tc, (short)0, 0x7fffffff, 0x00020000);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const int vb0 = (((w & 3) * 4 + ((lane & 31) >> 4)) * kC16Part + ((w >> 2) * 128 + 4 * (lane >> 5)) * 16) * 2;
+        const int vk0 = (lane & 15) * 2, vk1 = ((lane & 15) ^ 8) * 2;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float mc = sb * kl_sv[kSwB + sx_col(b)];
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const float y = acc[a][b][e] * mc;
+              const _Float16 yh = (_Float16)y;
+              const _Float16 yl = (_Float16)(y - (float)yh);
+              const int vo = vb0 + (((e >> 2) & 1) ? vk1 : vk0);
+              const int so = (2 * b * kC16Part + (32 * a + (e & 3) + 8 * (e >> 2)) * 16) * 2;
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yh), rh, vo, so, 0);
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yl), rl, vo, so, 0);
+            }
+        }
+      } else if (g.bh_out) {
         // B(i, j) = T diag(sqrt v_j): column-scaled, straight from the registers
         const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(g.bh_out + tb, (short)0, 0x7fffffff, 0x00020000);
         const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(g.bl_out + tb, (short)0, 0x7fffffff, 0x00020000);
@@ -856,7 +884,9 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
           *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
           if (g.bh_out) {
             const f32x4 s4 = *reinterpret_cast<const f32x4*>(&kl_sv[r0]);
-            ci_split4(v * s4, sb, g.bh_out + tbt + (int64_t)c * np_ + r0, g.bl_out + tbt + (int64_t)c * np_ + r0);
+            // B(j, i) row c, columns r0 .. r0 + 3 (one 4-half run of a chunk either way)
+            const int64_t o = kCiBC16 ? c16_off(l, np_, j * kSwB + c, i * kSwB + r0) : tbt + (int64_t)c * np_ + r0;
+            ci_split4(v * s4, sb, g.bh_out + o, g.bl_out + o);
           }
         });
     } else if (i != j) {

@@ -23,6 +23,7 @@
 // column): the 32 tiles an XCD runs at once form a 4 x 8 block sharing 4 A and 8 B panels in its L2
 // (r3, scripts/gemm_ab.py: 3.19 vs 3.46 ms at np = 4096, L = 16 against the row-major order; 51.1 vs
 // 55.9 ms at np = 16384, L = 4).
+#include "x3_c16.hpp"
 #include "x3_dma.hpp"
 #include "x3_gemm4.hpp"
 
@@ -284,13 +285,56 @@ __global__ __launch_bounds__(512) void syrk_tiles_kernel(const _Float16* __restr
                                               ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
 }
 
+// The S GEMM on the chunk-major planes (x3_c16.hpp): NS-stage ring of 16-deep chunks, fragments of the
+// next chunk read under the current chunk's MFMAs.  Same tile order, K split and epilogue as
+// syrk_tiles_kernel.
+template <int NS>
+__global__ __launch_bounds__(512) void syrk_c16_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
+                                                       const float* __restrict__ bsc, float* __restrict__ S,
+                                                       float* __restrict__ Sx, int np_, int ntl, int nwg, int L, int ns) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[NS * kC16Stage];
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int sp = wgid / (ntl * L), l = (wgid / ntl) % L, nt = np_ / kSxT;
+  int I, J;
+  sx_tri_blocked(wgid % ntl, nt, I, J);
+  const int kb0 = sp * nt / ns, kb1 = (sp + 1) * nt / ns;
+  const int64_t ld = np_;
+  const int64_t base = (int64_t)l * np_ * np_, c0 = (int64_t)kb0 * (kSxT / kC16BK) * kC16Part;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  if (kb1 > kb0) {
+    const int64_t pa = c16_panel(l, np_, I) + c0, pb = c16_panel(l, np_, J) + c0;
+    c16_gemm<NS>(Bh + pa, Bl - Bh, pb - pa, (kb1 - kb0) * (kSxT / kC16BK), lds, acc);
+  }
+  const float sc = bsc[l], inv = 1.0f / (sc * sc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* C = (sp == 0 ? S : Sx + (int64_t)(sp - 1) * L * np_ * np_) + base + (int64_t)I * kSxT * ld + J * kSxT;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+  const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), rc, vo,
+                                              ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+}
+
 int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st) {
   if (np_ % kSxT) return -1;
   const int64_t per = (int64_t)np_ * np_;
   const int ns = syrk_x3_splits(np_, L);
   if (ns > 1 && !Sx) return -2;
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L * ns;
-  syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
+  if (kCiBC16)
+    syrk_c16_kernel<kC16NS><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
+  else
+    syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -307,6 +351,10 @@ int syrk_dev_variant(int variant, int np_, int L, const float* rsc, const _Float
     syrk_x3_kernel<1><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, np_);
   else if (variant == 4)  // the product kernel (rsc[l * np] read as the dims' scales: ones)
     syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
+  else if (variant == 5)  // chunk-major planes (x3_c16.hpp), 4-stage ring
+    syrk_c16_kernel<4><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
+  else if (variant == 6)  // chunk-major planes, 5-stage ring (all 160 KB of LDS)
+    syrk_c16_kernel<5><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
   else if (variant == 3)
     syrk_h2_kernel<<<2 * nwg, 256, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, np_, 2 * ntl, 2 * nwg, L);
   else

@@ -19,15 +19,19 @@ from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_b
 
 class ClosedStep:
     def __init__(self, vae, kernel, likelihood, optimiser, weight=0.15, loss_function="mse",
-                 constrain_scales=True, grad_hook=None):
+                 constrain_scales=True, grad_hook=None, vae_stream_priority=-1):
         self.vae, self.kernel, self.lik, self.opt = vae, kernel, likelihood, optimiser
         self.weight, self.loss_function, self.constrain_scales = weight, loss_function, constrain_scales
         self.grad_hook = grad_hook  # e.g. the data-parallel all-reduce
+        # The ConvVAE's stream is created with a high priority by default: its kernels are small and
+        # would otherwise queue behind the KL's grids of thousands of LDS-heavy workgroups (one per CU)
+        # until those drain, which put the encoder backward at the end of the step.
+        self.vae_stream_priority = vae_stream_priority
 
     def _stream(self, name, device):
         s = getattr(self, name, None)
         if s is None or s.device != device:
-            s = torch.cuda.Stream(device=device)
+            s = torch.cuda.Stream(device=device, priority=self.vae_stream_priority)
             setattr(self, name, s)
         return s
 
