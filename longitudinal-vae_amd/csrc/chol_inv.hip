@@ -42,7 +42,15 @@
 #include "side_stream.hpp"
 #include "x3_c16.hpp"
 
+#ifndef LVAE_CI_C16
+#define LVAE_CI_C16 1
+#endif
+
 namespace lvae {
+
+// the trtri / lauum planes (Y, Y^T, X^T) in the chunk-major layout and their GEMMs on the c16 core
+// (x3_c16.hpp: a 4-stage ring, 128 KB of LDS beside the epilogues' own); 0: row-major planes on x3_dma.hpp
+constexpr bool kCiC16 = LVAE_CI_C16 != 0;
 
 struct CiScratch {
   _Float16 *Ch[2], *Cl[2];  // [L][np][256] planes of the updated column (pass k's C operand), by parity
@@ -596,8 +604,10 @@ __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_,
     const int r = e >> 3, c = (e & 7) * 8;
     const x3_half8 h = *reinterpret_cast<const x3_half8*>(S.Dh + od + r * kSwB + c);
     const x3_half8 lo = *reinterpret_cast<const x3_half8*>(S.Dl + od + r * kSwB + c);
-    *reinterpret_cast<x3_half8*>(Yh + oy + (int64_t)r * np_ + c) = h;
-    *reinterpret_cast<x3_half8*>(Yl + oy + (int64_t)r * np_ + c) = lo;
+    // (chunk-major: an aligned 8-half run stays one 16-B run under the swizzle)
+    const int64_t oyc = kCiC16 ? c16_off(l, np_, k * kSwB + 64 * pa + r, k * kSwB + 64 * pb + c) : oy + (int64_t)r * np_ + c;
+    *reinterpret_cast<x3_half8*>(Yh + oyc) = h;
+    *reinterpret_cast<x3_half8*>(Yl + oyc) = lo;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       tp[0][r][c + q] = h[q];
@@ -607,8 +617,9 @@ __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_,
   __syncthreads();
   for (int e = t; e < 64 * 64; e += 256) {  // Y^T (b, a) row c, column r = D (a, b) (r, c)
     const int c = e >> 6, r = e & 63;
-    YTh[oyt + (int64_t)c * np_ + r] = tp[0][r][c];
-    YTl[oyt + (int64_t)c * np_ + r] = tp[1][r][c];
+    const int64_t o = kCiC16 ? c16_off(l, np_, k * kSwB + 64 * pb + c, k * kSwB + 64 * pa + r) : oyt + (int64_t)c * np_ + r;
+    YTh[o] = tp[0][r][c];
+    YTl[o] = tp[1][r][c];
   }
 }
 
@@ -786,21 +797,40 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     kl_mu[t] = (float)g.mu[p];
     kl_sv[t] = g.sv[p];
   }
-  const float inv = 1.0f / sx_gemm_scaled(ah, al, bh, bl, np_, nkb, sprod, lds, acc);
+  float inv;
+  if constexpr (kCiC16) {
+    // operands: A = L planes (row-major) for X, else chunk-major panels from block kb0 on; B chunk-major
+    const int64_t kc0 = (int64_t)kb0 * (kSwB / kC16BK) * kC16Part;
+    const C16Opnd A = MODE == kCiX ? C16Opnd{ah, g.al - g.ah, np_}
+                                   : C16Opnd{g.ah + c16_panel(l, np_, i) + kc0, g.al - g.ah, 0};
+    const C16Opnd B{g.bh + c16_panel(l, np_, j) + kc0, g.bl - g.bh, 0};
+    C16BlockRescale rs{sprod, 1.f};
+    c16_gemm<4>(A, B, nkb * (kSwB / kC16BK), lds, acc, rs);
+    inv = 1.0f / rs.scur;
+  } else {
+    inv = 1.0f / sx_gemm_scaled(ah, al, bh, bl, np_, nkb, sprod, lds, acc);
+  }
   if constexpr (MODE == kCiX) {
     const float sx = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
     const int64_t ot = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // X^T tile (j, i)
     ci_transposed_out(acc, inv, lds, [&](int c, int r0, f32x4 v) {
-      ci_split4(v, sx, g.oth + ot + (int64_t)c * np_ + r0, g.otl + ot + (int64_t)c * np_ + r0);
+      const int64_t o = kCiC16 ? c16_off(l, np_, j * kSwB + c, i * kSwB + r0) : ot + (int64_t)c * np_ + r0;
+      ci_split4(v, sx, g.oth + o, g.otl + o);
     });
     if (threadIdx.x == 0) S.xsc[sl + (int64_t)i * nt + j] = sx;
   } else if constexpr (MODE == kCiY) {
     const float sy = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
     const int64_t ot = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;   // Y tile (i, j)
     const int64_t ott = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // Y^T tile (j, i)
-    ci_planes_out(acc, -inv, sy, g.oh + ot, g.ol + ot, np_);
+    if constexpr (kCiC16) {
+      const int64_t oc = c16_off(l, np_, i * kSwB, j * kSwB);
+      c16_tile_planes_out(acc, [&](int) { return -inv * sy; }, g.oh + oc, g.ol + oc);
+    } else {
+      ci_planes_out(acc, -inv, sy, g.oh + ot, g.ol + ot, np_);
+    }
     ci_transposed_out(acc, -inv, lds, [&](int c, int r0, f32x4 v) {
-      ci_split4(v, sy, g.oth + ott + (int64_t)c * np_ + r0, g.otl + ott + (int64_t)c * np_ + r0);
+      const int64_t o = kCiC16 ? c16_off(l, np_, j * kSwB + c, i * kSwB + r0) : ott + (int64_t)c * np_ + r0;
+      ci_split4(v, sy, g.oth + o, g.otl + o);
     });
     if (threadIdx.x == 0) S.ysc[sl + (int64_t)i * nt + j] = sy;
   } else {
@@ -832,31 +862,9 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
       const float sb = g.bh_out ? g.bsc[l] : 0.f;  // the dim's split scale of B (ci_bscale_kernel)
       if (g.bh_out && kCiBC16) {
         // B(i, j) = T diag(sqrt v_j), column-scaled, straight from the registers into the chunk-major
-        // planes (x3_c16.hpp): tile (i, j) is the 128 KB run of chunks 16 j .. 16 j + 15 of row block i;
-        // lane (w, lane): chunk (w & 3) * 4 + 2 b + (lane & 31) / 16, row (w >> 2) 128 + 32 a + .. + 4 (lane
-        // >> 5), half (lane & 15) ^ 8 (bit 3 of the row = bit 0 of e >> 2: a compile-time choice per e)
+        // planes (x3_c16.hpp): tile (i, j) is the 128 KB run of chunks 16 j .. 16 j + 15 of row block i
         const int64_t tc = c16_off(l, np_, i * kSwB, j * kSwB);
-        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(g.bh_out + tc, (short)0, 0x7fffffff, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(g.bl_out + tc, (short)0, 0x7fffffff, 0x00020000);
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        const int vb0 = (((w & 3) * 4 + ((lane & 31) >> 4)) * kC16Part + ((w >> 2) * 128 + 4 * (lane >> 5)) * 16) * 2;
-        const int vk0 = (lane & 15) * 2, vk1 = ((lane & 15) ^ 8) * 2;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const float mc = sb * kl_sv[kSwB + sx_col(b)];
-#pragma unroll
-          for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              const float y = acc[a][b][e] * mc;
-              const _Float16 yh = (_Float16)y;
-              const _Float16 yl = (_Float16)(y - (float)yh);
-              const int vo = vb0 + (((e >> 2) & 1) ? vk1 : vk0);
-              const int so = (2 * b * kC16Part + (32 * a + (e & 3) + 8 * (e >> 2)) * 16) * 2;
-              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yh), rh, vo, so, 0);
-              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yl), rl, vo, so, 0);
-            }
-        }
+        c16_tile_planes_out(acc, [&](int b) { return sb * kl_sv[kSwB + sx_col(b)]; }, g.bh_out + tc, g.bl_out + tc);
       } else if (g.bh_out) {
         // B(i, j) = T diag(sqrt v_j): column-scaled, straight from the registers
         const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(g.bh_out + tb, (short)0, 0x7fffffff, 0x00020000);

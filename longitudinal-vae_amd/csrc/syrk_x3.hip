@@ -308,7 +308,7 @@ __global__ __launch_bounds__(512) void syrk_c16_kernel(const _Float16* __restric
     for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
   if (kb1 > kb0) {
     const int64_t pa = c16_panel(l, np_, I) + c0, pb = c16_panel(l, np_, J) + c0;
-    c16_gemm<NS>(Bh + pa, Bl - Bh, pb - pa, (kb1 - kb0) * (kSxT / kC16BK), lds, acc);
+    c16_gemm<NS>(C16Opnd{Bh + pa, Bl - Bh, 0}, C16Opnd{Bh + pb, Bl - Bh, 0}, (kb1 - kb0) * (kSxT / kC16BK), lds, acc);
   }
   const float sc = bsc[l], inv = 1.0f / (sc * sc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

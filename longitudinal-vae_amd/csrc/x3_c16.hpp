@@ -12,6 +12,10 @@
 // (stored at position kk ^ 8 (r >> 3 & 1)): the producer applies the swizzle, the DMA copies linearly,
 // and a ds_read_b128 lane group (16 consecutive rows, one 8-half group) then covers all 64 banks.
 //
+// An operand may also be a plain row-major plane (rows of ld halves, K contiguous; C16Opnd.ld != 0): its
+// DMA pieces are then 32 rows x 2 16-B chunks, the chunk swizzle applied on the global address (the
+// LDS image is the same), at twice the requests per byte.
+//
 // 512 threads = 8 waves (2 along M x 4 along N, 128 x 64 each = 4 x 2 blocks of
 // v_mfma_f32_32x32x16_f16, three products per block): 24 MFMAs, 12 ds_read_b128 and 4 DMA pieces per
 // wave and stage.  The accumulator layout is x3_dma.hpp's (sx_row / sx_col).
@@ -42,17 +46,43 @@ __host__ __device__ inline int64_t c16_panel(int64_t l, int np_, int R) {
   return l * np_ * np_ + (int64_t)R * (np_ >> 4) * kC16Part;
 }
 
-// one stage: 4 parts x 8 pieces of 1 KB; wave w issues pieces 4 (w & 1) .. + 3 of part w >> 1.  Part p's
-// panel is a + (p & 1) lo + (p >> 1) b (halves): uniform integer arithmetic, no select branches.
-__device__ inline void c16_issue(const _Float16* __restrict__ a, int64_t lo, int64_t b, int c,
-                                 _Float16* __restrict__ stage) {
+// one operand of the core: the panel of its 256 rows from the first K chunk of the range on, in the
+// chunk-major layout (ld == 0) or row-major (row stride ld halves); lo = lo plane - hi plane (halves)
+struct C16Opnd {
+  const _Float16* hi;
+  int64_t lo;
+  int64_t ld;
+};
+
+// the DMA addressing of one wave: part p = w >> 1 (A hi, A lo, B hi, B lo), pieces 4 (w & 1) .. + 3 of it
+// (32-row blocks).  Piece blk of stage c reads base + c cs + blk bs + lane_off: chunk-major cs = 4096,
+// bs = 512, lane_off = 8 lane (1 KB runs); row-major cs = 16, bs = 32 ld, lane_off = row (lane >> 1) and
+// logical chunk (lane & 1) ^ (bit 3 of the row) (the swizzle moved to the source).  Set once per GEMM
+// from wave-uniform scalars: no branch at the issue.
+struct C16Dma {
+  const _Float16* g;  // + lane_off, + (w & 1) * 4 blocks
+  int64_t cs, bs;
+  int doff;           // LDS offset (halves) of the wave's first piece in a stage
+};
+__device__ inline C16Dma c16_dma(const C16Opnd& A, const C16Opnd& B) {
   // the wave id through readfirstlane: provably uniform, so the LDS base (M0) needs no waterfall loop
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), p = w >> 1;
-  const _Float16* g = a + (p & 1) * lo + (p >> 1) * b + (int64_t)c * kC16Part + (w & 1) * 2048 + lane * 8;
-  _Float16* d = stage + p * kC16Part + (w & 1) * 2048;
+  const bool isb = p >= 2;
+  const uintptr_t hi = isb ? (uintptr_t)B.hi : (uintptr_t)A.hi;
+  const int64_t lo = isb ? B.lo : A.lo, ld = isb ? B.ld : A.ld;
+  C16Dma d;
+  d.cs = ld ? kC16BK : kC16Part;
+  d.bs = ld ? 32 * ld : 512;
+  const int64_t lane_off = ld ? (lane >> 1) * ld + 8 * ((lane & 1) ^ ((lane >> 4) & 1)) : 8 * lane;
+  d.g = reinterpret_cast<const _Float16*>(hi) + (p & 1) * lo + 4 * (w & 1) * d.bs + lane_off;
+  d.doff = p * kC16Part + (w & 1) * 2048;
+  return d;
+}
+__device__ inline void c16_issue(const C16Dma& d, int c, _Float16* __restrict__ stage) {
+  const _Float16* g = d.g + (int64_t)c * d.cs;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
-    __builtin_amdgcn_global_load_lds((const void*)(g + q * 512), (void*)(d + q * 512), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(g + q * d.bs), (void*)(stage + d.doff + q * 512), 16, 0, 0);
 }
 
 struct C16Frags {
@@ -110,11 +140,12 @@ __device__ inline void c16_interleave() {
 // the DMA of stage s+NS-1 is issued.  Every step issues one (branch-free: past the last chunk it re-reads
 // chunk nk-1 into the buffer of stage s-1, which no later step reads for real), so stages s+2 .. s+NS-2
 // (NS - 3 of them) may stay in flight while stage s+1 must have landed.  The last step reads a stale
-// buffer into `nxt` (unused).
-template <int NS>
-__device__ inline void c16_step(const _Float16* __restrict__ a, int64_t lo, int64_t b, int s, int nk,
-                                _Float16* __restrict__ lds, const C16Frags& cur, C16Frags& nxt,
-                                sx_f32x16 (&acc)[4][2]) {
+// buffer into `nxt` (unused).  rescale(s, acc) runs first (callers with per-K-block split scales move
+// the accumulators to the units of the block that starts at chunk s).
+template <int NS, typename Rescale>
+__device__ inline void c16_step(const C16Dma& dma, int s, int nk, _Float16* __restrict__ lds, const C16Frags& cur,
+                                C16Frags& nxt, sx_f32x16 (&acc)[4][2], Rescale& rescale) {
+  rescale(s, acc);
   c16_wait_vm<4 * (NS - 3)>();
   // this wave's reads of stage s (into cur, issued a step ago under the MFMAs) retired: a counted wait
   // the compiler sees, so it needs none between the reads below and the MFMAs on cur
@@ -126,19 +157,24 @@ __device__ inline void c16_step(const _Float16* __restrict__ a, int64_t lo, int6
   // below the MFMAs into the registers the MFMAs free, exposing their latency at the next barrier)
   c16_read(lds + ((s + 1) % NS) * kC16Stage, nxt);
   __builtin_amdgcn_sched_barrier(0);
-  c16_issue(a, lo, b, min(s + NS - 1, nk - 1), lds + ((s + NS - 1) % NS) * kC16Stage);
+  c16_issue(dma, min(s + NS - 1, nk - 1), lds + ((s + NS - 1) % NS) * kC16Stage);
   c16_mma(cur, acc);
   c16_interleave();
 }
 
-// acc[a][b] += A B^T over nk 16-deep chunks: A = (a hi, a + lo lo), B = (a + b hi, a + b + lo lo) chunk-major
-// panels (stage c of a part at its panel + c * kC16Part); lds = NS * kC16Stage halves, the kernel's only
-// __shared__ object; nk even.  Returns with no DMA outstanding.
-template <int NS>
-__device__ inline void c16_gemm(const _Float16* __restrict__ a, int64_t lo, int64_t b, int nk,
-                                _Float16* __restrict__ lds, sx_f32x16 (&acc)[4][2]) {
+struct C16NoRescale {
+  __device__ void operator()(int, sx_f32x16 (&)[4][2]) const {}
+};
+
+// acc[a][b] += A B^T over nk 16-deep chunks (A, B: C16Opnd panels); lds = NS * kC16Stage halves, the
+// kernel's only staging object; nk even; rescale(s, acc) at the top of every step (state kept in the
+// caller's functor).  Returns with no DMA outstanding.
+template <int NS, typename Rescale>
+__device__ inline void c16_gemm(const C16Opnd& A, const C16Opnd& B, int nk, _Float16* __restrict__ lds,
+                                sx_f32x16 (&acc)[4][2], Rescale& rescale) {
+  const C16Dma dma = c16_dma(A, B);
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s) c16_issue(a, lo, b, min(s, nk - 1), lds + s * kC16Stage);
+  for (int s = 0; s < NS - 1; ++s) c16_issue(dma, min(s, nk - 1), lds + s * kC16Stage);
   c16_wait_vm<4 * (NS - 2)>();
   __builtin_amdgcn_s_barrier();
   C16Frags f0, f1;
@@ -147,10 +183,67 @@ __device__ inline void c16_gemm(const _Float16* __restrict__ a, int64_t lo, int6
   // names (no runtime-indexed register arrays), and no branch between the steps invites the compiler to
   // sink a step's fragment reads past its MFMAs
   for (int s = 0; s < nk; s += 2) {
-    c16_step<NS>(a, lo, b, s, nk, lds, f0, f1, acc);
-    c16_step<NS>(a, lo, b, s + 1, nk, lds, f1, f0, acc);
+    c16_step<NS>(dma, s, nk, lds, f0, f1, acc, rescale);
+    c16_step<NS>(dma, s + 1, nk, lds, f1, f0, acc, rescale);
   }
   c16_wait_vm<0>();  // the re-read pieces past the last chunk: none may land after the workgroup ends
+}
+template <int NS>
+__device__ inline void c16_gemm(const C16Opnd& A, const C16Opnd& B, int nk, _Float16* __restrict__ lds,
+                                sx_f32x16 (&acc)[4][2]) {
+  C16NoRescale none;
+  c16_gemm<NS>(A, B, nk, lds, acc, none);
+}
+
+// per-K-block split scales (operands split with a power-of-two scale per 256 x 256 block, sprod[kb] =
+// sA(kb) sB(kb) in LDS): the accumulators move to the units of each new block at its first chunk (ratios
+// of powers of two: exact); value = acc / scur at the end
+struct C16BlockRescale {
+  const float* sprod;
+  float scur;
+  __device__ void operator()(int s, sx_f32x16 (&acc)[4][2]) {
+    if (s == 0) {
+      scur = sprod[0];
+    } else if ((s & 15) == 0) {
+      const float snew = sprod[s >> 4], ratio = snew / scur;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] *= ratio;
+      scur = snew;
+    }
+  }
+};
+
+// accumulator tile (value = acc * colmul(b), colmul: the multiplier of the lane's column block b) -> the fp16
+// hi / lo planes of one 256 x 256 tile in the chunk-major layout (hi, lo: the tile's base, c16_off of its
+// first element: 16 chunks of 8 KB).  Lane (w, lane) holds chunk (w & 3) 4 + 2 b + (lane & 31) / 16, half
+// (lane & 15) of rows sx_row(a, e); bit 3 of the row is bit 0 of e >> 2, so the half's swizzle is a
+// compile-time choice per e.
+template <typename ColMul>
+__device__ inline void c16_tile_planes_out(const sx_f32x16 (&acc)[4][2], ColMul colmul, _Float16* __restrict__ hi,
+                                           _Float16* __restrict__ lo) {
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hi, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(lo, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int vb0 = (((w & 3) * 4 + ((lane & 31) >> 4)) * kC16Part + ((w >> 2) * 128 + 4 * (lane >> 5)) * 16) * 2;
+  const int vk0 = (lane & 15) * 2, vk1 = ((lane & 15) ^ 8) * 2;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const float mc = colmul(b);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float y = acc[a][b][e] * mc;
+        const _Float16 yh = (_Float16)y;
+        const _Float16 yl = (_Float16)(y - (float)yh);
+        const int vo = vb0 + (((e >> 2) & 1) ? vk1 : vk0);
+        const int so = (2 * b * kC16Part + (32 * a + (e & 3) + 8 * (e >> 2)) * 16) * 2;
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yh), rh, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yl), rl, vo, so, 0);
+      }
+  }
 }
 
 }  // namespace lvae
