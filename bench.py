@@ -44,7 +44,7 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3s_pmc_summary.json")
 # the Cholesky's trailing rank-256 update (chol_inv.hip): U2 alone (MODE kCiU2) when the lookahead chain
 # runs on the side stream (schedule (b), > CI_FUSE_MAX_L dims per call), else fused with U1 (kCiU12)
 CI_FUSE_MAX_L = 16
@@ -309,10 +309,11 @@ def run_closed(args, world, rank, dev):
         flops = Lr * np_ * np_ * (np_ + 1)
         if syrk_ms > 0:
             ach = X3_PRODUCTS * flops / (syrk_ms * 1e-3) / 1e12
-            res["roofline"] = {"kernel": "syrk_tiles_kernel (S = K^-1 V K^-1, syrk_x3.hip; the largest GPU-time share of the step)",
+            res["roofline"] = {"kernel": "syrk_c16_kernel<5> (S = K^-1 V K^-1, syrk_x3.hip on the chunk-major core x3_c16.hpp; "
+                                         "the largest GPU-time share of the step)",
                                "bound": "mfma", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                               "traffic": pmc_traffic(("syrk_tiles_kernel",)) if world == 1 else None,
+                               "traffic": pmc_traffic(("syrk_c16_kernel",)) if world == 1 else None,
                                "traffic_source": os.path.basename(PMC_SUMMARY),
                                "algorithmic_flop_per_launch": X3_PRODUCTS * flops,
                                "fp32_equivalent_tflops": flops / (syrk_ms * 1e-3) / 1e12,

@@ -4,10 +4,11 @@
  * Every entry point is a plain C function over caller-owned device pointers: no allocation of
  * device memory inside, all work enqueued asynchronously on the caller's hipStream_t (passed as
  * void*), safe to call from several host threads.  Process-wide state is limited to (1) the
- * opt-in phase timer (lvae_prof_*) and (2) the sweep's side stream (lvae_spd_sweep_f32,
- * lvae_kl_closed_fwd_f32): one high-priority stream + seven events (fork, prep, c, and two pairs
- * alternating by pass parity) per (device, caller stream), created on first use, kept for the process lifetime, and guarded by a mutex held
- * for each call's whole enqueue sequence.  The calls are graph-capturable (the side stream joins
+ * opt-in phase timer (lvae_prof_*) and (2) the blocked inverses' side stream (lvae_spd_inv_chol_f32,
+ * lvae_kl_closed_*, lvae_spd_sweep_f32): ONE high-priority stream + seven events (fork, prep, c, and
+ * two pairs alternating by pass parity) per device, shared by every caller stream, created on first
+ * use, kept for the process lifetime, and guarded by a mutex held for each call's whole enqueue
+ * sequence (calls from different caller streams serialise on it).  The calls are graph-capturable (the side stream joins
  * the capture through the fork event and is joined back before the call returns).  Return value: 0 = ok, <0 = -(index of the bad argument),
  * LVAE_ERR_LAUNCH on a HIP launch error.  Numerical failure (a non-positive-definite pivot) is
  * NOT a return code (the call is asynchronous): it is written to the device `info` array,
@@ -99,10 +100,10 @@ int lvae_gram_bwd_f64(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x2
 /* ---------------------------------------------------------------------------------------- */
 /* Regime B: exact KL over the full N x N covariance (elbo_functions.py:8-34), batched over L */
 /* latent dims.  Arithmetic: fp32 storage; every GEMM on the f16 matrix cores with the       */
-/* 3-product hi / lo split (fp32-equivalent, ~2^-22 of max|operand| per product; per-(dim,   */
-/* pass) power-of-two split scales from measured operand bounds, so any K scale / noise level */
-/* that fp32 itself can represent is safe).  Covariance padded to Np =                        */
-/* lvae_kl_closed_padded_n(n) (identity on the padding).                                     */
+/* 3-product hi / lo split (fp32-equivalent, ~2^-22 of max|operand| per product; power-of-two */
+/* split scales per 256 x 256 block from each block's exact max, so any K scale / noise level */
+/* that fp32 itself can represent is safe); K^-1 mu refined once in fp64.  Covariance padded  */
+/* to Np = lvae_kl_closed_padded_n(n) (identity on the padding).                              */
 /* ---------------------------------------------------------------------------------------- */
 int lvae_kl_closed_padded_n(int n);
 /* bytes of device workspace the fwd+bwd pair needs (kept between the two calls) */
@@ -152,13 +153,14 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
                                  void* workspace, void* stream);
 
 /* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
- * 256-wide pivot blocks -- the default Regime B inverse of lvae_kl_closed_fwd_f32: per pivot block k,
+ * 256-wide pivot blocks (the r1-r2 Regime B inverse; lvae_kl_closed_* now use lvae_spd_inv_chol_f32's
+ * blocked Cholesky, which is ~100x more accurate at cond 1e5; kept as a C-ABI entry): per pivot block k,
  * A_kk <- -P^-1, A_ik <- A_ik P^-1, A_ij <- A_ij - A_ik P^-1 A_kj (P = A_kk); after the last block
  * A = -K^-1.  np % 256 == 0.  A [L, np, np] (lower 256-block tiles read, overwritten);
  * scratch: lvae_spd_sweep_scratch_size(np, L) bytes, 256-B aligned; Ainv [L, np, np] full
  * symmetric out; logdet [L]; info [L] LAPACK-style (first bad column + 1).  Pivot blocks are
  * inverted by a blocked Cholesky in LDS (fp32 MFMA); with lookahead, the next pivot and its
- * prep run on a second (internal, per caller stream) stream beside each interior update and are
+ * prep run on the internal side stream beside each interior update and are
  * joined back to `stream`.
  * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
 size_t lvae_spd_sweep_scratch_size(int np_, int L);

@@ -19,6 +19,6 @@ for c in "${P[@]}"; do
     python3 $ROOT/bench.py --regime closed ${PMC_ARGS} --steps 2 --warmup 1 --no-cpu-baseline --no-phase-timing --no-c2 \
     > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pass $i failed"; tail -5 $OUT/p$i.err; exit 1; }
 done
-PMC_STEPS=3 PMC_KERNELS=${PMC_KERNELS:-"syrk_x3,ci_,kl_,gram_"} python3 $ROOT/scripts/pmc_summary.py $OUT > $OUT/pmc_summary.txt
+PMC_STEPS=3 PMC_KERNELS=${PMC_KERNELS:-"syrk,ci_,kl_,gram_"} python3 $ROOT/scripts/pmc_summary.py $OUT > $OUT/pmc_summary.txt
 cat $OUT/pmc_summary.txt | head -150
 for d in $OUT/p*/; do rm -rf "$d"; done
