@@ -244,7 +244,13 @@ def run_closed(args, world, rank, dev):
     vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(dev)
     kernel = la.generate_kernel(**CFG, latent_dim=L).to(dev)
     lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(dev)
-    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3, fused=True)
+    # --graph (one GPU): the whole step (forward, backward, Adam) captured once and replayed as ONE HIP
+    # graph (steps.GraphedStep).  Measured slower than eager (15.4-15.7 vs 12.8 ms at L = 16, 8.9-9.0 vs
+    # 5.2 ms at L = 2, scripts/graph_ab.sh): the replay does not keep the side stream's pivot chain and the
+    # ConvVAE stream running beside the caller's stream, so the default stays eager.
+    use_graph = world == 1 and args.graph
+    opt = torch.optim.Adam([{"params": kernel.parameters()}, {"params": vae.parameters()}], lr=1e-3, fused=True,
+                           capturable=use_graph)
     img, mask, X = health_mnist_batch(P, T, seed=100, device=dev)   # the same data set on every rank
     gen = torch.Generator(device=dev).manual_seed(7)
     eps = torch.randn(N, L, device=dev, generator=gen)
@@ -259,21 +265,38 @@ def run_closed(args, world, rank, dev):
         inputs = (img, mask, X, eps)
         d0, d1 = 0, L
 
-    for _ in range(args.warmup):
-        out = step(*inputs)
+    if use_graph:
+        from lvae_amd.steps import GraphedStep
+        graph = GraphedStep(step, inputs, warmup=max(args.warmup, 1))  # warm-up steps, then the capture
+        run = graph
+    else:
+        def run():
+            return step(*inputs)
+        for _ in range(args.warmup):
+            run()
     torch.cuda.synchronize()
     la.check_pending()
-    if not args.no_phase_timing:
+    if not args.no_phase_timing and not use_graph:
         _lib.prof_enable(True)
         _lib.prof_collect()
     sync_barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step(*inputs)
+        out = run()
     sync_barrier(world)
     elapsed = time.perf_counter() - t0
+    if use_graph:
+        graph.check()
     phase = {}
     if not args.no_phase_timing:
+        if use_graph:
+            # the phase (and roofline kernel) times come from the same number of eager steps right after
+            # the graph-timed region: the library's HIP events bracket its own launches on their streams
+            _lib.prof_enable(True)
+            _lib.prof_collect()
+            for _ in range(args.steps):
+                step(*inputs)
+            torch.cuda.synchronize()
         phase = _lib.prof_collect()
         _lib.prof_enable(False)
     la.check_pending()
@@ -290,7 +313,8 @@ def run_closed(args, world, rank, dev):
            "config": {"workload": f"closed-form KL step (standard_training, type_KL='closed'): N={N} (P={P} subjects "
                                   f"x T={T}), L={L}, R=5 additive components (config/LVAE_config_sample.txt)",
                       "N": N, "L": L,
-                      "parallelism": ("single GPU" if world == 1 else
+                      "parallelism": (("single GPU, the step replayed as one HIP graph" if use_graph else "single GPU")
+                                      if world == 1 else
                                       f"latent dims sharded over {world} ranks ({Lr} dims/rank on rank 0), images "
                                       f"split {N // world}/rank, 1 all-gather + 2 all-reduces per step")}}
     if phase and Lr > 0:
@@ -303,6 +327,9 @@ def run_closed(args, world, rank, dev):
                                            f"Cholesky factorisation phase (potrf: {potrf_ms:.2f} ms/step on rank 0; the "
                                            f"triangular inverse + product, trtri + lauum, take {potri_ms:.2f} ms more)")
         res["phase_ms_per_step"] = {k: v[0] / args.steps for k, v in phase.items() if v[1]}
+        if use_graph:
+            res["phase_timing"] = (f"HIP events around the library's launches over {args.steps} eager steps run "
+                                   f"right after the graph-timed region (the same kernels, host-enqueued)")
         # dominant kernel by GPU time: the S GEMM S = K^-1 V K^-1 (one launch per step), L np^2 (np + 1)
         # fp32-equivalent flop (lower 256-tiles incl. the diagonal ones, whole), each a 3-product f16 split:
         # 3 x that in f16 MFMA flop against the dense f16 peak
@@ -508,6 +535,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-timing", action="store_true")
     ap.add_argument("--no-c2", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="closed regime on one GPU: time the step as one replayed HIP graph (slower, see run_closed)")
     ap.add_argument("--vae-stream-priority", dest="vae_stream_priority", type=int, default=-1,
                     help="priority of the ConvVAE's stream in the closed step (lower = higher; 0 = default)")
     args = ap.parse_args()
