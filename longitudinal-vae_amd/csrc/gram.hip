@@ -169,13 +169,35 @@ __device__ inline void tri_index(int t, int& I, int& J) {
 // [row][dim] image puts those 16 reads on one bank pair: 16-way conflicts).
 constexpr int kMaxQB = 16;  // covariate columns the Regime B kernels stage (spec dims < 16)
 __device__ inline int cov_slot(int r) { return (r & 3) * 16 + (r >> 2); }
+template <typename CT>
 __device__ inline void stage_cov(const double* __restrict__ x, int ldx, int n, int qs, int i0, int j0,
-                                 double* __restrict__ sx1, double* __restrict__ sx2) {
+                                 CT* __restrict__ sx1, CT* __restrict__ sx2) {
   for (int e = threadIdx.x; e < kGT * qs; e += 256) {
     const int r = e / qs, q = e % qs;
-    sx1[q * kGT + cov_slot(r)] = (i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0;
-    sx2[q * kGT + cov_slot(r)] = (j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
+    sx1[q * kGT + cov_slot(r)] = CT((i0 + r < n) ? x[(int64_t)(i0 + r) * ldx + q] : 0.0);
+    sx2[q * kGT + cov_slot(r)] = CT((j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0);
   }
+}
+
+// Integer-coded covariates (the common case: subject / time / class indices) take an fp32 path in the
+// Regime B Gram kernels: covariates staged as fp32, category / binary tests and differences in fp32 --
+// exact, and bitwise the same Gram, when every covariate is an integer of magnitude < 2^22 (the
+// fp64 path rounds the exact fp64 difference to fp32 as well).  flag = 1 iff the first qs columns of x
+// qualify; one workgroup, written by the factor for its kernels.
+__global__ __launch_bounds__(1024) void cov_int_check_kernel(const double* __restrict__ x, int ldx, int n, int qs,
+                                                             int* __restrict__ flag) {
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  int b = 0;
+  for (int r = threadIdx.x; r < n; r += 1024)
+    for (int q = 0; q < qs; ++q) {
+      const double v = x[(int64_t)r * ldx + q];
+      b |= !(v == rint(v) && fabs(v) < 4194304.0);
+    }
+  if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(&bad, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = bad ? 0 : 1;
 }
 
 // sin(pi t) for t = |d| / p >= 0: reduced to pi r, r = t - rint(t) in [-1/2, 1/2] in fp64 (the
@@ -185,9 +207,10 @@ __device__ inline float per_sin(double t) { return __sinf(float(M_PI) * float(t 
 __device__ inline float per_sin2(double t) { return __sinf(2.f * float(M_PI) * float(t - rint(t))); }
 
 // factor (kind, dim d, params pf) on the thread's 4 x 4 micro-tile: v[a][c] *= phi(x_i, x_j)
-__device__ inline void apply_factor(int kind, int d, const float* __restrict__ pf, const double* __restrict__ sx1,
-                                    const double* __restrict__ sx2, int tr, int tc, float (&v)[4][4]) {
-  double xr[4], xc[4];
+template <typename CT>
+__device__ inline void apply_factor(int kind, int d, const float* __restrict__ pf, const CT* __restrict__ sx1,
+                                    const CT* __restrict__ sx2, int tr, int tc, float (&v)[4][4]) {
+  CT xr[4], xc[4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
 #pragma unroll
@@ -201,7 +224,7 @@ __device__ inline void apply_factor(int kind, int d, const float* __restrict__ p
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] + xc[c] == 2.0) ? v[a][c] : 0.f;
+      for (int c = 0; c < 4; ++c) v[a][c] = (xr[a] + xc[c] == CT(2)) ? v[a][c] : 0.f;
   } else if (kind == LVAE_RBF) {
     const float ell = pf[0], cf = -0.5f * kLog2e / (ell * ell);
 #pragma unroll
@@ -218,23 +241,57 @@ __device__ inline void apply_factor(int kind, int d, const float* __restrict__ p
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float sn = per_sin(fabs(xr[a] - xc[c]) * ip);
+        const float sn = per_sin(fabs(double(xr[a]) - double(xc[c])) * ip);
         v[a][c] *= __builtin_amdgcn_exp2f(cf * sn * sn);
       }
   } else {  // LVAE_LIN
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[a][c] *= float(xr[a] * xc[c]);
+      for (int c = 0; c < 4; ++c) v[a][c] *= float(double(xr[a]) * double(xc[c]));
   }
+}
+
+// component r's factors on the micro-tile, Cat / Bin gates first: when they leave the whole WAVE at zero
+// (e.g. Cat(subject) on a tile pair of different subjects) the parametrised factors (exp / sin) are
+// skipped and false returned (v is then 0: the component adds nothing; wave-uniform, no divergence)
+template <typename CT>
+__device__ inline bool apply_factors_gated(const DevSpec& s, int r, const float* __restrict__ sp,
+                                           const CT* __restrict__ sx1, const CT* __restrict__ sx2, int tr,
+                                           int tc, float (&v)[4][4]) {
+  bool gated = false;
+#pragma unroll 1
+  for (int f = 0; f < s.n_fac[r]; ++f) {
+    const int kind = s.kind[r][f];
+    if (kind != LVAE_CAT && kind != LVAE_BIN) continue;
+    apply_factor(kind, s.dim[r][f], sp, sx1, sx2, tr, tc, v);
+    gated = true;
+  }
+  if (gated) {
+    bool any = false;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) any |= v[a][c] != 0.f;
+    if (!__any(any)) return false;
+  }
+#pragma unroll 1
+  for (int f = 0; f < s.n_fac[r]; ++f) {
+    const int kind = s.kind[r][f];
+    if (kind == LVAE_CAT || kind == LVAE_BIN) continue;
+    const int pi = s.param_idx[r][f];
+    apply_factor(kind, s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
+  }
+  return true;
 }
 
 // the adjoint's per-factor sums over the micro-tile: u0 = sum v d^2 (RBF) or sum v sin^2 u (PER),
 // u1 = sum v |d| sin 2u (PER); the ingredients are recomputed so only v stays live
-__device__ inline void factor_sums(int kind, int d, const float* __restrict__ pf, const double* __restrict__ sx1,
-                                   const double* __restrict__ sx2, int tr, int tc, const float (&v)[4][4], float& u0,
+template <typename CT>
+__device__ inline void factor_sums(int kind, int d, const float* __restrict__ pf, const CT* __restrict__ sx1,
+                                   const CT* __restrict__ sx2, int tr, int tc, const float (&v)[4][4], float& u0,
                                    float& u1) {
-  double xr[4], xc[4];
+  CT xr[4], xc[4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
 #pragma unroll
@@ -254,7 +311,7 @@ __device__ inline void factor_sums(int kind, int d, const float* __restrict__ pf
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const double ad = fabs(xr[a] - xc[c]), t = ad * ip;
+        const double ad = fabs(double(xr[a]) - double(xc[c])), t = ad * ip;
         const float sn = per_sin(t);
         u0 += v[a][c] * sn * sn;
         u1 += v[a][c] * float(ad) * per_sin2(t);
@@ -276,13 +333,14 @@ struct CovPrefetch {
       b[u] = (ok && j0 + r < n) ? x[(int64_t)(j0 + r) * ldx + q] : 0.0;
     }
   }
-  __device__ inline void store(int qs, double* __restrict__ sx1, double* __restrict__ sx2) const {
+  template <typename CT>
+  __device__ inline void store(int qs, CT* __restrict__ sx1, CT* __restrict__ sx2) const {
 #pragma unroll
     for (int u = 0; u < kPre; ++u) {
       const int e = threadIdx.x + 256 * u, r = e / qs, q = e % qs;
       if (e < kGT * qs) {
-        sx1[q * kGT + cov_slot(r)] = a[u];
-        sx2[q * kGT + cov_slot(r)] = b[u];
+        sx1[q * kGT + cov_slot(r)] = CT(a[u]);
+        sx2[q * kGT + cov_slot(r)] = CT(b[u]);
       }
     }
   }
@@ -292,14 +350,18 @@ struct CovPrefetch {
 // the padding rows / cols (keeps log|K| and the leading block of K^-1).  Grid (G, L): workgroup g
 // of dim l fills the tiles t = g, g + G, ... (t -> (I, J), I >= J), prefetching the next tile's
 // covariates under the current tile's arithmetic.  HBM-write-bound: 4 B per element.
-template <int MC, int MF>
+// CT: the covariates' type in LDS; both instantiations are launched and the one that does not match the
+// factor's covariate flag (cov_int_check_kernel: float for integer covariates) exits at once.
+template <int MC, int MF, typename CT>
 __global__ __launch_bounds__(256) void gram_sq_fill_kernel(DevSpec s, const double* __restrict__ x, int ldx,
                                                            int n, int np_, int qs,
                                                            const double* __restrict__ params,
                                                            const double* __restrict__ noise,
-                                                           float* __restrict__ K, int ntiles) {
-  __shared__ double sx1[kGT * kMaxQB];
-  __shared__ double sx2[kGT * kMaxQB];
+                                                           float* __restrict__ K, int ntiles,
+                                                           const int* __restrict__ covflag) {
+  if ((*covflag != 0) != (sizeof(CT) == 4)) return;  // (uniform, before any barrier)
+  __shared__ CT sx1[kGT * kMaxQB];
+  __shared__ CT sx2[kGT * kMaxQB];
   __shared__ float sp[64];
   const int G = gridDim.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
   if (tid < s.n_params) sp[tid] = float(params[(int64_t)l * s.n_params + tid]);
@@ -329,11 +391,7 @@ __global__ __launch_bounds__(256) void gram_sq_fill_kernel(DevSpec s, const doub
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[a][c] = sc;
-#pragma unroll 1
-      for (int f = 0; f < s.n_fac[r]; ++f) {
-        const int pi = s.param_idx[r][f];
-        apply_factor(s.kind[r][f], s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
-      }
+      if (!apply_factors_gated(s, r, sp, sx1, sx2, tr, tc, v)) continue;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -377,16 +435,18 @@ __global__ __launch_bounds__(256) void gram_sq_fill_kernel(DevSpec s, const doub
 constexpr int kNoiseSlot = 64;
 constexpr int kBwdSlots = 65;
 
-template <int MC, int MF>
+template <int MC, int MF, typename CT>
 __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double* __restrict__ x, int ldx, int n,
                                                          int np_, int qs, const double* __restrict__ params,
                                                          const float* __restrict__ Kinv,
                                                          const float* __restrict__ S,
                                                          const float* __restrict__ Sx, int nsplit,
                                                          const double* __restrict__ alpha,
-                                                         double* __restrict__ part, int ntiles) {
-  __shared__ double sx1[kGT * kMaxQB];
-  __shared__ double sx2[kGT * kMaxQB];
+                                                         double* __restrict__ part, int ntiles,
+                                                         const int* __restrict__ covflag) {
+  if ((*covflag != 0) != (sizeof(CT) == 4)) return;  // (uniform, before any barrier)
+  __shared__ CT sx1[kGT * kMaxQB];
+  __shared__ CT sx2[kGT * kMaxQB];
   __shared__ float sp[64];
   __shared__ float sa1[kGT], sa2[kGT];
   __shared__ double wred[4][kBwdSlots];
@@ -450,11 +510,7 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[a][c] = g[a][c];
-#pragma unroll 1
-      for (int f = 0; f < s.n_fac[r]; ++f) {
-        const int pi = s.param_idx[r][f];
-        apply_factor(s.kind[r][f], s.dim[r][f], sp + (pi < 0 ? 0 : pi), sx1, sx2, tr, tc, v);
-      }
+      if (!apply_factors_gated(s, r, sp, sx1, sx2, tr, tc, v)) continue;  // (every sum below is 0)
       // v = g prod_r: the scale's slot; g k_r = sc v for the parametrised factors
       float ssum = 0.f;
 #pragma unroll
@@ -766,7 +822,7 @@ static int gram_launch(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x
 }
 
 int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
-                 const double* params, const double* noise, float* K, hipStream_t st) {
+                 const double* params, const double* noise, float* K, int* covflag, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
   if (!bucket || qs > kMaxQB || qs > ldx) return -1;
@@ -775,10 +831,14 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   int G = (2048 + L - 1) / L;  // ~8 resident workgroups per CU, 2 rounds
   G = G < ntiles ? G : ntiles;
   dim3 grid(G, L);
-  if (bucket == 1)
-    gram_sq_fill_kernel<8, 2><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles);
-  else
-    gram_sq_fill_kernel<16, 4><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles);
+  cov_int_check_kernel<<<1, 1024, 0, st>>>(x, ldx, n, qs, covflag);
+  if (bucket == 1) {
+    gram_sq_fill_kernel<8, 2, float><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
+    gram_sq_fill_kernel<8, 2, double><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
+  } else {
+    gram_sq_fill_kernel<16, 4, float><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
+    gram_sq_fill_kernel<16, 4, double><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
+  }
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -819,7 +879,7 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L) {
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
                 const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
-                hipStream_t st) {
+                const int* covflag, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
   if (!bucket || qs > kMaxQB || spec->n_params > 64) return -1;
@@ -837,12 +897,17 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
     }
   const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2, G = kl_gram_bwd_groups(np_, L);
   const size_t dyn = (size_t)(spec->n_params + 1) * 256 * sizeof(float);
-  if (bucket == 1)
-    kl_gram_bwd_tiles<8, 2><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
-                                                           alpha, part, ntiles);
-  else
-    kl_gram_bwd_tiles<16, 4><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
-                                                            alpha, part, ntiles);
+  if (bucket == 1) {
+    kl_gram_bwd_tiles<8, 2, float><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                                  alpha, part, ntiles, covflag);
+    kl_gram_bwd_tiles<8, 2, double><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                                   alpha, part, ntiles, covflag);
+  } else {
+    kl_gram_bwd_tiles<16, 4, float><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx,
+                                                                   nsplit, alpha, part, ntiles, covflag);
+    kl_gram_bwd_tiles<16, 4, double><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx,
+                                                                    nsplit, alpha, part, ntiles, covflag);
+  }
   kl_gram_bwd_reduce<<<dim3(spec->n_params + 1, L), 256, 0, st>>>(pinfo, spec->n_params, part, G, params, gkl,
                                                                   dparams, dnoise);
   LVAE_CHECK_LAUNCH();

@@ -26,12 +26,12 @@
 namespace lvae {
 
 int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
-                 const double* params, const double* noise, float* K, hipStream_t st);
+                 const double* params, const double* noise, float* K, int* covflag, hipStream_t st);
 size_t kl_gram_bwd_partials_bytes(int np_, int L);
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
                 const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
-                hipStream_t st);
+                const int* covflag, hipStream_t st);
 int syrk_x3_splits(int np_, int L);
 int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
 int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
@@ -53,6 +53,7 @@ struct KLWorkspace {
   float* apart;      // [L, nt, np] the partials of K^-1 mu (lauum epilogue)
   char* chol;        // ci_factor_f32 scratch
   double *mu, *alpha, *res, *kdiag, *logdet, *part, *rpart;
+  int* covflag;      // 1: integer covariates (the Gram kernels' fp32 covariate path; set by the factor)
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
     size_t off = 0;
@@ -78,6 +79,7 @@ struct KLWorkspace {
     chol = take(ci_scratch_bytes(np_, L));
     part = (double*)take(kl_gram_bwd_partials_bytes(np_, L));
     rpart = (double*)take(kl_resid_partials_bytes(np_, L));
+    covflag = (int*)take(sizeof(int));
     Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
     bytes = off;
   }
@@ -189,7 +191,7 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
   KLWorkspace ws((char*)workspace, np_, L);
   {
     ProfScope ps(LVAE_PH_GRAM, st);
-    LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, st));
+    LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, ws.covflag, st));
   }
   // Y = L^-1 and log|K|: blocked Cholesky + trtri (chol_inv.hip; phases POTRF / POTRI inside); lauum
   // runs in the reduce
@@ -262,7 +264,7 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);
     LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, S, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
-                         gkl, ws.part, dparams, dnoise, st));
+                         gkl, ws.part, dparams, dnoise, ws.covflag, st));
   }
   LVAE_CHECK_LAUNCH();
   return 0;
