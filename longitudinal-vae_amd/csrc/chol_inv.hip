@@ -947,7 +947,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
   auto ok = [](hipError_t e) { return e == hipSuccess; };
   {
     ProfScope ps(LVAE_PH_POTRF, st);
-    std::lock_guard<std::mutex> lock(side_mutex());
+    std::lock_guard<std::recursive_mutex> lock(side_mutex());
     SideStream* sd = nullptr;
     LVAE_TRY(side_stream(sd));
     (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);

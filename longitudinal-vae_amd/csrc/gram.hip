@@ -626,7 +626,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
                                                       int qs, const double* __restrict__ params,
                                                       const double* __restrict__ noise,
                                                       const double* __restrict__ alpha, double* __restrict__ part,
-                                                      int ntiles) {
+                                                      int ntiles, const int* __restrict__ skip) {
+  if (skip && *skip) return;  // the binned path (kl_resid_bins.hip) took this call
   __shared__ double sx1[kGT * kMaxQB];
   __shared__ double sx2[kGT * kMaxQB];
   __shared__ double sp[64];
@@ -743,9 +744,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
 // r[l][i] = mu[l][i] - sum_s part[l][s][i] (fixed order), 0 on the padding.  Grid (np / 256, L).
 __global__ __launch_bounds__(256) void kl_resid_reduce(const double* __restrict__ part, const double* __restrict__ muc,
-                                                       int n, int np_, double* __restrict__ res) {
+                                                       int n, int np_, double* __restrict__ res,
+                                                       const int* __restrict__ skip) {
   const int i = blockIdx.x * 256 + threadIdx.x, l = blockIdx.y, nt = np_ / kGT;
-  if (i >= np_) return;
+  if (i >= np_ || (skip && *skip)) return;
   double acc = 0.0;
   for (int s = 0; s < nt; ++s) acc += part[((int64_t)l * nt + s) * np_ + i];
   res[(int64_t)l * np_ + i] = i < n ? muc[(int64_t)l * np_ + i] - acc : 0.0;
@@ -843,23 +845,34 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   return 0;
 }
 
+int kl_resid_bins(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                  const double* params, const double* noise, const double* alpha0, const double* muc, double* res,
+                  void* wsbuf, int** okflag, hipStream_t st);
+
 size_t kl_resid_partials_bytes(int np_, int L) { return (size_t)L * (np_ / kGT) * np_ * sizeof(double); }
 
 int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                   const double* params, const double* noise, const double* alpha0, const double* muc, double* part,
-                  double* res, hipStream_t st) {
+                  double* res, void* rbws, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
   if (!bucket || qs > kMaxQB || qs > ldx || spec->n_params > 64) return -1;
   const DevSpec ds = to_dev(spec);
   const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2;
-  int G = (2048 + L - 1) / L;
+  // ~8 resident workgroups per CU in 2 rounds; one round of 2 per CU behind the binned path (when it
+  // runs, these launches only read the flag and exit: fewer of them)
+  int G = ((rbws ? 512 : 2048) + L - 1) / L;
   G = G < ntiles ? G : ntiles;
+  // rbws (the binned residual's planned workspace, kl_resid_bins_plan): integer-coded covariates take
+  // the binned O(N W) residual and the tiled kernels below exit at once (checked on the device: *skip)
+  int* skip = nullptr;
+  if (rbws)
+    LVAE_TRY(kl_resid_bins(spec, x, ldx, n, np_, L, params, noise, alpha0, muc, res, rbws, &skip, st));
   if (bucket == 1)
-    kl_resid_tiles<8, 2><<<dim3(G, L), 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, alpha0, part, ntiles);
+    kl_resid_tiles<8, 2><<<dim3(G, L), 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, alpha0, part, ntiles, skip);
   else
-    kl_resid_tiles<16, 4><<<dim3(G, L), 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, alpha0, part, ntiles);
-  kl_resid_reduce<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(part, muc, n, np_, res);
+    kl_resid_tiles<16, 4><<<dim3(G, L), 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, alpha0, part, ntiles, skip);
+  kl_resid_reduce<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(part, muc, n, np_, res, skip);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

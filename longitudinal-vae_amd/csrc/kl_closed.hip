@@ -20,6 +20,7 @@
 //   dmu = g a,  dlogv = g/2 (v d - 1)
 // One reduce per factor: the backward's S overwrites the Y^T planes.
 #include "common.hpp"
+#include "side_stream.hpp"
 #include "prof.hpp"
 
 
@@ -42,7 +43,11 @@ size_t ci_scratch_bytes(int np_, int L);
 size_t kl_resid_partials_bytes(int np_, int L);
 int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                   const double* params, const double* noise, const double* alpha0, const double* muc, double* part,
-                  double* res, hipStream_t st);
+                  double* res, void* rbws, hipStream_t st);
+size_t kl_resid_bins_bytes(int np_, int L, int ncomp);
+bool kl_resid_bins_enabled(const lvae_kernel_spec* spec, int n);
+int kl_resid_bins_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, void* wsbuf,
+                       hipStream_t st);
 
 struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
@@ -54,6 +59,7 @@ struct KLWorkspace {
   char* chol;        // ci_factor_f32 scratch
   double *mu, *alpha, *res, *kdiag, *logdet, *part, *rpart;
   int* covflag;      // 1: integer covariates (the Gram kernels' fp32 covariate path; set by the factor)
+  char* rb;          // the binned residual's plan / bin sums (kl_resid_bins.hip)
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
     size_t off = 0;
@@ -80,6 +86,7 @@ struct KLWorkspace {
     part = (double*)take(kl_gram_bwd_partials_bytes(np_, L));
     rpart = (double*)take(kl_resid_partials_bytes(np_, L));
     covflag = (int*)take(sizeof(int));
+    rb = take(kl_resid_bins_bytes(np_, L, LVAE_MAX_COMP));
     Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
     bytes = off;
   }
@@ -189,6 +196,17 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
+  // the binned residual's plan (x only) goes on the side stream behind the Cholesky's pivot chain, beside
+  // the trailing updates / trtri; the reduce waits for it (event rb)
+  const bool rb_on = kl_resid_bins_enabled(spec, n);
+  std::unique_lock<std::recursive_mutex> lock(side_mutex(), std::defer_lock);
+  SideStream* sd = nullptr;
+  auto ok = [](hipError_t e) { return e == hipSuccess; };
+  if (rb_on) {
+    lock.lock();
+    LVAE_TRY(side_stream(sd));
+    if (!ok(hipEventRecord(sd->rbx, st))) return LVAE_ERR_LAUNCH;
+  }
   {
     ProfScope ps(LVAE_PH_GRAM, st);
     LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, ws.covflag, st));
@@ -196,6 +214,11 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
   // Y = L^-1 and log|K|: blocked Cholesky + trtri (chol_inv.hip; phases POTRF / POTRI inside); lauum
   // runs in the reduce
   LVAE_TRY(ci_factor_f32(np_, L, ws.A, ws.chol, ws.planes, ws.Kinv, ws.logdet, info, st));
+  if (rb_on) {
+    if (!ok(hipStreamWaitEvent(sd->s, sd->rbx, 0))) return LVAE_ERR_LAUNCH;
+    LVAE_TRY(kl_resid_bins_plan(spec, x, ldx, n, np_, L, ws.rb, sd->s));
+    if (!ok(hipEventRecord(sd->rb, sd->s))) return LVAE_ERR_LAUNCH;
+  }
   LVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -222,7 +245,15 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
   LVAE_TRY(ci_lauum_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.mu, ws.sv, ws.apart, need_bwd ? ws.Bp : nullptr,
                         ws.bsc, st));
   kl_alpha0_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.apart, ws.Kinv, np_, ws.alpha, ws.kdiag);
-  LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res, st));
+  const bool rb_on = kl_resid_bins_enabled(spec, n);
+  if (rb_on) {  // the plan enqueued by the factor call
+    std::lock_guard<std::recursive_mutex> lock(side_mutex());
+    SideStream* sd = nullptr;
+    LVAE_TRY(side_stream(sd));
+    if (hipStreamWaitEvent(st, sd->rb, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
+  }
+  LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res,
+                         rb_on ? ws.rb : nullptr, st));
   kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.alpha, ws.alpha);
   kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   LVAE_CHECK_LAUNCH();

@@ -10,8 +10,8 @@ constexpr int kMaxDev = 64;
 SideStream g_side[kMaxDev];
 }  // namespace
 
-std::mutex& side_mutex() {
-  static std::mutex mu;
+std::recursive_mutex& side_mutex() {
+  static std::recursive_mutex mu;
   return mu;
 }
 
@@ -23,7 +23,7 @@ int side_stream(SideStream*& out) {
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (hipStreamCreateWithPriority(&sd.s, hipStreamNonBlocking, greatest) != hipSuccess) return LVAE_ERR_LAUNCH;
-    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.c, &sd.u2p[0], &sd.u2p[1], &sd.piv[0], &sd.piv[1]})
+    for (hipEvent_t* e : {&sd.fork, &sd.prep, &sd.c, &sd.u2p[0], &sd.u2p[1], &sd.piv[0], &sd.piv[1], &sd.rbx, &sd.rb})
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return LVAE_ERR_LAUNCH;
   }
   out = &sd;

@@ -871,7 +871,7 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
                   hipStream_t st) {
   if (np_ <= 0 || np_ % kSwB) return -1;
   if (L <= 0) return -2;
-  std::lock_guard<std::mutex> lock(side_mutex());
+  std::lock_guard<std::recursive_mutex> lock(side_mutex());
   SideStream* sd = nullptr;
   LVAE_TRY(side_stream(sd));
   SwScratch S((char*)scratch, np_, L);

@@ -624,6 +624,58 @@ def test_kl_closed_periodic_linear(hip, P, L, dev):
         assert rel(torch.stack([p.grad[l] for _, p in kd.named_parameters()]), r.grad) < 1e-4
 
 
+CFG_GATES = dict(cat_kernel=[2], bin_kernel=[4], sqexp_kernel=[0],
+                 cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 3}],
+                 bin_int_kernel=[{'cont_covariate': 1, 'bin_covariate': 4}],
+                 covariate_missing_val=[{'covariate': 1, 'mask': 5}])
+
+
+@pytest.mark.parametrize("case", ["integer", "half_time", "wide_window", "gates_masks", "c5"])
+def test_kl_closed_resid_paths(hip, case):
+    """The fp64 residual r = mu - K a0 behind the K^-1 mu refinement (elbo_functions.py:27-30) on both
+    of its paths: integer-coded covariates go through the binned O(N W) kernels (kl_resid_bins.hip:
+    "integer", Bin gates and a missing-value mask in "gates_masks", the periodic / linear C5 factors in
+    "c5"), the rest through the tiled O(N^2) kernel (times shifted by 0.5: "half_time"; a time window
+    of 76 > 64 values: "wide_window").  dmu = K^-1 mu is the refined quantity: within 1e-8 of the fp64
+    oracle (the refinement reaches ~1e-10 here; a residual that missed terms leaves the fp32-equivalent
+    inverse's ~1e-5), and the KL within 1e-6."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    P, T, L = 64, 16, 2
+    cfg = CFG_GATES if case == "gates_masks" else CFG
+    X = torch.tensor(health_mnist_covariates(P, T, seed=7))
+    if case == "half_time":
+        X[:, 0] += 0.5
+    elif case == "wide_window":
+        X[:, 0] *= 5.0
+    gen = torch.Generator().manual_seed(7)
+    mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    rng = np.random.default_rng(7)
+    if case == "c5":  # around its own init (the linear factor's scale 0.05 keeps cond(K) moderate)
+        k = _c5_kernel(L).double()
+        with torch.no_grad():
+            for _, p in k.named_parameters():
+                p.add_(torch.tensor(rng.uniform(-0.3, 0.3, L)))
+    else:
+        k = la.generate_kernel(**cfg, latent_dim=L).double()
+        set_raw(k, _random_hypers(k, L, rng))
+    raw = torch.stack([p.detach().clone() for _, p in k.named_parameters()], 1)
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    mu_d, lv_d = mu.to(DEV).requires_grad_(), lv.to(DEV).requires_grad_()
+    kl = la.KL_closed_batched(kd, X.to(DEV), lik, mu_d, lv_d)
+    kl.sum().backward()
+    spec = _c5_spec() if case == "c5" else O.spec_full(**cfg)
+    for l in range(L):
+        m_ = mu[:, l].clone().requires_grad_()
+        ref = O.kl_closed(spec, O.constrain(raw[l]), X, 1.0, m_, lv[:, l])
+        ref.backward()
+        e_kl, e_mu = rel(kl[l], ref), rel(mu_d.grad[:, l], m_.grad)
+        print(f"{case} dim {l}: kl {e_kl:.2e} dmu {e_mu:.2e}")
+        assert e_kl < 1e-6 and e_mu < 1e-8, (case, l, e_kl, e_mu)
+
+
 def test_closed_step_vs_oracle(hip):
     """One full standard_training step with type_KL='closed' (training.py:484-592): ConvVAE forward /
     backward over all N = 1024 images, the exact KL of L = 4 dims, the step composition
