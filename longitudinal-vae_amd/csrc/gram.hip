@@ -182,22 +182,50 @@ __device__ inline void stage_cov(const double* __restrict__ x, int ldx, int n, i
 // Integer-coded covariates (the common case: subject / time / class indices) take an fp32 path in the
 // Regime B Gram kernels: covariates staged as fp32, category / binary tests and differences in fp32 --
 // exact, and bitwise the same Gram, when every covariate is an integer of magnitude < 2^22 (the
-// fp64 path rounds the exact fp64 difference to fp32 as well).  flag = 1 iff the first qs columns of x
-// qualify; one workgroup, written by the factor for its kernels.
+// fp64 path rounds the exact fp64 difference to fp32 as well).  One workgroup, written by the factor for
+// its kernels: flag 0 = not integer-coded (fp64 covariates), 1 = integer-coded, 2 = integer-coded and
+// every dim of tabmask spans < kTabD values (the table path, gram_tab_*; tab_ok: the spec allows it).
+constexpr int kTabD = 64;
 __global__ __launch_bounds__(1024) void cov_int_check_kernel(const double* __restrict__ x, int ldx, int n, int qs,
-                                                             int* __restrict__ flag) {
-  __shared__ int bad;
-  if (threadIdx.x == 0) bad = 0;
+                                                             int tab_ok, int tabmask, int* __restrict__ flag) {
+  __shared__ int bad, wide;
+  __shared__ int lo[kMaxQB], hi[kMaxQB];
+  if (threadIdx.x == 0) bad = wide = 0;
+  if (threadIdx.x < kMaxQB) {
+    lo[threadIdx.x] = INT_MAX;
+    hi[threadIdx.x] = INT_MIN;
+  }
   __syncthreads();
   int b = 0;
-  for (int r = threadIdx.x; r < n; r += 1024)
-    for (int q = 0; q < qs; ++q) {
+  for (int q = 0; q < qs; ++q) {
+    int mn = INT_MAX, mx = INT_MIN;
+    for (int r = threadIdx.x; r < n; r += 1024) {
       const double v = x[(int64_t)r * ldx + q];
-      b |= !(v == rint(v) && fabs(v) < 4194304.0);
+      const bool ok = v == rint(v) && fabs(v) < 4194304.0;
+      b |= !ok;
+      if (ok) {
+        mn = min(mn, (int)v);
+        mx = max(mx, (int)v);
+      }
     }
+    if ((tabmask >> q) & 1) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, __shfl_xor(mn, o, 64));
+        mx = max(mx, __shfl_xor(mx, o, 64));
+      }
+      if ((threadIdx.x & 63) == 0) {
+        atomicMin(&lo[q], mn);
+        atomicMax(&hi[q], mx);
+      }
+    }
+  }
   if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(&bad, 1);
   __syncthreads();
-  if (threadIdx.x == 0) *flag = bad ? 0 : 1;
+  if (threadIdx.x < qs && ((tabmask >> threadIdx.x) & 1) && hi[threadIdx.x] - lo[threadIdx.x] >= kTabD)
+    atomicOr(&wide, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = bad ? 0 : (tab_ok && !wide ? 2 : 1);
 }
 
 // sin(pi t) for t = |d| / p >= 0: reduced to pi r, r = t - rint(t) in [-1/2, 1/2] in fp64 (the
@@ -346,6 +374,30 @@ struct CovPrefetch {
   }
 };
 
+// the same for integer-coded covariates (flag >= 1: exact in fp32), half the registers
+struct CovPrefetchF {
+  float a[kPre], b[kPre];
+  __device__ inline void load(const double* __restrict__ x, int ldx, int n, int qs, int i0, int j0) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int e = threadIdx.x + 256 * u, r = e / qs, q = e % qs;
+      const bool ok = e < kGT * qs;
+      a[u] = (ok && i0 + r < n) ? float(x[(int64_t)(i0 + r) * ldx + q]) : 0.f;
+      b[u] = (ok && j0 + r < n) ? float(x[(int64_t)(j0 + r) * ldx + q]) : 0.f;
+    }
+  }
+  __device__ inline void store(int qs, float* __restrict__ sx1, float* __restrict__ sx2) const {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int e = threadIdx.x + 256 * u, r = e / qs, q = e % qs;
+      if (e < kGT * qs) {
+        sx1[q * kGT + cov_slot(r)] = a[u];
+        sx2[q * kGT + cov_slot(r)] = b[u];
+      }
+    }
+  }
+};
+
 // Lower 64-tiles of the padded [np, np] covariance, f32 out, + noise on the diagonal, identity on
 // the padding rows / cols (keeps log|K| and the leading block of K^-1).  Grid (G, L): workgroup g
 // of dim l fills the tiles t = g, g + G, ... (t -> (I, J), I >= J), prefetching the next tile's
@@ -359,7 +411,7 @@ __global__ __launch_bounds__(256) void gram_sq_fill_kernel(DevSpec s, const doub
                                                            const double* __restrict__ noise,
                                                            float* __restrict__ K, int ntiles,
                                                            const int* __restrict__ covflag) {
-  if ((*covflag != 0) != (sizeof(CT) == 4)) return;  // (uniform, before any barrier)
+  if (*covflag != (sizeof(CT) == 4 ? 1 : 0)) return;  // (uniform, before any barrier)
   __shared__ CT sx1[kGT * kMaxQB];
   __shared__ CT sx2[kGT * kMaxQB];
   __shared__ float sp[64];
@@ -444,7 +496,7 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
                                                          const double* __restrict__ alpha,
                                                          double* __restrict__ part, int ntiles,
                                                          const int* __restrict__ covflag) {
-  if ((*covflag != 0) != (sizeof(CT) == 4)) return;  // (uniform, before any barrier)
+  if (*covflag != (sizeof(CT) == 4 ? 1 : 0)) return;  // (uniform, before any barrier)
   __shared__ CT sx1[kGT * kMaxQB];
   __shared__ CT sx2[kGT * kMaxQB];
   __shared__ float sp[64];
@@ -540,6 +592,431 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
         if (lane == 0) wred[wv][q] += (double)w;
         tacc(q) = 0.f;
       }
+    }
+  }
+  __syncthreads();
+  for (int sl = tid; sl < kBwdSlots; sl += 256)
+    part[((int64_t)l * kBwdSlots + sl) * G + g0] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
+}
+
+// ------------------------------------------------------------------------------------------
+// Table path of the Regime B Gram fill and adjoint (covariate flag 2: integer-coded covariates whose
+// continuous dims each span < kTabD values).  Every component is gates (Cat / Bin tests) times at most
+// one RBF / periodic factor of |x_i[d] - x_j[d]|, so with B distinct gates and the components grouped by
+// the dim of their continuous factor, an element of K is
+//   K_ij = sum_g T_g[bits_ij][|x_i[d_g] - x_j[d_g]|],   T_g[b][m] = sum_{r in g, gates_r in b} s_r phi_r(m)
+// (bits_ij: which of the B gates pass; components with no continuous factor join group 0 as
+// d-independent terms), and each raw adjoint sum is  sum_ij w g_ij D_p[bits_ij][|d_ij|]  with D_p the
+// same derivative factors as kl_gram_bwd_tiles'.  The tables (fp32, from the same fp32 formulas as the
+// direct path) are built per workgroup into LDS; per element the work drops to the B gate tests, one
+// difference + table read per group and, in the adjoint, one FMA per parameter.
+// ------------------------------------------------------------------------------------------
+#ifndef LVAE_TAB_WPE
+#define LVAE_TAB_WPE 3  // the table adjoint's waves per SIMD (register cap)
+#endif
+#ifndef LVAE_TAB_PIPE
+#define LVAE_TAB_PIPE 0  // 1: the table adjoint holds the next tile's K^-1 / S rows in registers
+#endif
+constexpr int kTabMaxG = 3, kTabMaxBits = 5;
+constexpr int kTabR = kTabD + 1;  // table row stride (odd: the rows of different gate bits on other banks)
+constexpr int kTabMaxFillLds = kTabMaxG * (1 << kTabMaxBits) * kTabR;  // floats
+constexpr int kTabMaxBwdLds = 256 * kTabR;                             // floats (n_params 2^B <= 256)
+struct GramTab {
+  int ng, nbits, n_params;
+  int gdim[kTabMaxG];                               // the group's continuous dim (-1: none at all)
+  int bkind[kTabMaxBits], bdim[kTabMaxBits];        // gate b: LVAE_CAT / LVAE_BIN on dim
+  int cgrp[LVAE_MAX_COMP], cmask[LVAE_MAX_COMP];    // component r: its group, the gate bits it needs
+  int ckind[LVAE_MAX_COMP], cpi[LVAE_MAX_COMP];     // its continuous factor (kind -1: none), param index
+  int csc[LVAE_MAX_COMP];                           // its scale's param index
+  int n_comp;
+  int porder[64];                                   // parameter slots ordered by group
+  int pbeg[kTabMaxG + 1];                           // porder[pbeg[g] .. pbeg[g + 1]) belong to group g
+  int pcomp[64], ptype[64];                         // slot p: its component, 0 scale / 1 RBF l / 2 PER l / 3 PER p
+};
+
+// host: the table description of spec, false if the spec does not fit it
+static bool gram_tab_build(const lvae_kernel_spec* s, GramTab& t) {
+  t = GramTab{};
+  t.n_comp = s->n_comp;
+  t.n_params = s->n_params;
+  if (s->n_params > 64 || s->n_comp < 1) return false;
+  for (int r = 0; r < s->n_comp; ++r) {
+    int nc = 0, mask = 0;
+    t.ckind[r] = -1;
+    t.cpi[r] = 0;
+    t.cgrp[r] = -1;
+    t.csc[r] = s->scale_idx[r];
+    for (int f = 0; f < s->n_fac[r]; ++f) {
+      const int k = s->kind[r][f], d = s->dim[r][f];
+      if (k == LVAE_CAT || k == LVAE_BIN) {
+        int b = 0;
+        while (b < t.nbits && !(t.bkind[b] == k && t.bdim[b] == d)) ++b;
+        if (b == t.nbits) {
+          if (t.nbits == kTabMaxBits) return false;
+          t.bkind[b] = k;
+          t.bdim[b] = d;
+          ++t.nbits;
+        }
+        mask |= 1 << b;
+      } else if (k == LVAE_RBF || k == LVAE_PER) {
+        if (++nc > 1) return false;
+        int g = 0;
+        while (g < t.ng && t.gdim[g] != d) ++g;
+        if (g == t.ng) {
+          if (t.ng == kTabMaxG) return false;
+          t.gdim[g] = d;
+          ++t.ng;
+        }
+        t.cgrp[r] = g;
+        t.ckind[r] = k;
+        t.cpi[r] = s->param_idx[r][f];
+      } else {
+        return false;  // linear factors: not a function of the distance
+      }
+    }
+    t.cmask[r] = mask;
+  }
+  if (t.ng == 0) {
+    t.ng = 1;
+    t.gdim[0] = -1;
+  }
+  for (int r = 0; r < s->n_comp; ++r)
+    if (t.cgrp[r] < 0) t.cgrp[r] = 0;
+  // parameter slots -> (component, type); ordered by group
+  for (int p = 0; p < 64; ++p) t.pcomp[p] = -1;
+  for (int r = 0; r < s->n_comp; ++r) {
+    t.pcomp[t.csc[r]] = r;
+    t.ptype[t.csc[r]] = 0;
+    if (t.ckind[r] == LVAE_RBF) {
+      t.pcomp[t.cpi[r]] = r;
+      t.ptype[t.cpi[r]] = 1;
+    } else if (t.ckind[r] == LVAE_PER) {
+      t.pcomp[t.cpi[r]] = r;
+      t.ptype[t.cpi[r]] = 2;
+      t.pcomp[t.cpi[r] + 1] = r;
+      t.ptype[t.cpi[r] + 1] = 3;
+    }
+  }
+  int k = 0;
+  for (int g = 0; g < t.ng; ++g) {
+    t.pbeg[g] = k;
+    for (int p = 0; p < s->n_params; ++p)
+      if (t.pcomp[p] >= 0 && t.cgrp[t.pcomp[p]] == g) t.porder[k++] = p;
+  }
+  t.pbeg[t.ng] = k;
+  if (t.ng * (1 << t.nbits) * kTabR > kTabMaxFillLds) return false;
+  if (k * (1 << t.nbits) * kTabR > kTabMaxBwdLds) return false;
+  return true;
+}
+
+// the continuous factor phi_r(m) of component r at integer distance m (1 without one), fp32 as the
+// direct path (apply_factor); and the parts of its parameter derivatives the raw sums carry
+__device__ inline float tab_phi(const GramTab& t, int r, const float* __restrict__ sp, int m) {
+  const int k = t.ckind[r];
+  if (k == LVAE_RBF) {
+    const float ell = sp[t.cpi[r]], cf = -0.5f * kLog2e / (ell * ell), df = float(m);
+    return __builtin_amdgcn_exp2f(cf * df * df);
+  }
+  if (k == LVAE_PER) {
+    const float ell = sp[t.cpi[r]], cf = -2.f * kLog2e / (ell * ell);
+    const float sn = per_sin((double)m / (double)sp[t.cpi[r] + 1]);
+    return __builtin_amdgcn_exp2f(cf * sn * sn);
+  }
+  return 1.f;
+}
+
+// fill tables: tab[(g * 2^B + b) * kTabR + m] = sum over the components r of group g whose gates are in b
+__device__ inline void tab_build_fill(const GramTab& t, const float* __restrict__ sp, float* __restrict__ tab) {
+  const int nb = 1 << t.nbits, ne = t.ng * nb * kTabR;
+  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+    const int m = e % kTabR, b = (e / kTabR) % nb, g = e / (kTabR * nb);
+    float v = 0.f;
+    for (int r = 0; r < t.n_comp; ++r)
+      if (t.cgrp[r] == g && (t.cmask[r] & ~b) == 0) v += sp[t.csc[r]] * tab_phi(t, r, sp, m);
+    tab[e] = v;
+  }
+}
+
+// adjoint tables: tab[(k * 2^B + b) * kTabR + m] for the k-th slot of porder: d k_r / d theta without
+// the constants kl_gram_bwd_reduce applies (scale: phi; RBF l: s phi m^2; PER l: s phi sin^2 u; PER p:
+// s phi m sin 2u), 0 when r's gates are not all in b
+__device__ inline void tab_build_bwd(const GramTab& t, const float* __restrict__ sp, float* __restrict__ tab) {
+  const int nb = 1 << t.nbits, np = t.pbeg[t.ng], ne = np * nb * kTabR;
+  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+    const int m = e % kTabR, b = (e / kTabR) % nb, k = e / (kTabR * nb);
+    const int p = t.porder[k], r = t.pcomp[p], ty = t.ptype[p];
+    float v = 0.f;
+    if ((t.cmask[r] & ~b) == 0) {
+      const float phi = tab_phi(t, r, sp, m), sc = sp[t.csc[r]];
+      if (ty == 0) v = phi;
+      else if (ty == 1) v = sc * phi * float(m) * float(m);
+      else {
+        const double u = (double)m / (double)sp[t.cpi[r] + 1];
+        if (ty == 2) {
+          const float sn = per_sin(u);
+          v = sc * phi * sn * sn;
+        } else {
+          v = sc * phi * float(m) * per_sin2(u);
+        }
+      }
+    }
+    tab[e] = v;
+  }
+}
+
+// the micro-tile's gate bits as table row offsets: bits[a][c] = (sum_b pass_b << b) * kTabR
+__device__ inline void tab_bits(const GramTab& t, const float* __restrict__ sx1, const float* __restrict__ sx2,
+                                int tr, int tc, int (&bits)[4][4]) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bits[a][c] = 0;
+#pragma unroll 1
+  for (int b = 0; b < t.nbits; ++b) {
+    const int d = t.bdim[b], bit = kTabR << b;
+    float xr[4], xc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xc[c] = sx2[d * kGT + c * 16 + tc];
+    if (t.bkind[b] == LVAE_CAT) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bits[a][c] += (xr[a] == xc[c]) ? bit : 0;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bits[a][c] += (xr[a] + xc[c] == 2.f) ? bit : 0;
+    }
+  }
+}
+
+// group g's table index per element: bits + |x_i[d_g] - x_j[d_g]| (< kTabD by the covariate flag)
+__device__ inline void tab_index(const GramTab& t, int g, const float* __restrict__ sx1,
+                                 const float* __restrict__ sx2, int tr, int tc, const int (&bits)[4][4],
+                                 int (&idx)[4][4]) {
+  const int d = t.gdim[g];
+  if (d < 0) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) idx[a][c] = bits[a][c];
+    return;
+  }
+  float xr[4], xc[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) xr[a] = sx1[d * kGT + a * 16 + tr];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xc[c] = sx2[d * kGT + c * 16 + tc];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) idx[a][c] = bits[a][c] + (int)fabsf(xr[a] - xc[c]);
+}
+
+// gram_sq_fill_kernel's table twin (flag 2)
+__global__ __launch_bounds__(256) void gram_sq_fill_tab_kernel(GramTab tb, const double* __restrict__ x, int ldx,
+                                                               int n, int np_, int qs,
+                                                               const double* __restrict__ params,
+                                                               const double* __restrict__ noise,
+                                                               float* __restrict__ K, int ntiles,
+                                                               const int* __restrict__ covflag) {
+  if (*covflag != 2) return;  // (uniform, before any barrier)
+  __shared__ float sx1[kGT * kMaxQB];
+  __shared__ float sx2[kGT * kMaxQB];
+  __shared__ float sp[64];
+  extern __shared__ float tab[];  // ng 2^B kTabR floats
+  const int G = gridDim.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  if (tid < tb.n_params) sp[tid] = float(params[(int64_t)l * tb.n_params + tid]);
+  const float nz = float(noise[l]);
+  float* o = K + (int64_t)l * np_ * np_;
+  int t = blockIdx.x, I, J;
+  if (t >= ntiles) return;
+  tri_index(t, I, J);
+  CovPrefetchF pf;
+  pf.load(x, ldx, n, qs, I * kGT, J * kGT);
+  pf.store(qs, sx1, sx2);
+  __syncthreads();
+  tab_build_fill(tb, sp, tab);
+  __syncthreads();
+  const int tstride = (1 << tb.nbits) * kTabR;
+  for (; t < ntiles; t += G) {
+    const int i0 = I * kGT, j0 = J * kGT;
+    int In = 0, Jn = 0;
+    const bool more = t + G < ntiles;
+    if (more) {
+      tri_index(t + G, In, Jn);
+      pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
+    }
+    int bits[4][4];
+    tab_bits(tb, sx1, sx2, tr, tc, bits);
+    float out[4][4] = {};
+#pragma unroll 1
+    for (int g = 0; g < tb.ng; ++g) {
+      int idx[4][4];
+      tab_index(tb, g, sx1, sx2, tr, tc, bits, idx);
+      const float* tg = tab + g * tstride;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) out[a][c] += tg[idx[a][c]];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int i = i0 + 4 * tr + a;
+      g_f32x4 w;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = j0 + 4 * tc + c;
+        float e = out[a][c];
+        if (i == j) e += nz;
+        if (i >= n || j >= n) e = (i == j) ? 1.0f : 0.0f;
+        w[c] = e;
+      }
+      *reinterpret_cast<g_f32x4*>(o + (int64_t)i * np_ + j0 + 4 * tc) = w;
+    }
+    if (more) {
+      __syncthreads();  // every reader of this tile's covariates is done
+      pf.store(qs, sx1, sx2);
+      __syncthreads();
+      I = In, J = Jn;
+    }
+  }
+}
+
+// kl_gram_bwd_tiles' table twin (flag 2): the same G, weights, slots and partials
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WPE))) void kl_gram_bwd_tab_kernel(GramTab tb, const double* __restrict__ x, int ldx,
+                                                              int n, int np_, int qs,
+                                                              const double* __restrict__ params,
+                                                              const float* __restrict__ Kinv,
+                                                              const float* __restrict__ S,
+                                                              const float* __restrict__ Sx, int nsplit,
+                                                              const double* __restrict__ alpha,
+                                                              double* __restrict__ part, int ntiles,
+                                                              const int* __restrict__ covflag) {
+  if (*covflag != 2) return;  // (uniform, before any barrier)
+  __shared__ float sx1[kGT * kMaxQB];
+  __shared__ float sx2[kGT * kMaxQB];
+  __shared__ float sp[64];
+  __shared__ float sa1[kGT], sa2[kGT];
+  __shared__ double wred[4][kBwdSlots];
+  extern __shared__ float tdyn[];  // [(n_params + 1) x 256] per-thread sums, then the tables
+  const int G = gridDim.x, g0 = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  const int lane = tid & 63, wv = tid >> 6, np_s = tb.n_params;
+  float* tab = tdyn + (np_s + 1) * 256;
+  auto tacc = [&](int q) -> float& { return tdyn[(q == kNoiseSlot ? np_s : q) * 256 + tid]; };
+  if (tid < np_s) sp[tid] = float(params[(int64_t)l * np_s + tid]);
+  for (int e = tid; e < 4 * kBwdSlots; e += 256) (&wred[0][0])[e] = 0.0;
+  for (int q = 0; q < np_s; ++q) tacc(q) = 0.f;
+  tacc(kNoiseSlot) = 0.f;
+  __syncthreads();
+  tab_build_bwd(tb, sp, tab);
+  const int tstride = (1 << tb.nbits) * kTabR;
+  const float* ki = Kinv + (int64_t)l * np_ * np_;
+  const float* si = S + (int64_t)l * np_ * np_;
+  const double* al = alpha + (int64_t)l * np_;
+  // software pipeline: tile t + G's K^-1 / S rows, covariates and alpha entries are loaded into registers
+  // while tile t is evaluated, and stored to LDS between two barriers at its end
+  auto load_ks = [&](int i0, int j0, g_f32x4 (&kv4)[4], g_f32x4 (&sv4)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int64_t o = (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc;
+      kv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(ki + o));
+      sv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(si + o));
+    }
+    for (int q = 1; q < nsplit; ++q) {  // K-split partials of S (syrk_x3_splits)
+      const float* sq = Sx + (int64_t)(q - 1) * gridDim.y * np_ * np_ + (int64_t)l * np_ * np_;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        sv4[a] += __builtin_nontemporal_load(
+            reinterpret_cast<const g_f32x4*>(sq + (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc));
+    }
+  };
+  float dd = 0.f;
+  int since_flush = 0;
+  int t = g0, I = 0, J = 0;
+  g_f32x4 kv4[4], sv4[4];
+  CovPrefetchF pf;
+  double an = 0.0;
+  if (t < ntiles) {
+    tri_index(t, I, J);
+    load_ks(I * kGT, J * kGT, kv4, sv4);
+    pf.load(x, ldx, n, qs, I * kGT, J * kGT);
+    if (tid < 2 * kGT) an = al[(tid < kGT ? I : J) * kGT + (tid & (kGT - 1))];
+    pf.store(qs, sx1, sx2);
+    if (tid < kGT) sa1[tid] = float(an);
+    else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
+  }
+  __syncthreads();  // the tables and the first tile's LDS
+  for (; t < ntiles; t += G) {
+    const int i0 = I * kGT, j0 = J * kGT;
+    const bool more = t + G < ntiles;
+    int In = 0, Jn = 0;
+    g_f32x4 kn4[4], sn4[4];
+    if (!LVAE_TAB_PIPE && t != g0) load_ks(i0, j0, kv4, sv4);
+    if (more) {
+      tri_index(t + G, In, Jn);
+      if (LVAE_TAB_PIPE) load_ks(In * kGT, Jn * kGT, kn4, sn4);
+      pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
+      if (tid < 2 * kGT) an = al[(tid < kGT ? In : Jn) * kGT + (tid & (kGT - 1))];
+    }
+    float g[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int i = i0 + 4 * tr + a;
+      const g_f32x4 kv = kv4[a], sv = sv4[a];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = j0 + 4 * tc + c;
+        const float gv = 0.5f * (kv[c] - sv[c] - sa1[4 * tr + a] * sa2[4 * tc + c]);
+        const bool in = i < n && j < n && j <= i;
+        if (in && i == j) dd += gv;
+        g[a][c] = in ? ((i == j) ? gv : 2.f * gv) : 0.f;
+      }
+    }
+#pragma unroll 1
+    for (int gi = 0; gi < tb.ng; ++gi) {
+      int idx[4][4];  // (the gate bits recomputed per group: fewer live registers)
+      tab_bits(tb, sx1, sx2, tr, tc, idx);
+      tab_index(tb, gi, sx1, sx2, tr, tc, idx, idx);
+#pragma unroll 1
+      for (int k = tb.pbeg[gi]; k < tb.pbeg[gi + 1]; ++k) {
+        const float* tk = tab + k * tstride;
+        float acc = 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc += g[a][c] * tk[idx[a][c]];
+        tacc(tb.porder[k]) += acc;
+      }
+    }
+    if (++since_flush == 4 || t + G >= ntiles) {  // fold the fp32 sums into the fp64 wave slots
+      since_flush = 0;
+      tacc(kNoiseSlot) += dd;
+      dd = 0.f;
+      for (int q = 0; q < kBwdSlots; ++q) {
+        if (q >= np_s && q != kNoiseSlot) continue;  // (uniform)
+        const float w = wave_sum(tacc(q));
+        if (lane == 0) wred[wv][q] += (double)w;
+        tacc(q) = 0.f;
+      }
+    }
+    if (more) {
+      __syncthreads();  // every reader of this tile's LDS is done
+      pf.store(qs, sx1, sx2);
+      if (tid < kGT) sa1[tid] = float(an);
+      else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
+      __syncthreads();
+      if (LVAE_TAB_PIPE) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          kv4[a] = kn4[a];
+          sv4[a] = sn4[a];
+        }
+      }
+      I = In, J = Jn;
     }
   }
   __syncthreads();
@@ -795,6 +1272,12 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_reduce(BwdParamInfo pinfo, in
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
+// LVAE_<name>=0 in the environment switches a fast path off (A/B runs)
+static bool getenv_off(const char* name) {
+  const char* v = getenv(name);
+  return v && atoi(v) == 0;
+}
+
 static int spec_qs(const lvae_kernel_spec* s) {
   int q = 0;
   for (int r = 0; r < s->n_comp; ++r)
@@ -833,7 +1316,15 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   int G = (2048 + L - 1) / L;  // ~8 resident workgroups per CU, 2 rounds
   G = G < ntiles ? G : ntiles;
   dim3 grid(G, L);
-  cov_int_check_kernel<<<1, 1024, 0, st>>>(x, ldx, n, qs, covflag);
+  GramTab tb;
+  const bool tab_ok = gram_tab_build(spec, tb) && !getenv_off("LVAE_GRAM_TAB");
+  int tabmask = 0;
+  for (int g = 0; g < tb.ng && tab_ok; ++g)
+    if (tb.gdim[g] >= 0) tabmask |= 1 << tb.gdim[g];
+  cov_int_check_kernel<<<1, 1024, 0, st>>>(x, ldx, n, qs, tab_ok, tabmask, covflag);
+  if (tab_ok)
+    gram_sq_fill_tab_kernel<<<grid, 256, (size_t)tb.ng * (1 << tb.nbits) * kTabR * sizeof(float), st>>>(
+        tb, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
   if (bucket == 1) {
     gram_sq_fill_kernel<8, 2, float><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
     gram_sq_fill_kernel<8, 2, double><<<grid, 256, 0, st>>>(ds, x, ldx, n, np_, qs, params, noise, K, ntiles, covflag);
@@ -910,6 +1401,12 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
     }
   const int nt = np_ / kGT, ntiles = nt * (nt + 1) / 2, G = kl_gram_bwd_groups(np_, L);
   const size_t dyn = (size_t)(spec->n_params + 1) * 256 * sizeof(float);
+  GramTab tb;
+  if (gram_tab_build(spec, tb) && !getenv_off("LVAE_GRAM_TAB")) {  // (the same decision as kl_gram_fill's)
+    const size_t tdyn = dyn + (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
+    kl_gram_bwd_tab_kernel<<<dim3(G, L), 256, tdyn, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                          alpha, part, ntiles, covflag);
+  }
   if (bucket == 1) {
     kl_gram_bwd_tiles<8, 2, float><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
                                                                   alpha, part, ntiles, covflag);

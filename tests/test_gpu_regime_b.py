@@ -638,7 +638,9 @@ def test_kl_closed_resid_paths(hip, case):
     "c5"), the rest through the tiled O(N^2) kernel (times shifted by 0.5: "half_time"; a time window
     of 76 > 64 values: "wide_window").  dmu = K^-1 mu is the refined quantity: within 1e-8 of the fp64
     oracle (the refinement reaches ~1e-10 here; a residual that missed terms leaves the fp32-equivalent
-    inverse's ~1e-5), and the KL within 1e-6."""
+    inverse's ~1e-5), and the KL within 1e-6.  The same cases select the Gram fill / adjoint paths
+    (gram.hip covariate flag): tables for "integer" / "gates_masks", fp32 covariates for "wide_window"
+    and "c5" (a linear factor), fp64 covariates for "half_time" -- dlogv and draw within 1e-4."""
     import lvae_amd as la
     from lvae_amd.data import health_mnist_covariates
     P, T, L = 64, 16, 2
@@ -668,12 +670,16 @@ def test_kl_closed_resid_paths(hip, case):
     kl.sum().backward()
     spec = _c5_spec() if case == "c5" else O.spec_full(**cfg)
     for l in range(L):
-        m_ = mu[:, l].clone().requires_grad_()
-        ref = O.kl_closed(spec, O.constrain(raw[l]), X, 1.0, m_, lv[:, l])
+        r = raw[l].clone().requires_grad_()
+        m_, v_ = mu[:, l].clone().requires_grad_(), lv[:, l].clone().requires_grad_()
+        ref = O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_)
         ref.backward()
         e_kl, e_mu = rel(kl[l], ref), rel(mu_d.grad[:, l], m_.grad)
-        print(f"{case} dim {l}: kl {e_kl:.2e} dmu {e_mu:.2e}")
+        e_lv = rel(lv_d.grad[:, l], v_.grad)
+        e_raw = rel(torch.stack([p.grad[l] for _, p in kd.named_parameters()]), r.grad)
+        print(f"{case} dim {l}: kl {e_kl:.2e} dmu {e_mu:.2e} dlogv {e_lv:.2e} draw {e_raw:.2e}")
         assert e_kl < 1e-6 and e_mu < 1e-8, (case, l, e_kl, e_mu)
+        assert e_lv < 1e-4 and e_raw < 1e-4, (case, l, e_lv, e_raw)
 
 
 def test_closed_step_vs_oracle(hip):
