@@ -638,6 +638,9 @@ __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_,
 // (workgroups with i >= nt exit at once); lauum the L nt (nt + 1) / 2 lower tiles.
 // ------------------------------------------------------------------------------------------
 constexpr int kCiX = 0, kCiY = 1, kCiLauum = 2, kCiLauumKL = 3;
+#ifndef LVAE_KL_MIRROR
+#define LVAE_KL_MIRROR 0  // 1: the KL lauum also writes the upper tiles of K^-1 (no reader needs them)
+#endif
 struct CiGemmArgs {
   const _Float16 *ah, *al, *bh, *bl;  // full plane arrays
   _Float16 *oh, *ol, *oth, *otl;      // outputs: row-major planes (kCiY), transposed planes (kCiX, kCiY)
@@ -887,9 +890,11 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
             }
         }
       }
-      if (i != j)
+      // (no mirror of K^-1 here: the exact KL's readers -- kl_alpha_sym_kernel, the Gram adjoint, the
+      // diagonal -- read its lower tiles only; the B planes need both halves)
+      if (i != j && (g.bh_out || LVAE_KL_MIRROR))
         ci_transposed_out(acc, 1.f, lds, [&](int c, int r0, f32x4 v) {
-          *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
+          if (LVAE_KL_MIRROR) *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
           if (g.bh_out) {
             const f32x4 s4 = *reinterpret_cast<const f32x4*>(&kl_sv[r0]);
             // B(j, i) row c, columns r0 .. r0 + 3 (one 4-half run of a chunk either way)

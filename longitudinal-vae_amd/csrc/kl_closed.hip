@@ -138,6 +138,84 @@ __global__ __launch_bounds__(256) void kl_alpha_kernel(const float* __restrict__
   }
 }
 
+// The same product over the lower 64-tiles only (K^-1 is symmetric; half the bytes): tile (I, J), I >= J,
+// gives its row sums K_IJ u_J to rows of block I and, off the diagonal, its column sums K_IJ^T u_I to rows
+// of block J, each written once to part[l][other block][row]; kl_alpha_reduce adds them in a fixed order
+// (deterministic).  Grid (G, L), the tiles t = g, g + G, ...; thread (tr, tc) reads rows 4 tr + a,
+// columns 4 tc .. 4 tc + 3 (float4: 16 lanes per 256-byte row segment).
+__device__ inline void alpha_tri_index(int t, int& I, int& J) {
+  int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  I = r;
+  J = t - r * (r + 1) / 2;
+}
+__global__ __launch_bounds__(256) void kl_alpha_sym_kernel(const float* __restrict__ Kinv,
+                                                           const double* __restrict__ u, int np_,
+                                                           double* __restrict__ part, int ntiles) {
+  __shared__ double cred[4][64];
+  const int G = gridDim.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15, wv = tid >> 6;
+  const int nt = np_ / 64;
+  const float* K = Kinv + (int64_t)l * np_ * np_;
+  const double* ul = u + (int64_t)l * np_;
+  for (int t = blockIdx.x; t < ntiles; t += G) {
+    int I, J;
+    alpha_tri_index(t, I, J);
+    const int i0 = I * 64, j0 = J * 64;
+    float4 k[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      k[a] = *reinterpret_cast<const float4*>(K + (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc);
+    double uj[4], ui[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) uj[c] = ul[j0 + 4 * tc + c];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) ui[a] = ul[i0 + 4 * tr + a];
+    double rs[4], cs[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      rs[a] = (double)k[a].x * uj[0] + (double)k[a].y * uj[1] + (double)k[a].z * uj[2] + (double)k[a].w * uj[3];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) rs[a] += __shfl_xor(rs[a], o, 64);
+    }
+    if (tc == 0) {
+      double* pr = part + ((int64_t)l * nt + J) * np_ + i0 + 4 * tr;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) pr[a] = rs[a];
+    }
+    if (I != J) {  // (uniform)
+      cs[0] = (double)k[0].x * ui[0] + (double)k[1].x * ui[1] + (double)k[2].x * ui[2] + (double)k[3].x * ui[3];
+      cs[1] = (double)k[0].y * ui[0] + (double)k[1].y * ui[1] + (double)k[2].y * ui[2] + (double)k[3].y * ui[3];
+      cs[2] = (double)k[0].z * ui[0] + (double)k[1].z * ui[1] + (double)k[2].z * ui[2] + (double)k[3].z * ui[3];
+      cs[3] = (double)k[0].w * ui[0] + (double)k[1].w * ui[1] + (double)k[2].w * ui[2] + (double)k[3].w * ui[3];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        cs[c] += __shfl_xor(cs[c], 16, 64);
+        cs[c] += __shfl_xor(cs[c], 32, 64);
+      }
+      __syncthreads();  // the previous tile's readers of cred are done
+      if ((tid & 63) < 16) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cred[wv][4 * tc + c] = cs[c];
+      }
+      __syncthreads();
+      if (tid < 64)
+        part[((int64_t)l * nt + I) * np_ + j0 + tid] = ((cred[0][tid] + cred[1][tid]) + cred[2][tid]) + cred[3][tid];
+    }
+  }
+}
+
+// alpha[l][i] = base[l][i] + sum_s part[l][s][i] (fixed order).  Grid (np / 256, L).
+__global__ __launch_bounds__(256) void kl_alpha_reduce(const double* __restrict__ part, const double* base, int np_,
+                                                       double* alpha) {
+  const int i = blockIdx.x * 256 + threadIdx.x, l = blockIdx.y, nt = np_ / 64;
+  if (i >= np_) return;
+  double acc = 0.0;
+  for (int s = 0; s < nt; ++s) acc += part[((int64_t)l * nt + s) * np_ + i];
+  const int64_t o = (int64_t)l * np_ + i;
+  alpha[o] = base[o] + acc;
+}
+
 __global__ __launch_bounds__(256) void kl_finalize_kernel(const double* __restrict__ muc, const double* __restrict__ logv,
                                                           int ld, const double* __restrict__ alpha,
                                                           const double* __restrict__ kdiag,
@@ -254,7 +332,13 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
   }
   LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res,
                          rb_on ? ws.rb : nullptr, st));
-  kl_alpha_kernel<<<dim3(np_ / 4, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.alpha, ws.alpha);
+  {  // alpha = a0 + K^-1 r over the lower tiles of K^-1 (the residual's partials buffer is free again)
+    const int nt64 = np_ / 64, ntiles = nt64 * (nt64 + 1) / 2;
+    int G = (2048 + L - 1) / L;
+    G = G < ntiles ? G : ntiles;
+    kl_alpha_sym_kernel<<<dim3(G, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.rpart, ntiles);
+    kl_alpha_reduce<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.rpart, ws.alpha, np_, ws.alpha);
+  }
   kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   LVAE_CHECK_LAUNCH();
   return 0;
