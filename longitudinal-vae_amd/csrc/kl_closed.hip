@@ -211,7 +211,15 @@ __global__ __launch_bounds__(256) void kl_alpha_reduce(const double* __restrict_
   const int i = blockIdx.x * 256 + threadIdx.x, l = blockIdx.y, nt = np_ / 64;
   if (i >= np_) return;
   double acc = 0.0;
-  for (int s = 0; s < nt; ++s) acc += part[((int64_t)l * nt + s) * np_ + i];
+  const double* pl = part + (int64_t)l * nt * np_ + i;
+  for (int s = 0; s < nt; s += 4) {  // (nt = np / 64: a multiple of 4) loads first, adds in order
+    const double v0 = pl[(int64_t)s * np_], v1 = pl[(int64_t)(s + 1) * np_];
+    const double v2 = pl[(int64_t)(s + 2) * np_], v3 = pl[(int64_t)(s + 3) * np_];
+    acc += v0;
+    acc += v1;
+    acc += v2;
+    acc += v3;
+  }
   const int64_t o = (int64_t)l * np_ + i;
   alpha[o] = base[o] + acc;
 }

@@ -1,11 +1,11 @@
 """Dev: one step's kernel timeline from a rocprofv3 --kernel-trace CSV (the last complete step: from the
-last-but-one to the last gram_sq_fill launch).  Prints every kernel (start offset, duration, stream /
+last-but-one to the last cov_int_check launch, the first kernel of a step).  Prints every kernel (start offset, duration, stream /
 queue, name) and the union of busy time, so the idle stretches of the step show."""
 import csv
 import sys
 
 
-def main(path, marker="gram_sq_fill"):
+def main(path, marker="cov_int_check"):
     rows = list(csv.DictReader(open(path)))
     ks = []
     for r in rows:
