@@ -6,7 +6,7 @@
 //                   Replaces torch.cholesky + cholesky_solve(I) at elbo_functions.py:176-186 and
 //                   training.py:130-134 (M = 120 -> 128: 8 waves x 8 tiles, 8 + 8 + 8 block steps).
 //   gemm_small    : C = alpha op(A) op(B) + beta C over a two-level batch; 32x32 output tile per
-//                   workgroup, K staged through LDS in chunks of 32.
+//                   workgroup on v_mfma_f64_16x16x4f64, K staged through LDS in one pass (K <= 128).
 #include "common.hpp"
 #include "blkinv.hpp"
 
@@ -34,55 +34,66 @@ __global__ __launch_bounds__(64 * TS * TS / TPW) void spd_inv_small_kernel(int n
                                  s.logdet + b, 0, s.info + b, 0);
 }
 
-constexpr int kGS = 32;
+constexpr int kGS = 32;   // output tile edge
+constexpr int kGK = 128;  // K staged per pass (every Hensman product has K <= 128: one pass)
 
+// 32 x 32 output tile per 256-thread workgroup, one 16 x 16 quarter per wave on v_mfma_f64_16x16x4f64
+// (C[(lane >> 4) + 4 r][lane & 15], blkinv.hpp); op(A) and op(B) staged for the whole K (<= 128 per pass)
+// in one round of loads, then kc / 4 MFMAs per wave -- one global-latency round trip per launch instead
+// of one per 32-deep chunk.
 __global__ __launch_bounds__(256) void gemm_small_kernel(int ta, int tb, int m, int n, int k, double alpha,
                                                          const double* __restrict__ A, int lda, int64_t sa1,
                                                          int64_t sa2, const double* __restrict__ B, int ldb,
                                                          int64_t sb1, int64_t sb2, double beta,
                                                          double* __restrict__ C, int ldc, int64_t sc1, int64_t sc2,
                                                          int nb2) {
-  __shared__ double As[kGS][kGS + 1];  // [i][kk]
-  __shared__ double Bs[kGS][kGS + 1];  // [kk][j]
+  __shared__ double As[kGS][kGK + 1];  // [i][kk]
+  __shared__ double Bs[kGK][kGS + 1];  // [kk][j]
   const int bz = blockIdx.z, b1 = bz / nb2, b2 = bz % nb2;
   const double* a = A + b1 * sa1 + b2 * sa2;
   const double* bb = B + b1 * sb1 + b2 * sb2;
   double* c = C + b1 * sc1 + b2 * sc2;
   const int i0 = blockIdx.y * kGS, j0 = blockIdx.x * kGS;
-  const int tid = threadIdx.x, tj = tid & 31, ti = tid >> 5;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < k; k0 += kGS) {
-    for (int e = tid; e < kGS * kGS; e += 256) {
-      const int r = e >> 5, q = e & 31;
-      // As[r][q] = op(A)[i0 + r][k0 + q];  Bs[r][q] = op(B)[k0 + r][j0 + q]
-      {
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wr = (w >> 1) * 16, wc = (w & 1) * 16;
+  bi_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < k; k0 += kGK) {
+    const int kc = k - k0 < kGK ? k - k0 : kGK, kc4 = (kc + 3) & ~3;  // zero-padded to whole MFMA steps
+    // op(A)[i0 + r][k0 + q]: q fastest when A is row-major in k (ta = 0), r fastest when transposed
+#pragma unroll
+    for (int u = 0; u < kGS * kGK / 256; ++u) {  // (constant trip count: the loads issue together)
+      const int e = tid + 256 * u;
+      const int r = ta ? (e & (kGS - 1)) : (e >> 7), q = ta ? (e >> 5) : (e & (kGK - 1));
+      if (q < kc4) {
         const int i = i0 + r, kk = k0 + q;
         double v = 0.0;
-        if (i < m && kk < k) v = ta ? a[(int64_t)kk * lda + i] : a[(int64_t)i * lda + kk];
+        if (i < m && q < kc) v = ta ? a[(int64_t)kk * lda + i] : a[(int64_t)i * lda + kk];
         As[r][q] = v;
       }
-      {
+    }
+    // op(B)[k0 + r][j0 + q]: q fastest for row-major B (tb = 0)
+#pragma unroll
+    for (int u = 0; u < kGK * kGS / 256; ++u) {
+      const int e = tid + 256 * u;
+      const int r = tb ? (e & (kGK - 1)) : (e >> 5), q = tb ? (e >> 7) : (e & (kGS - 1));
+      if (r < kc4) {
         const int kk = k0 + r, j = j0 + q;
         double v = 0.0;
-        if (kk < k && j < n) v = tb ? bb[(int64_t)j * ldb + kk] : bb[(int64_t)kk * ldb + j];
+        if (r < kc && j < n) v = tb ? bb[(int64_t)j * ldb + kk] : bb[(int64_t)kk * ldb + j];
         Bs[r][q] = v;
       }
     }
     __syncthreads();
-#pragma unroll 8
-    for (int q = 0; q < kGS; ++q) {
-      const double bv = Bs[q][tj];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] += As[ti + 8 * u][q] * bv;
-    }
+    for (int kk = 0; kk < kc4; kk += 4)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(As[wr + li][kk + lk], Bs[kk + lk][wc + li], acc, 0, 0, 0);
     __syncthreads();
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int i = i0 + ti + 8 * u, j = j0 + tj;
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + wr + lk + 4 * r, j = j0 + wc + li;
     if (i < m && j < n) {
       double* p = c + (int64_t)i * ldc + j;
-      *p = (beta == 0.0) ? alpha * acc[u] : alpha * acc[u] + beta * *p;
+      *p = (beta == 0.0) ? alpha * acc[r] : alpha * acc[r] + beta * *p;
     }
   }
 }
