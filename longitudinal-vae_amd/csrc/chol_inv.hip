@@ -615,11 +615,17 @@ __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_,
     }
   }
   __syncthreads();
-  for (int e = t; e < 64 * 64; e += 256) {  // Y^T (b, a) row c, column r = D (a, b) (r, c)
-    const int c = e >> 6, r = e & 63;
-    const int64_t o = kCiC16 ? c16_off(l, np_, k * kSwB + 64 * pb + c, k * kSwB + 64 * pa + r) : oyt + (int64_t)c * np_ + r;
-    YTh[o] = tp[0][r][c];
-    YTl[o] = tp[1][r][c];
+  for (int e = t; e < 64 * 8; e += 256) {  // Y^T (b, a) row c, columns r0 .. r0 + 7 = D (a, b) (r, c): 16-B stores
+    const int c = e >> 3, r0 = (e & 7) * 8;
+    x3_half8 h, lo;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      h[q] = tp[0][r0 + q][c];
+      lo[q] = tp[1][r0 + q][c];
+    }
+    const int64_t o = kCiC16 ? c16_off(l, np_, k * kSwB + 64 * pb + c, k * kSwB + 64 * pa + r0) : oyt + (int64_t)c * np_ + r0;
+    *reinterpret_cast<x3_half8*>(YTh + o) = h;
+    *reinterpret_cast<x3_half8*>(YTl + o) = lo;
   }
 }
 
