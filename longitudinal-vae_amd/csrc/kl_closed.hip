@@ -24,6 +24,10 @@
 #include "prof.hpp"
 
 
+#ifndef LVAE_ALPHA_WG
+#define LVAE_ALPHA_WG 4096
+#endif
+
 namespace lvae {
 
 int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
@@ -342,7 +346,7 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
                          rb_on ? ws.rb : nullptr, st));
   {  // alpha = a0 + K^-1 r over the lower tiles of K^-1 (the residual's partials buffer is free again)
     const int nt64 = np_ / 64, ntiles = nt64 * (nt64 + 1) / 2;
-    int G = (2048 + L - 1) / L;
+    int G = (LVAE_ALPHA_WG + L - 1) / L;  // workgroups in all (~16 resident per CU: more loads in flight)
     G = G < ntiles ? G : ntiles;
     kl_alpha_sym_kernel<<<dim3(G, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.rpart, ntiles);
     kl_alpha_reduce<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.rpart, ws.alpha, np_, ws.alpha);
