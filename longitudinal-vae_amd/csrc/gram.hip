@@ -863,19 +863,27 @@ __global__ __launch_bounds__(256) void gram_sq_fill_tab_kernel(GramTab tb, const
 #pragma unroll
         for (int c = 0; c < 4; ++c) out[a][c] += tg[idx[a][c]];
     }
+    if (I != J && i0 + kGT <= n) {  // (uniform) an interior tile below the diagonal: no noise, no padding
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int i = i0 + 4 * tr + a;
-      g_f32x4 w;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int j = j0 + 4 * tc + c;
-        float e = out[a][c];
-        if (i == j) e += nz;
-        if (i >= n || j >= n) e = (i == j) ? 1.0f : 0.0f;
-        w[c] = e;
+      for (int a = 0; a < 4; ++a) {
+        const g_f32x4 w = {out[a][0], out[a][1], out[a][2], out[a][3]};
+        *reinterpret_cast<g_f32x4*>(o + (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc) = w;
       }
-      *reinterpret_cast<g_f32x4*>(o + (int64_t)i * np_ + j0 + 4 * tc) = w;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int i = i0 + 4 * tr + a;
+        g_f32x4 w;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int j = j0 + 4 * tc + c;
+          float e = out[a][c];
+          if (i == j) e += nz;
+          if (i >= n || j >= n) e = (i == j) ? 1.0f : 0.0f;
+          w[c] = e;
+        }
+        *reinterpret_cast<g_f32x4*>(o + (int64_t)i * np_ + j0 + 4 * tc) = w;
+      }
     }
     if (more) {
       __syncthreads();  // every reader of this tile's covariates is done
