@@ -614,9 +614,6 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
 #ifndef LVAE_TAB_WPE
 #define LVAE_TAB_WPE 3  // the table adjoint's waves per SIMD (register cap)
 #endif
-#ifndef LVAE_TAB_PIPE
-#define LVAE_TAB_PIPE 0  // 1: the table adjoint holds the next tile's K^-1 / S rows in registers
-#endif
 constexpr int kTabMaxG = 3, kTabMaxBits = 5;
 constexpr int kTabR = kTabD + 1;  // table row stride (odd: the rows of different gate bits on other banks)
 constexpr int kTabMaxFillLds = kTabMaxG * (1 << kTabMaxBits) * kTabR;  // floats
@@ -925,8 +922,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
   const float* ki = Kinv + (int64_t)l * np_ * np_;
   const float* si = S + (int64_t)l * np_ * np_;
   const double* al = alpha + (int64_t)l * np_;
-  // software pipeline: tile t + G's K^-1 / S rows, covariates and alpha entries are loaded into registers
-  // while tile t is evaluated, and stored to LDS between two barriers at its end
+  // tile t + G's covariates and alpha entries are loaded into registers while tile t is evaluated, and
+  // stored to LDS between two barriers at its end (holding its K^-1 / S rows too was slower: registers)
   auto load_ks = [&](int i0, int j0, g_f32x4 (&kv4)[4], g_f32x4 (&sv4)[4]) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -962,11 +959,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
     const int i0 = I * kGT, j0 = J * kGT;
     const bool more = t + G < ntiles;
     int In = 0, Jn = 0;
-    g_f32x4 kn4[4], sn4[4];
-    if (!LVAE_TAB_PIPE && t != g0) load_ks(i0, j0, kv4, sv4);
+    if (t != g0) load_ks(i0, j0, kv4, sv4);
     if (more) {
       tri_index(t + G, In, Jn);
-      if (LVAE_TAB_PIPE) load_ks(In * kGT, Jn * kGT, kn4, sn4);
       pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
       if (tid < 2 * kGT) an = al[(tid < kGT ? In : Jn) * kGT + (tid & (kGT - 1))];
     }
@@ -1017,13 +1012,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
       if (tid < kGT) sa1[tid] = float(an);
       else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
       __syncthreads();
-      if (LVAE_TAB_PIPE) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          kv4[a] = kn4[a];
-          sv4[a] = sn4[a];
-        }
-      }
       I = In, J = Jn;
     }
   }
