@@ -44,7 +44,7 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3s3_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3s3f_pmc_summary.json")
 # the Cholesky's trailing rank-256 update (chol_inv.hip): U2 alone (MODE kCiU2) when the lookahead chain
 # runs on the side stream (schedule (b), > CI_FUSE_MAX_L dims per call), else fused with U1 (kCiU12)
 CI_FUSE_MAX_L = 16

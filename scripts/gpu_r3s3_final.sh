@@ -4,10 +4,10 @@
 # default bench line (CPU baseline included).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 PYTEST_TIMEOUT=700 SKIP_BENCH=1 bash scripts/gpu_tests.sh || exit $?
-PMC_NAME=pmc_r3s3 bash scripts/pmc_r3.sh > gpurun_out/pmc_r3s3.log 2>&1 || { tail -20 gpurun_out/pmc_r3s3.log; exit 1; }
-tail -3 gpurun_out/pmc_r3s3.log
-PROF_NAME=r3s3 CFGS="headline c5rank L2" bash scripts/prof_r3.sh > gpurun_out/prof_r3s3.log 2>&1 || { tail -20 gpurun_out/prof_r3s3.log; exit 1; }
-grep -h "ms_per_step\|total kernel" gpurun_out/prof_r3s3.log | cut -c1-200
+PMC_NAME=pmc_${PROF_NAME:-r3s3} bash scripts/pmc_r3.sh > gpurun_out/pmc_${PROF_NAME:-r3s3}.log 2>&1 || { tail -20 gpurun_out/pmc_${PROF_NAME:-r3s3}.log; exit 1; }
+tail -3 gpurun_out/pmc_${PROF_NAME:-r3s3}.log
+PROF_NAME=${PROF_NAME:-r3s3} CFGS="headline c5rank L2" bash scripts/prof_r3.sh > gpurun_out/prof_${PROF_NAME:-r3s3}.log 2>&1 || { tail -20 gpurun_out/prof_${PROF_NAME:-r3s3}.log; exit 1; }
+grep -h "ms_per_step\|total kernel" gpurun_out/prof_${PROF_NAME:-r3s3}.log | cut -c1-200
 echo "[$(date +%T)] default bench"
-timeout -k 10 600 python3 bench.py > gpurun_out/r3s3_bench.json 2> gpurun_out/r3s3_bench.err || { tail -20 gpurun_out/r3s3_bench.err; exit 1; }
-cut -c1-400 gpurun_out/r3s3_bench.json
+timeout -k 10 600 python3 bench.py > gpurun_out/${PROF_NAME:-r3s3}_bench.json 2> gpurun_out/${PROF_NAME:-r3s3}_bench.err || { tail -20 gpurun_out/${PROF_NAME:-r3s3}_bench.err; exit 1; }
+cut -c1-400 gpurun_out/${PROF_NAME:-r3s3}_bench.json
