@@ -2,20 +2,25 @@
 // analytic backward, batched over the L latent dims (replaces the Python loop at training.py:515-522).
 //
 // factor (needs only the covariates and hyper-parameters: launched before the encoder has run):
-//   K_l = Gram_l(x, x) + noise_l I                (gram_sq_fill, f32, padded to np)
+//   K_l = Gram_l(x, x) + noise_l I                (kl_gram_fill, f32, padded to np; table / fp32 / fp64
+//                                                   covariate paths chosen on the device, gram.hip)
 //   Y = L^-1, log|K|                               (ci_factor_f32: blocked Cholesky + trtri, f16 x3 MFMA,
 //                                                   chol_inv.hip)
+//   the binned residual's plan                     (kl_resid_bins_plan, on the side stream behind the
+//                                                   pivot chain; integer-coded covariates only)
 // reduce (needs mu, log v):
 //   K^-1 = Y^T Y, the partials of a0 = K^-1 mu,    (ci_lauum_f32 with the KL epilogue: one pass over the
 //   and B = K^-1 diag(sqrt v) as fp16 hi / lo       K^-1 tiles while they are in registers; B only when a
 //   planes, one power-of-two scale per dim          backward follows)
 //   a0, d = diag K^-1                              (kl_alpha0_kernel: fixed-order sum of the partials)
-//   r = mu - K a0                                  (kl_gram_resid: fp64 Gram-free residual, gram.hip)
-//   a = a0 + K^-1 r                                (kl_alpha_kernel, f64 accumulation: one step of
-//                                                   iterative refinement)
+//   r = mu - K a0                                  (kl_gram_resid: fp64 Gram-free residual, binned
+//                                                   O(N W) (kl_resid_bins.hip) or tiled O(N^2), gram.hip)
+//   a = a0 + K^-1 r                                (kl_alpha_sym_kernel over the lower tiles of K^-1, f64
+//                                                   accumulation: one step of iterative refinement)
 //   kl_l = 1/2 (sum v d + mu.a - n + logdet - sum log v)
 // backward (dL/dkl_l = g_l):
-//   S = K^-1 V K^-1 = B B^T                        (syrk_tiles_f32, f16 x3 MFMA, lower tiles)
+//   S = K^-1 V K^-1 = B B^T                        (syrk_tiles_f32, f16 x3 MFMA, lower tiles; K^-1 itself
+//                                                   is kept as its lower tiles only)
 //   G = 1/2 (K^-1 - S - a a^T) -> dtheta, dnoise   (kl_gram_bwd, fused, never materialised)
 //   dmu = g a,  dlogv = g/2 (v d - 1)
 // One reduce per factor: the backward's S overwrites the Y^T planes.
