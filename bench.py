@@ -3,7 +3,8 @@
 Headline (`value`): the exact-KL step of standard_training (type_KL='closed', loss='mse';
 training.py:484-592) at BASELINE configs[2] = N = 4096 observations (P = 256 subjects x T = 16),
 L = 16 latent dims: full-batch ConvVAE forward / backward (fp32, PyTorch-ROCm) + the exact GP-prior
-KL of all L dims forward and backward (HIP: Gram, block-sweep inverse, S GEMM, Gram adjoint) + Adam.
+KL of all L dims forward and backward (HIP: Gram, blocked Cholesky potrf + trtri + lauum, fp64
+refinement of K^-1 mu, S GEMM, Gram adjoint) + Adam.
   N = 1: one process.  N > 1: the SAME step (same objective, same N and L) with the latent dims
   sharded over the ranks and the images split over them (lvae_amd.distributed.
   LatentShardedClosedStep): strong scaling, value = whole-job ELBO-steps/s.
@@ -12,8 +13,9 @@ Sub-record `regime_a` (BASELINE configs[3], the path config/LVAE_config_sample.t
 Hensman SVI step (training.py:90-140) at L = 16, M = 120, P_b = 5 subjects x T = 16 per rank, data
 parallel over subject mini-batches for N > 1 (weak scaling), replayed as HIP graphs.
 
-Sub-record `c2` (BASELINE configs[1], N = 1 only): HIP Gram + sweep inverse + log-det vs PyTorch-ROCm
-Gram + torch.linalg.cholesky (+ cholesky_inverse) at N = 1024, L = 8.
+Sub-record `c2` (BASELINE configs[1], N = 1 only): HIP Gram + blocked Cholesky inverse + log-det (the
+product route, lvae_spd_inv_chol_f32) vs PyTorch-ROCm Gram + torch.linalg.cholesky (+ cholesky_inverse)
+at N = 1024, L = 8; GP-Cholesky GFLOP/s from the potrf phase alone on both sides.
 
 Prints ONE JSON line on rank 0 (the driver's contract); diagnostics go to stderr.
 """
@@ -45,6 +47,10 @@ DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3s3f_pmc_summary.json")
+# The committed rocprofv3 --kernel-trace --stats summary of the default closed bench on the final tree
+# (scripts/gpu_r4a.sh): the roofline's `frac` is priced on its average launch duration of the dominant
+# kernel, so that it recomputes from profiles/; the live HIP-event figure is reported beside it.
+KSTATS = os.path.join(ROOT, "profiles", "r4_headline_kernel_stats.csv")
 # the Cholesky's trailing rank-256 update (chol_inv.hip): U2 alone (MODE kCiU2) when the lookahead chain
 # runs on the side stream (schedule (b), > CI_FUSE_MAX_L dims per call), else fused with U1 (kCiU12)
 CI_FUSE_MAX_L = 16
@@ -74,15 +80,37 @@ def pmc_traffic(kernels, per_step=False):
         return None
 
 
-def setup_dist():
+def kstats_avg_us(name_part, path=KSTATS):
+    """(average launch duration in us, calls) of the kernel whose name contains name_part in the
+    committed rocprofv3 stats CSV, or None."""
+    import csv
+    try:
+        for r in csv.DictReader(open(path)):
+            if name_part in r["Name"]:
+                return float(r["AverageNs"]) / 1e3, int(r["Calls"])
+    except (OSError, KeyError, ValueError):
+        pass
+    return None
+
+
+def setup_dist(force_group=False):
     """One process per GPU (torchrun env).  Returns (world, rank, device index).  RCCL ("nccl") by
-    default; LVAE_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on fewer GPUs."""
+    default; LVAE_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on fewer GPUs.
+    force_group: a process group even at world 1 (--sharded-world1: the sharded step through RCCL)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = max(torch.cuda.device_count(), 1)
     dev = local % ndev
-    if world > 1:
+    if force_group and not dist.is_initialized() and "MASTER_ADDR" not in os.environ:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or force_group:
         torch.cuda.set_device(dev)
         backend = os.environ.get("LVAE_DIST_BACKEND", "nccl")
         if backend == "nccl":
@@ -254,11 +282,15 @@ def run_closed(args, world, rank, dev):
     img, mask, X = health_mnist_batch(P, T, seed=100, device=dev)   # the same data set on every rank
     gen = torch.Generator(device=dev).manual_seed(7)
     eps = torch.randn(N, L, device=dev, generator=gen)
-    if world > 1:
-        lo, hi = shard_bounds(N, world, rank)
-        step = LatentShardedClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True)
+    share = args.rank_share if world == 1 else 0
+    if world > 1 or share > 1 or args.sharded_world1:
+        W, r = (world, rank) if world > 1 else (max(share, 1), 0)
+        lo, hi = shard_bounds(N, W, r)
+        step = LatentShardedClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True,
+                                       sim_world=share if share > 1 else None,
+                                       vae_stream_priority=args.vae_stream_priority)
         inputs = (img[lo:hi].contiguous(), mask[lo:hi].contiguous(), X, eps[lo:hi].contiguous())
-        d0, d1 = shard_bounds(L, world, rank)
+        d0, d1 = shard_bounds(L, W, r)
     else:
         step = ClosedStep(vae, kernel, lik, opt, weight=0.15, loss_function="mse", constrain_scales=True,
                           vae_stream_priority=args.vae_stream_priority)
@@ -313,7 +345,12 @@ def run_closed(args, world, rank, dev):
            "config": {"workload": f"closed-form KL step (standard_training, type_KL='closed'): N={N} (P={P} subjects "
                                   f"x T={T}), L={L}, R=5 additive components (config/LVAE_config_sample.txt)",
                       "N": N, "L": L,
-                      "parallelism": (("single GPU, the step replayed as one HIP graph" if use_graph else "single GPU")
+                      "parallelism": (f"rank-share rehearsal on one GPU: rank 0 of {share} ({Lr} dims, {N // share} "
+                                      f"images), collectives replaced by local stand-ins -- NOT the union step"
+                                      if share > 1 else
+                                      "single GPU, LatentShardedClosedStep through a world-1 RCCL group"
+                                      if args.sharded_world1 and world == 1 else
+                                      ("single GPU, the step replayed as one HIP graph" if use_graph else "single GPU")
                                       if world == 1 else
                                       f"latent dims sharded over {world} ranks ({Lr} dims/rank on rank 0), images "
                                       f"split {N // world}/rank, 1 all-gather + 2 all-reduces per step")}}
@@ -335,7 +372,10 @@ def run_closed(args, world, rank, dev):
         # 3 x that in f16 MFMA flop against the dense f16 peak
         flops = Lr * np_ * np_ * (np_ + 1)
         if syrk_ms > 0:
-            ach = X3_PRODUCTS * flops / (syrk_ms * 1e-3) / 1e12
+            ach_ev = X3_PRODUCTS * flops / (syrk_ms * 1e-3) / 1e12
+            prof = kstats_avg_us("syrk_c16_kernel") if (world == 1 and Lr == 16 and np_ == 4096) else None
+            avg_us = prof[0] if prof else syrk_ms * 1e3
+            ach = X3_PRODUCTS * flops / (avg_us * 1e-6) / 1e12
             res["roofline"] = {"kernel": "syrk_c16_kernel<5> (S = K^-1 V K^-1, syrk_x3.hip on the chunk-major core x3_c16.hpp; "
                                          "the largest GPU-time share of the step)",
                                "bound": "mfma", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -343,8 +383,13 @@ def run_closed(args, world, rank, dev):
                                "traffic": pmc_traffic(("syrk_c16_kernel",)) if world == 1 else None,
                                "traffic_source": os.path.basename(PMC_SUMMARY),
                                "algorithmic_flop_per_launch": X3_PRODUCTS * flops,
-                               "fp32_equivalent_tflops": flops / (syrk_ms * 1e-3) / 1e12,
-                               "avg_launch_us": syrk_ms * 1e3,
+                               "fp32_equivalent_tflops": flops / (avg_us * 1e-6) / 1e12,
+                               "avg_launch_us": avg_us,
+                               "avg_launch_source": (f"profiles/{os.path.basename(KSTATS)} (rocprofv3 --kernel-trace "
+                                                     f"--stats of this bench command, {prof[1]} launches)") if prof
+                                                    else "live HIP events (no committed profile for this shape)",
+                               "achieved_event": ach_ev, "frac_event": ach_ev / F16_MFMA_PEAK_TFLOPS,
+                               "avg_launch_us_event": syrk_ms * 1e3,
                                "engine": "f16 MFMA (v_mfma_f32_32x32x16_f16), 3-product split: achieved counts the 3 "
                                          "f16 products per fp32-equivalent product"}
         # secondary: the trailing rank-256 update of the Cholesky (U2, HBM-streaming); per step the passes
@@ -378,7 +423,7 @@ def run_closed(args, world, rank, dev):
 def run_hensman(args, world, rank, dev):
     import lvae_amd as la
     from lvae_amd.data import health_mnist_batch
-    from lvae_amd.samplers import hensman_batches, SubjectSampler
+    from lvae_amd.samplers import check_same_permutation, hensman_batches, SubjectSampler
     from lvae_amd.steps import GraphedStep, HensmanStep
     from lvae_amd.vae import ConvVAE
 
@@ -405,6 +450,8 @@ def run_hensman(args, world, rank, dev):
     step = HensmanStep(vae, k0, k1, lik, opt, m, H, z, P, T, weight=0.15, natural_gradient=True,
                        natural_gradient_lr=0.01, world=world, grad_hook=hook, ng_reduce=ngr)
     perm = SubjectSampler(P, T, seed=0).permutation()
+    if world > 1:
+        check_same_permutation(perm)  # once per run (a collective)
     batches = [b.to(dev) for b in hensman_batches(perm, P_b, T, rank, world) if b is not None and len(b) == P_b * T]
     gen = torch.Generator(device=dev).manual_seed(7 + rank)
     eps = torch.randn(P_b * T, L, device=dev, generator=gen)
@@ -459,6 +506,13 @@ def torch_gram_f32(params, X):
 
 
 def run_c2(dev, reps=20):
+    """BASELINE configs[1]: the product's Gram + blocked Cholesky route (lvae_gram_f32 +
+    lvae_spd_inv_chol_f32: potrf, trtri, lauum -- the inverse KL_closed uses, elbo_functions.py:26-29)
+    against PyTorch-ROCm fp32 Gram + torch.linalg.cholesky (rocSOLVER potrf) and + cholesky_inverse.
+    gp_cholesky_gflops_hip is the potrf phase ALONE (the library's HIP events around its potrf
+    sequence, LVAE_PH_POTRF), against torch.linalg.cholesky alone; the whole inverse is compared with
+    cholesky + cholesky_inverse.  The retired Gauss-Jordan sweep (lvae_spd_sweep_f32) is kept as a
+    labelled extra."""
     import lvae_amd as la
     from lvae_amd import _lib
     from lvae_amd.data import health_mnist_covariates
@@ -472,21 +526,32 @@ def run_c2(dev, reps=20):
     np_ = lib.lvae_kl_closed_padded_n(N)
     A = torch.empty(L, np_, np_, dtype=torch.float32, device=dev)
     Kinv = torch.empty_like(A)
-    scr = torch.empty(int(lib.lvae_spd_sweep_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
+    scr = torch.empty(int(lib.lvae_spd_inv_chol_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
+    sscr = torch.empty(int(lib.lvae_spd_sweep_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
     logdet = torch.empty(L, dtype=torch.float64, device=dev)
     info = torch.empty(L, dtype=torch.int32, device=dev)
     noise = torch.ones(L, dtype=torch.float64, device=dev)
     xv = _lib.xview(X, 0, 0)
 
-    def hip():
+    def gram():
         _lib.check(lib.lvae_gram_f32(spec, xv, xv, 1, L, N, N, _lib.ptr(params), _lib.ptr(noise), _lib.ptr(A), 0,
                                      np_ * np_, np_, _lib.stream_ptr()), "gram")
-        _lib.check(lib.lvae_spd_sweep_f32(np_, L, _lib.ptr(A), _lib.ptr(scr), _lib.ptr(Kinv), _lib.ptr(logdet),
+
+    def hip():
+        gram()
+        _lib.check(lib.lvae_spd_inv_chol_f32(np_, L, _lib.ptr(A), _lib.ptr(scr), _lib.ptr(Kinv), _lib.ptr(logdet),
+                                             _lib.ptr(info), _lib.stream_ptr()), "chol")
+
+    def hip_sweep():
+        gram()
+        _lib.check(lib.lvae_spd_sweep_f32(np_, L, _lib.ptr(A), _lib.ptr(sscr), _lib.ptr(Kinv), _lib.ptr(logdet),
                                           _lib.ptr(info), _lib.stream_ptr()), "sweep")
 
     def torch_chol():
-        Lc = torch.linalg.cholesky(torch_gram_f32(params, X))
-        return Lc
+        return torch.linalg.cholesky(torch_gram_f32(params, X))
+
+    def torch_potrf_only(Kt):
+        return torch.linalg.cholesky(Kt)
 
     def torch_chol_inv():
         Lc = torch_chol()
@@ -504,20 +569,47 @@ def run_c2(dev, reps=20):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
 
-    t_hip, t_chol, t_inv = timed(hip), timed(torch_chol), timed(torch_chol_inv)
+    # the potrf phase of the product route alone (HIP events around the library's potrf sequence)
+    for _ in range(3):
+        hip()
+    torch.cuda.synchronize()
+    _lib.prof_enable(True)
+    _lib.prof_collect()
+    for _ in range(reps):
+        hip()
+    ph = _lib.prof_collect()
+    _lib.prof_enable(False)
+    t_potrf = ph["potrf"][0] / max(ph["potrf"][1], 1)
+    t_hip = timed(hip)
+    info_ok = int(info.abs().sum()) == 0
+    inv_chol = Kinv[:, :N, :N].clone()
+    ld_chol = logdet.clone()
+    Kt = torch_gram_f32(params, X)
+    t_gram_torch = timed(lambda: torch_gram_f32(params, X))
+    t_potrf_torch = timed(lambda: torch_potrf_only(Kt))
+    t_chol, t_inv = timed(torch_chol), timed(torch_chol_inv)
+    t_sweep = timed(hip_sweep)
     ref_inv, ref_ld = torch_chol_inv()
-    err = float((Kinv[:, :N, :N] - ref_inv).abs().max() / ref_inv.abs().max())
+    err = float((inv_chol - ref_inv).abs().max() / ref_inv.abs().max())
     flop = L * N ** 3 / 3
     return {"config": f"N={N} (P={P} x T={T}), L={L}, sample-config kernel, fp32",
-            "hip_gram_sweep_inverse_ms": t_hip, "torch_gram_cholesky_ms": t_chol,
-            "torch_gram_cholesky_inverse_ms": t_inv,
-            "speedup_vs_torch_cholesky": t_chol / t_hip, "speedup_vs_torch_cholesky_inverse": t_inv / t_hip,
-            "gp_cholesky_gflops_hip": flop / (t_hip * 1e-3) / 1e9,
-            "gp_cholesky_gflops_torch": flop / (t_chol * 1e-3) / 1e9,
-            "hip_vs_torch_inverse_max_rel_diff": err,
-            "logdet_max_rel_diff": float(((logdet.float() - ref_ld).abs() / ref_ld.abs()).max()),
-            "note": "HIP: lvae_gram_f32 + lvae_spd_sweep_f32 (K^-1 and log|K|); torch: PyTorch fp32 Gram + "
-                    "torch.linalg.cholesky (rocSOLVER) [+ cholesky_inverse + log-det for the same outputs]"}
+            "hip_route": "lvae_gram_f32 + lvae_spd_inv_chol_f32 (blocked potrf + trtri + lauum, chol_inv.hip)",
+            "hip_gram_chol_inverse_ms": t_hip, "hip_potrf_ms": t_potrf,
+            "torch_gram_ms": t_gram_torch, "torch_potrf_ms": t_potrf_torch,
+            "torch_gram_cholesky_ms": t_chol, "torch_gram_cholesky_inverse_ms": t_inv,
+            "speedup_potrf_vs_torch_cholesky": t_potrf_torch / t_potrf if t_potrf > 0 else None,
+            "speedup_vs_torch_cholesky_inverse": t_inv / t_hip,
+            "gp_cholesky_gflops_hip": flop / (t_potrf * 1e-3) / 1e9 if t_potrf > 0 else None,
+            "gp_cholesky_gflops_torch": flop / (t_potrf_torch * 1e-3) / 1e9,
+            "gp_cholesky_gflops_basis": "L*N^3/3 / potrf time alone (HIP: the library's potrf phase events; "
+                                        "torch: torch.linalg.cholesky on the prebuilt fp32 Gram)",
+            "hip_vs_torch_inverse_max_rel_diff": err, "hip_info_ok": info_ok,
+            "logdet_max_rel_diff": float(((ld_chol.float() - ref_ld).abs() / ref_ld.abs()).max()),
+            "extra_retired_sweep": {"hip_gram_sweep_inverse_ms": t_sweep,
+                                    "note": "lvae_spd_sweep_f32, the rounds 1-2 block Gauss-Jordan inverse; the KL "
+                                            "no longer uses it"},
+            "note": "HIP: Gram + Cholesky route (K^-1 and log|K|); torch: PyTorch fp32 Gram + torch.linalg.cholesky "
+                    "(rocSOLVER) [+ cholesky_inverse + log-det for the same outputs]"}
 
 
 def main():
@@ -537,11 +629,17 @@ def main():
     ap.add_argument("--no-c2", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="closed regime on one GPU: time the step as one replayed HIP graph (slower, see run_closed)")
+    ap.add_argument("--sharded-world1", dest="sharded_world1", action="store_true",
+                    help="one GPU: the latent-sharded step (distributed.LatentShardedClosedStep) through a world-1 "
+                         "RCCL group instead of ClosedStep (its overlap against the single-GPU step's)")
+    ap.add_argument("--rank-share", dest="rank_share", type=int, default=0,
+                    help="one GPU: time rank 0's share of a W-rank latent-sharded step (L/W dims, N/W images; "
+                         "collectives replaced by local stand-ins) -- the per-rank compute of the W-GPU line")
     ap.add_argument("--vae-stream-priority", dest="vae_stream_priority", type=int, default=-1,
                     help="priority of the ConvVAE's stream in the closed step (lower = higher; 0 = default)")
     args = ap.parse_args()
 
-    world, rank, local = setup_dist()
+    world, rank, local = setup_dist(force_group=args.sharded_world1)
     dev = torch.device("cuda", local)
     res = None
     if args.regime in ("both", "closed"):
@@ -568,7 +666,7 @@ def main():
                 if "regime_a" not in res:
                     res["vs_cpu_baseline"] = ra["vs_cpu_baseline"]
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

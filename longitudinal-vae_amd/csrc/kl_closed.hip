@@ -313,6 +313,10 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
     if (!ok(hipStreamWaitEvent(sd->s, sd->rbx, 0))) return LVAE_ERR_LAUNCH;
     LVAE_TRY(kl_resid_bins_plan(spec, x, ldx, n, np_, L, ws.rb, sd->s));
     if (!ok(hipEventRecord(sd->rb, sd->s))) return LVAE_ERR_LAUNCH;
+    // join the side stream back before returning (the header's contract): the wait sits behind the
+    // trtri launches already on `st`, so the plan still runs beside them; each call is self-contained
+    // (separate graph captures, a caller that syncs `st` and frees the workspace after the factor)
+    if (!ok(hipStreamWaitEvent(st, sd->rb, 0))) return LVAE_ERR_LAUNCH;
   }
   LVAE_CHECK_LAUNCH();
   return 0;
@@ -340,13 +344,7 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
   LVAE_TRY(ci_lauum_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.mu, ws.sv, ws.apart, need_bwd ? ws.Bp : nullptr,
                         ws.bsc, st));
   kl_alpha0_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.apart, ws.Kinv, np_, ws.alpha, ws.kdiag);
-  const bool rb_on = kl_resid_bins_enabled(spec, n);
-  if (rb_on) {  // the plan enqueued by the factor call
-    std::lock_guard<std::recursive_mutex> lock(side_mutex());
-    SideStream* sd = nullptr;
-    LVAE_TRY(side_stream(sd));
-    if (hipStreamWaitEvent(st, sd->rb, 0) != hipSuccess) return LVAE_ERR_LAUNCH;
-  }
+  const bool rb_on = kl_resid_bins_enabled(spec, n);  // (the plan: the factor call's, joined on `st`)
   LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res,
                          rb_on ? ws.rb : nullptr, st));
   {  // alpha = a0 + K^-1 r over the lower tiles of K^-1 (the residual's partials buffer is free again)

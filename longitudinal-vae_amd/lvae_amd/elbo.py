@@ -54,7 +54,9 @@ def check_pending(pend=None):
 class KLFactor:
     """K^-1 and log|K| of the L covariances, computed ahead of (mu, logvar) on a caller stream
     (lvae_kl_closed_factor_f32): kl_closed_prefactor launches it, KL_closed_batched(..., factor=)
-    waits for it and finishes with lvae_kl_closed_reduce_f32."""
+    waits for it and finishes with lvae_kl_closed_reduce_f32.  Single use: the reduce writes the B
+    planes over the factor's Gram buffer and the backward writes S over its Y^T planes, so a second
+    KL_closed_batched(..., factor=) on the same factor would read overwritten operands -- it raises."""
 
     def __init__(self, spec, params, noise, x, stream):
         lib = _lib.lib()
@@ -76,6 +78,7 @@ class KLFactor:
             _lib.check(rc, "kl_closed_factor")
         self.stream = stream
         self.n, self.L = n, L
+        self.consumed = False
 
     def join(self):
         """Make the current stream wait for the factorisation (and own its buffers)."""
@@ -118,6 +121,9 @@ class _KLHyperFn(torch.autograd.Function):
     def backward(ctx, gkl):
         lib = _lib.lib()
         st = ctx.state
+        if st.ws is None:
+            raise RuntimeError("KL_closed: the hyper-parameter backward ran twice (its workspace is released "
+                               "after the first; use retain_graph only for the (mu, logvar) half)")
         g = gkl.detach().to(torch.float64).reshape(st.L).contiguous()
         dp = torch.empty_like(st.p)
         dnz = torch.empty(st.L, dtype=torch.float64, device=st.p.device)
@@ -125,6 +131,9 @@ class _KLHyperFn(torch.autograd.Function):
                                               _lib.ptr(g), _lib.ptr(dp), _lib.ptr(dnz), _lib.ptr(st.ws),
                                               _lib.stream_ptr())
         _lib.check(rc, "kl_closed_bwd_hyper")
+        # the backward consumed the workspace (S over the Y^T planes): release it now rather than with the
+        # graph (GBs at the headline shape); the stream order keeps it alive for the kernels just queued
+        st.ws = st.p = st.x64 = None
         pd, nd, nshape = ctx.in_dtypes
         return dp.to(pd), dnz.to(nd).reshape(nshape), None, None
 
@@ -213,6 +222,10 @@ def KL_closed_batched(covar_modules, train_x, likelihoods, mu, log_var, factor=N
     inverse were launched ahead (its hyperparameters are the ones differentiated)."""
     L = mu.shape[1]
     if factor is not None:
+        if factor.consumed:
+            raise RuntimeError("KL_closed_batched: this KLFactor was already used (one reduce per factor: "
+                               "launch a new kl_closed_prefactor for each step)")
+        factor.consumed = True
         return _kl_closed_apply(factor.params, factor.noise, mu, log_var, train_x, factor.spec, factor)
     spec, params = _stack_modules(covar_modules)
     if params.shape[0] != L:

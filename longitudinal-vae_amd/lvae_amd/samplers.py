@@ -44,10 +44,11 @@ def subject_rows(subjects, T):
     return (s[:, None] * T + torch.arange(T, dtype=torch.int64, device=s.device)[None, :]).reshape(-1)
 
 
-def _check_same_permutation(perm, group=None):
+def check_same_permutation(perm, group=None):
     """Raise if the ranks of an initialised process group hold different subject orders (a sampler
     built without a seed draws from each process's own NumPy global state): one MIN / MAX all-reduce
-    of a checksum of the order."""
+    of a checksum of the order.  A collective: every rank of the group calls it, once per run (the
+    distributed drivers do, right after building the sampler), not per epoch."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
@@ -62,14 +63,15 @@ def _check_same_permutation(perm, group=None):
                          "with the same explicit seed on every rank (or broadcast rank 0's permutation)")
 
 
-def hensman_batches(perm, P_b, T, rank=0, world=1, check=True, group=None):
+def hensman_batches(perm, P_b, T, rank=0, world=1, check=False, group=None):
     """Batches of one epoch for one rank: the global batch of world*P_b consecutive subjects of the
     permutation is split into contiguous per-rank slices of P_b subjects (the last global batch may be
-    short, as with drop_last=False; ranks whose slice is empty get no batch in that step).  With
-    world > 1 inside an initialised process group (and check=True) the ranks' orders are compared
-    first: different orders would silently give overlapping / missing subjects."""
+    short, as with drop_last=False; ranks whose slice is empty get no batch in that step).  A pure index
+    utility by default; check=True (world > 1, inside an initialised process group) first compares the
+    ranks' orders with check_same_permutation -- a collective every rank must reach -- since different
+    orders would silently give overlapping / missing subjects."""
     if world > 1 and check:
-        _check_same_permutation(perm, group)
+        check_same_permutation(perm, group)
     perm = np.asarray(perm)
     G = world * P_b
     out = []

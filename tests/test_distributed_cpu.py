@@ -70,10 +70,11 @@ def _worker(rank, world, port, q):
         # --- hensman_batches refuses per-rank subject orders that differ ---
         from lvae_amd.samplers import SubjectSampler, hensman_batches
         same = SubjectSampler(P_tot, T, seed=4).permutation()
-        hensman_batches(same, P_b, T, rank, world)  # agreeing orders pass
+        hensman_batches(same, P_b, T, rank, world, check=True)  # agreeing orders pass
+        hensman_batches(SubjectSampler(P_tot, T, seed=100 + rank).permutation(), P_b, T, rank, world)  # no collective
         own = SubjectSampler(P_tot, T, seed=100 + rank).permutation()
         try:
-            hensman_batches(own, P_b, T, rank, world)
+            hensman_batches(own, P_b, T, rank, world, check=True)
             q.put(("perm", rank, False))
         except ValueError:
             q.put(("perm", rank, True))
