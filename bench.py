@@ -613,6 +613,10 @@ def run_c2(dev, reps=20):
 
 
 def main():
+    # ONE JSON line on stdout: libraries that print there (RCCL's version banner at communicator init,
+    # MIOpen notes) write to stderr instead -- fd 1 is pointed at fd 2 and the line goes to the saved fd
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -665,7 +669,7 @@ def main():
                 ra["vs_cpu_baseline"] = ra["value"] / cb["value"]
                 if "regime_a" not in res:
                     res["vs_cpu_baseline"] = ra["vs_cpu_baseline"]
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -45,12 +45,50 @@
 #ifndef LVAE_CI_C16
 #define LVAE_CI_C16 1
 #endif
+// the pivot's pending update (dev A/B switches): skip the zero half of Y_kk in X = C Y_kk^T, and load X's
+// planes once for X X^T
+#ifndef LVAE_PV_BTRI
+#define LVAE_PV_BTRI 1
+#endif
+#ifndef LVAE_PV_SAMEAB
+#define LVAE_PV_SAMEAB 1
+#endif
 
 namespace lvae {
 
 // the trtri / lauum planes (Y, Y^T, X^T) in the chunk-major layout and their GEMMs on the c16 core
 // (x3_c16.hpp: a 4-stage ring, 128 KB of LDS beside the epilogues' own); 0: row-major planes on x3_dma.hpp
 constexpr bool kCiC16 = LVAE_CI_C16 != 0;
+
+// Few latent dims per call (a sharded rank: L <= kCiPipeMaxL): trtri runs PIPELINED with potrf, by block
+// rows, on the caller's stream between the passes (the GPU is mostly idle beside the pivot chain there):
+// once pivot(m) has Y_mm and panel(m) column m of L,
+//   rowY(m)   Y_mj = -Y_mm X_mj for j < m (+ the diagonal Y^T tile from D)   X_mj = sum_{k=j}^{m-1} L_mk Y_kj
+//   Xupd(m)   X_ij += L_im Y_mj for i > m, j <= m (fp32 in the Kinv buffer; row m+1, complete now, as the
+//             split X^T planes rowY(m+1) reads)
+// so that after the last pivot only rowY(nt-1) is left of trtri (recursive doubling: 2 log2(nt) launches
+// of under-filled tiles after potrf).  Same flops; the Y planes (row-major Y, read only by the doubling's
+// Y step) are not produced.
+#ifndef LVAE_CI_PIPE_MAX_L
+#define LVAE_CI_PIPE_MAX_L 4
+#endif
+// the latent-dim bound of the pipelined schedule: LVAE_CI_PIPE_L overrides it for A/B runs (read once per
+// process, so the workspace size query and the calls agree)
+inline int ci_pipe_max_l() {
+  static const int v = getenv("LVAE_CI_PIPE_L") ? atoi(getenv("LVAE_CI_PIPE_L")) : LVAE_CI_PIPE_MAX_L;
+  return v;
+}
+inline bool ci_pipe_alloc(int np_, int L) { return L <= ci_pipe_max_l() && L <= 16 && np_ >= 512; }  // (16: kCiFuseMaxL)
+// 0: recursive-doubling trtri after potrf; 1: pipelined trtri; 2: pipelined trtri + lauum (K^-1 accumulated
+// as the rows of Y arrive: Lupd(m), K^-1_IJ += Y_mI^T Y_mJ for J <= I <= m, fp32 in the Kinv buffer, whose
+// tiles of rows <= m the pipelined X no longer uses; the reduce's lauum is then its epilogue alone).
+// LVAE_CI_PIPE=0 / LVAE_CI_PIPE_LAUUM=0 switch the stages off (A/B runs; read once per process).
+inline int ci_pipe_mode(int np_, int L) {
+  static const bool on = !getenv("LVAE_CI_PIPE") || atoi(getenv("LVAE_CI_PIPE")) != 0;
+  static const bool lau = !getenv("LVAE_CI_PIPE_LAUUM") || atoi(getenv("LVAE_CI_PIPE_LAUUM")) != 0;
+  if (!on || !ci_pipe_alloc(np_, L)) return 0;
+  return lau ? 2 : 1;
+}
 
 struct CiScratch {
   _Float16 *Ch[2], *Cl[2];  // [L][np][256] planes of the updated column (pass k's C operand), by parity
@@ -61,6 +99,8 @@ struct CiScratch {
   float* lsc;               // [L][nt][nt] (l, i, k): tile (i, k) of L
   float* ysc;               // [L][nt][nt] (l, i, j): tile (i, j) of Y (both plane orientations; D for i == j)
   float* xsc;               // [L][nt][nt] (l, i, j): tile (i, j) of the trtri intermediate X
+  _Float16 *XRh[2], *XRl[2];  // pipelined trtri: the X^T tiles (j, m) of row block m, [L][nt][256 x 256] (one
+                              // chunk-major tile each), by row parity; nullptr unless ci_pipe_alloc
   int nt;
   size_t bytes;
   CiScratch(char* base, int np_, int L) {
@@ -87,6 +127,10 @@ struct CiScratch {
     lsc = (float*)take((size_t)L * nt * nt * 4);
     ysc = (float*)take((size_t)L * nt * nt * 4);
     xsc = (float*)take((size_t)L * nt * nt * 4);
+    for (int b = 0; b < 2; ++b) {
+      XRh[b] = ci_pipe_alloc(np_, L) ? (_Float16*)take(col * 2) : nullptr;
+      XRl[b] = ci_pipe_alloc(np_, L) ? (_Float16*)take(col * 2) : nullptr;
+    }
     bytes = off;
   }
   __device__ float& c_scale(int l, int k, int i) const { return csc[((int64_t)l * nt + k) * nt + i]; }
@@ -115,7 +159,7 @@ __device__ inline void ci_pending_update(const float* __restrict__ T, int64_t np
     pv_f32x16 x[4];
 #pragma unroll
     for (int h = 0; h < 4; ++h) x[h] = pv_f32x16{};
-    pv_x3_gemm<4, false>(src, lf, bi, bj, x);
+    pv_x3_gemm<4, false, false, LVAE_PV_BTRI != 0>(src, lf, bi, bj, x);  // (D = Y_kk: lower triangular)
     const float inv = 1.0f / (S.c_scale(l, kp, kb) * S.ysc[((int64_t)l * S.nt + kp) * S.nt + kp]);
     float m = 0.f;
 #pragma unroll
@@ -156,7 +200,7 @@ __device__ inline void ci_pending_update(const float* __restrict__ T, int64_t np
   pv_f32x16 acc[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
-  pv_x3_gemm<3, true>(src, lf, bi, bj, acc);
+  pv_x3_gemm<3, true, LVAE_PV_SAMEAB != 0>(src, lf, bi, bj, acc);  // (X X^T: X's planes loaded once)
   const float inv = 1.0f / (sx * sx);
   float old[3][16];
 #pragma unroll
@@ -644,6 +688,16 @@ __global__ __launch_bounds__(256) void ci_diag_copy_kernel(CiScratch S, int np_,
 // (workgroups with i >= nt exit at once); lauum the L nt (nt + 1) / 2 lower tiles.
 // ------------------------------------------------------------------------------------------
 constexpr int kCiX = 0, kCiY = 1, kCiLauum = 2, kCiLauumKL = 3;
+// pipelined trtri (ci_pipe_alloc; h = the pass m):
+//   kCiTrY  rowY(m): tile j < m: Y_mj = -Y_mm X_mj   A = D_m (row-major planes), B = the X^T row planes (j)
+//                    of parity m & 1 -> Y^T planes tile (j, m) (transposed out), scale ysc(m, j); workgroups
+//                    t >= m: the 16 64 x 64 pieces of Y^T (m, m) = D_m^T
+//   kCiTrX  Xupd(m): tile (i, j), i > m, j <= m: X_ij (+)= L_im Y_mj   A = L planes (i, m), B = Y^T planes
+//                    (j, m) -> fp32 X in g.Kinv (written at j == m, accumulated after), or for i == m + 1 (its
+//                    last term) the X^T row planes of parity (m + 1) & 1, scale xsc(m + 1, j); workgroups
+//                    t >= g.inst0 (mode 2): Lupd(m), tile (I, J), J <= I <= m: K^-1_IJ (+)= Y_mI^T Y_mJ
+//                    (A, B = Y^T planes (I, m), (J, m); written at m == I) into g.Kinv
+constexpr int kCiTrY = 4, kCiTrX = 5;
 #ifndef LVAE_KL_MIRROR
 #define LVAE_KL_MIRROR 0  // 1: the KL lauum also writes the upper tiles of K^-1 (no reader needs them)
 #endif
@@ -652,7 +706,7 @@ struct CiGemmArgs {
   _Float16 *oh, *ol, *oth, *otl;      // outputs: row-major planes (kCiY), transposed planes (kCiX, kCiY)
   float* Kinv;                         // kCiLauum(KL)
   int np_, nt, h, per_dim, nwg;        // per_dim: workgroups per latent dim
-  int inst0;                           // trtri: first recursive-doubling instance of the launch
+  int inst0;                           // trtri: first recursive-doubling instance; kCiTrX: its X tiles per dim
   // kCiLauumKL (the exact KL's reduce, kl_closed.hip): mu [L, np] fp64 and sqrt v [L, np] in; out the
   // partials of K^-1 mu, apart[l][s][p] = sum over column block s of Kinv(p, .) mu (every (s, p) once),
   // and -- if bh -- the fp16 hi / lo planes of B = K^-1 diag(sqrt v) (row stride np) split with the
@@ -662,6 +716,7 @@ struct CiGemmArgs {
   float* apart;
   _Float16 *bh_out, *bl_out;
   float* bsc;
+  int pre = 0;  // kCiLauum(KL): K^-1's lower tiles are in Kinv already (pipelined lauum): epilogue only
 };
 
 // one halving butterfly step over lane bit D (D <= 16): the lane keeps the half of its N partial sums
@@ -728,6 +783,37 @@ __device__ inline void ci_kl_partials(const sx_f32x16 (&acc)[4][2], float inv, c
   }
 }
 
+// Y^T (k, k) = D_k^T, 64 x 64 piece (pa, pb) of D_k -> block (pb, pa) of tile (k, k) of the chunk-major Y^T
+// planes, through tp (2 x 64 x 66 halves of LDS); any block size.  Ends with the writes (no barrier).
+__device__ inline void ci_diag_t_piece(const CiScratch& S, int np_, int l, int k, int pa, int pb,
+                                       _Float16* __restrict__ YTh, _Float16* __restrict__ YTl, _Float16* tp) {
+  const int t = threadIdx.x, nth = blockDim.x;
+  const int64_t od = ((int64_t)l * S.nt + k) * kSwBB + (int64_t)(64 * pa) * kSwB + 64 * pb;
+  for (int e = t; e < 64 * 8; e += nth) {
+    const int r = e >> 3, c = (e & 7) * 8;
+    const x3_half8 h = *reinterpret_cast<const x3_half8*>(S.Dh + od + r * kSwB + c);
+    const x3_half8 lo = *reinterpret_cast<const x3_half8*>(S.Dl + od + r * kSwB + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      tp[r * 66 + c + q] = h[q];
+      tp[64 * 66 + r * 66 + c + q] = lo[q];
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * 8; e += nth) {
+    const int c = e >> 3, r0 = (e & 7) * 8;
+    x3_half8 h, lo;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      h[q] = tp[(r0 + q) * 66 + c];
+      lo[q] = tp[64 * 66 + (r0 + q) * 66 + c];
+    }
+    const int64_t o = c16_off(l, np_, k * kSwB + 64 * pb + c, k * kSwB + 64 * pa + r0);
+    *reinterpret_cast<x3_half8*>(YTh + o) = h;
+    *reinterpret_cast<x3_half8*>(YTl + o) = lo;
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
@@ -745,6 +831,25 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     sx_tri_blocked(wgid % g.per_dim, nt, i, j);
     kb0 = i;
     kb1 = nt;
+  } else if constexpr (MODE == kCiTrY || MODE == kCiTrX) {
+    // dims interleaved (block b: dim b % L): the first L (m + 1) workgroups of Xupd are row m + 1's tiles
+    const int L = g.nwg / g.per_dim, t = blockIdx.x / L, m = g.h;
+    l = blockIdx.x % L;
+    if constexpr (MODE == kCiTrY) {
+      i = m;
+      j = t;
+      if (t >= m) {  // (uniform) a piece of the diagonal tile
+        ci_diag_t_piece(S, np_, l, m, (t - m) >> 2, (t - m) & 3, g.oth, g.otl, lds);
+        return;
+      }
+    } else if (t < g.inst0) {
+      i = m + 1 + t / (m + 1);
+      j = t % (m + 1);
+    } else {
+      sx_tri(t - g.inst0, i, j);  // Lupd tile (i, j), j <= i <= m
+    }
+    kb0 = m;
+    kb1 = m + 1;
   } else {
     // longest K first over the whole launch (the tiles of a level span K = 1 .. h blocks): block b
     // takes latent dim b % L (an XCD then keeps the dims b % 8 selects, and their panels) and the
@@ -781,6 +886,13 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     } else if constexpr (MODE == kCiY) {
       sa = S.ysc[sl + (int64_t)i * nt + kb];
       sb = S.xsc[sl + (int64_t)kb * nt + j];
+    } else if constexpr (MODE == kCiTrY) {  // (kb = m = i)
+      sa = S.ysc[sl + (int64_t)i * nt + i];
+      sb = S.xsc[sl + (int64_t)i * nt + j];
+    } else if constexpr (MODE == kCiTrX) {  // (kb = m)
+      sa = (int)(blockIdx.x / (g.nwg / g.per_dim)) < g.inst0 ? S.lsc[sl + (int64_t)i * nt + kb]
+                                                            : S.ysc[sl + (int64_t)kb * nt + i];
+      sb = S.ysc[sl + (int64_t)kb * nt + j];
     } else {
       sa = S.ysc[sl + (int64_t)kb * nt + i];
       sb = S.ysc[sl + (int64_t)kb * nt + j];
@@ -810,16 +922,91 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
   if constexpr (kCiC16) {
     // operands: A = L planes (row-major) for X, else chunk-major panels from block kb0 on; B chunk-major
     const int64_t kc0 = (int64_t)kb0 * (kSwB / kC16BK) * kC16Part;
-    const C16Opnd A = MODE == kCiX ? C16Opnd{ah, g.al - g.ah, np_}
-                                   : C16Opnd{g.ah + c16_panel(l, np_, i) + kc0, g.al - g.ah, 0};
-    const C16Opnd B{g.bh + c16_panel(l, np_, j) + kc0, g.bl - g.bh, 0};
-    C16BlockRescale rs{sprod, 1.f};
-    c16_gemm<4>(A, B, nkb * (kSwB / kC16BK), lds, acc, rs);
-    inv = 1.0f / rs.scur;
+    C16Opnd A = MODE == kCiX || MODE == kCiTrX ? C16Opnd{ah, g.al - g.ah, np_}
+                                               : C16Opnd{g.ah + c16_panel(l, np_, i) + kc0, g.al - g.ah, 0};
+    C16Opnd B{g.bh + c16_panel(l, np_, j) + kc0, g.bl - g.bh, 0};
+    if constexpr (MODE == kCiTrX) {
+      if ((int)(blockIdx.x / (g.nwg / g.per_dim)) >= g.inst0)  // Lupd: A = Y^T planes (i, m)
+        A = C16Opnd{g.bh + c16_panel(l, np_, i) + kc0, g.bl - g.bh, 0};
+    }
+    if constexpr (MODE == kCiTrY) {  // A = D_m (row-major, stride 256), B = X^T row tile j (one chunk-major tile)
+      const int64_t od = ((int64_t)l * nt + i) * kSwBB, ox = ((int64_t)l * nt + j) * kSwBB;
+      A = C16Opnd{S.Dh + od, S.Dl - S.Dh, kSwB};
+      B = C16Opnd{S.XRh[i & 1] + ox, S.XRl[i & 1] - S.XRh[i & 1], 0};
+    }
+    if ((MODE == kCiLauum || MODE == kCiLauumKL) && g.pre) {  // (uniform) K^-1 tile from the pipelined lauum
+      const float* T = g.Kinv + l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;
+      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T), (short)0, 0x7fffffff,
+                                                                          0x00020000);
+      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+      const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rt, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0));
+      __syncthreads();  // (kl_mu / kl_sv written above)
+      inv = 1.f;
+    } else {
+      C16BlockRescale rs{sprod, 1.f};
+      c16_gemm<4>(A, B, nkb * (kSwB / kC16BK), lds, acc, rs);
+      inv = 1.0f / rs.scur;
+    }
   } else {
     inv = 1.0f / sx_gemm_scaled(ah, al, bh, bl, np_, nkb, sprod, lds, acc);
   }
-  if constexpr (MODE == kCiX) {
+  if constexpr (MODE == kCiTrY) {
+    const float sy = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
+    ci_transposed_out(acc, -inv, lds, [&](int c, int r0, f32x4 v) {
+      const int64_t o = c16_off(l, np_, j * kSwB + c, i * kSwB + r0);  // Y^T tile (j, m)
+      ci_split4(v, sy, g.oth + o, g.otl + o);
+    });
+    if (threadIdx.x == 0) S.ysc[sl + (int64_t)i * nt + j] = sy;
+  } else if constexpr (MODE == kCiTrX) {
+    const int m = g.h;
+    const bool lup = (int)(blockIdx.x / (g.nwg / g.per_dim)) >= g.inst0;
+    float* Xt = g.Kinv + l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;  // fp32 X / K^-1 tile (i, j)
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(Xt, (short)0, 0x7fffffff, 0x00020000);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] *= inv;
+    if (lup ? i < m : j < m) {  // (uniform) the terms so far: X k = j .. m-1, K^-1 k = i .. m-1
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b][e] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rx, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0));
+    }
+    if (!lup && i == m + 1) {  // X_{m+1, j} complete: the split X^T planes of the next rowY
+      const float sx = x3_scale(sw_block_max(ci_acc_absmax(acc), &red));
+      const int64_t ox = ((int64_t)l * nt + j) * kSwBB;
+      _Float16* xh = S.XRh[(m + 1) & 1] + ox;
+      _Float16* xl = S.XRl[(m + 1) & 1] + ox;
+      ci_transposed_out(acc, 1.f, lds, [&](int c, int r0, f32x4 v) {
+        const int64_t o = c16_off(0, kSwB, c, r0);
+        ci_split4(v, sx, xh + o, xl + o);
+      });
+      if (threadIdx.x == 0) S.xsc[sl + (int64_t)i * nt + j] = sx;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e]), rx, vo,
+                                                  ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+    }
+  } else if constexpr (MODE == kCiX) {
     const float sx = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
     const int64_t ot = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // X^T tile (j, i)
     ci_transposed_out(acc, inv, lds, [&](int c, int r0, f32x4 v) {
@@ -856,14 +1043,16 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(O, (short)0, 0x7fffffff, 0x00020000);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+    if (!g.pre) {  // (pipelined lauum: the lower tile is already there)
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int e = 0; e < 16; ++e)
+        for (int e = 0; e < 16; ++e)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * osc), ro, vo,
-                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+          for (int b = 0; b < 2; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * osc), ro, vo,
+                                                  ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+    }
     if constexpr (MODE == kCiLauumKL) {
       ci_kl_partials(acc, 1.f, g, l, i, j, kl_mu, kl_part);
       const int64_t tb = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;   // B tile (i, j)
@@ -956,6 +1145,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
   _Float16* XTh = reinterpret_cast<_Float16*>(Kinv);  // Kinv is written last (lauum): the X^T planes until then
   _Float16* XTl = XTh + full;
   auto ok = [](hipError_t e) { return e == hipSuccess; };
+  bool pipe = false;
   {
     ProfScope ps(LVAE_PH_POTRF, st);
     std::lock_guard<std::recursive_mutex> lock(side_mutex());
@@ -965,6 +1155,8 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
     if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
     const bool fuse = L <= kCiFuseMaxL;
+    const int pmode = ci_pipe_mode(np_, L);  // (implies fuse and the XR planes)
+    pipe = pmode > 0;
     if (fuse) {
       ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, g_pivot_prof);
       if (!ok(hipEventRecord(sd->piv[0], sd->s))) return LVAE_ERR_LAUNCH;
@@ -986,6 +1178,20 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
             ci_update_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
           }
           if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
+        }
+        if (pipe) {  // trtri by block rows beside the chain (after U2(m): off pivot(m+2)'s path)
+          ProfScope pt(LVAE_PH_POTRI, st);
+          const int pery = m + 16;
+          CiGemmArgs gy{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, YTh, YTl, nullptr, np_, nt, m, pery,
+                        pery * L, 0};
+          ci_gemm_kernel<kCiTrY><<<pery * L, 512, 0, st>>>(gy, S);
+          // Xupd(m) (+ Lupd(m) in mode 2), one launch
+          const int perx = (nt - m - 1) * (m + 1), perl = pmode == 2 ? (m + 1) * (m + 2) / 2 : 0;
+          if (perx + perl > 0) {
+            CiGemmArgs gx{S.Lh, S.Ll, YTh, YTl, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, m, perx + perl,
+                          (perx + perl) * L, perx};
+            ci_gemm_kernel<kCiTrX><<<(perx + perl) * L, 512, 0, st>>>(gx, S);
+          }
         }
       }
     } else {
@@ -1012,7 +1218,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     }
   }
   LVAE_CHECK_LAUNCH();
-  {
+  if (!pipe) {
     // trtri (recursive doubling, 2 launches per level): with lauum (ci_lauum_f32) the rest of potri
     ProfScope ps(LVAE_PH_POTRI, st);
     ci_diag_copy_kernel<<<dim3(16 * nt, L), 256, 0, st>>>(S, np_, Yh, Yl, YTh, YTl);
@@ -1067,6 +1273,7 @@ int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv,
   const int64_t full = (int64_t)L * np_ * np_;
   ProfScope ps(LVAE_PH_POTRI, st);
   CiGemmArgs gl{YT, YT + full, YT, YT + full, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg, 0};
+  gl.pre = ci_pipe_mode(np_, L) == 2;  // (the factor accumulated K^-1 already: the same decision)
   if (mu) {
     gl.mu = mu;
     gl.sv = sv;

@@ -318,21 +318,29 @@ __device__ inline void pv_ij(int n, int& i, int& j) {
 // wave (I_h < 0: none), A = (src[0] hi, src[1] lo) and B = (src[2], src[3]) fp16 planes, 256 rows of
 // 256 halves each.  K in 4 chunks of 64 staged in the pivot's LDS ([4 parts][256 rows][72 halves]: the
 // 144-B row pitch puts a 16-lane ds_read_b128 phase on 16 distinct bank groups); PREF: the next chunk's
-// global loads are issued under the current chunk's MFMAs (8 more VGPR quads).  Ends after a barrier
-// only if the caller adds one: the staging area is still being read.
+// global loads are issued under the current chunk's MFMAs (8 more VGPR quads).  SAMEAB: B = A (only the
+// A parts are loaded, B's fragments read from them: half the bytes of X X^T).  BTRI: B is lower
+// triangular ([row][k] = 0 for k > row): chunk kc loads only B rows >= kc and skips the blocks J_h whose
+// rows all lie above it (the zero upper half of Y_kk in X = C Y_kk^T).  Ends after a barrier only if the
+// caller adds one: the staging area is still being read.
 constexpr int kPvKC = 64, kPvKP = kPvKC + 8;
-template <int NB, bool PREF>
+template <int NB, bool PREF, bool SAMEAB = false, bool BTRI = false>
 __device__ inline void pv_x3_gemm(const _Float16* const* src, float* __restrict__ lf, const int* bi, const int* bj,
                                   pv_f32x16* acc, const int64_t* sld = nullptr) {
   // sld: row stride (halves) of each of the 4 sources (nullptr: kSwB, the [256][256] plane blocks)
   const int tid = threadIdx.x, lane = tid & 63, rl = lane & 31, hh = lane >> 5;
+  constexpr int NU = SAMEAB ? 4 : 8;  // 16-B pieces per thread and chunk
   _Float16* st = reinterpret_cast<_Float16*>(lf);
-  x3_half8 v[8];
+  x3_half8 v[NU];
+  auto need = [&](int u, int kc) {  // (thread-dependent) the piece is not a zero of a triangular B
+    const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255;
+    return !(BTRI && p >= 2 && row < kc);
+  };
   auto load = [&](int kc) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {  // 4 parts x 256 rows x 8 16-B chunks = 8 per thread
+    for (int u = 0; u < NU; ++u) {  // parts x 256 rows x 8 16-B chunks
       const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
-      v[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * (sld ? sld[p] : kSwB) + kc + 8 * c8);
+      if (need(u, kc)) v[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * (sld ? sld[p] : kSwB) + kc + 8 * c8);
     }
   };
   if (PREF) load(0);
@@ -340,23 +348,24 @@ __device__ inline void pv_x3_gemm(const _Float16* const* src, float* __restrict_
     __syncthreads();  // the previous chunk's readers are done
     if (PREF) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < NU; ++u) {
         const int e = tid + 1024 * u, p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
-        *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = v[u];
+        if (need(u, kc)) *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = v[u];
       }
-    } else {  // two rounds of 4 (fewer live registers beside a 4-block accumulator set)
+    } else {  // rounds of 4 (fewer live registers beside a 4-block accumulator set)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < NU / 4; ++q) {
         x3_half8 t[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e = tid + 1024 * (4 * q + u), p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
-          t[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * (sld ? sld[p] : kSwB) + kc + 8 * c8);
+          if (need(4 * q + u, kc))
+            t[u] = *reinterpret_cast<const x3_half8*>(src[p] + row * (sld ? sld[p] : kSwB) + kc + 8 * c8);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e = tid + 1024 * (4 * q + u), p = e >> 11, row = (e >> 3) & 255, c8 = e & 7;
-          *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = t[u];
+          if (need(4 * q + u, kc)) *reinterpret_cast<x3_half8*>(st + (p * kSwB + row) * kPvKP + 8 * c8) = t[u];
         }
       }
     }
@@ -365,8 +374,9 @@ __device__ inline void pv_x3_gemm(const _Float16* const* src, float* __restrict_
 #pragma unroll
     for (int h = 0; h < NB; ++h) {
       if (bi[h] < 0) continue;
+      if (BTRI && 32 * bj[h] + 31 < kc) continue;  // (wave-uniform) a zero chunk of the triangular B
       const _Float16* ar = st + (32 * bi[h] + rl) * kPvKP;
-      const _Float16* br = st + (2 * kSwB + 32 * bj[h] + rl) * kPvKP;
+      const _Float16* br = st + ((SAMEAB ? 0 : 2 * kSwB) + 32 * bj[h] + rl) * kPvKP;
 #pragma unroll
       for (int ks = 0; ks < kPvKC / 16; ++ks) {
         const int ko = 16 * ks + 8 * hh;
