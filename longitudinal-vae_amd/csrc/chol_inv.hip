@@ -101,6 +101,8 @@ struct CiScratch {
   float* xsc;               // [L][nt][nt] (l, i, j): tile (i, j) of the trtri intermediate X
   _Float16 *XRh[2], *XRl[2];  // pipelined trtri: the X^T tiles (j, m) of row block m, [L][nt][256 x 256] (one
                               // chunk-major tile each), by row parity; nullptr unless ci_pipe_alloc
+  int* cnt;                   // [L][nt] split pivots: arrival tickets per (dim, pass), zeroed per call (own block)
+  float* xs;                  // [L][kCiPvG] split pivots: the split scale of each helper's X slab
   int nt;
   size_t bytes;
   CiScratch(char* base, int np_, int L) {
@@ -131,8 +133,11 @@ struct CiScratch {
       XRh[b] = ci_pipe_alloc(np_, L) ? (_Float16*)take(col * 2) : nullptr;
       XRl[b] = ci_pipe_alloc(np_, L) ? (_Float16*)take(col * 2) : nullptr;
     }
+    cnt = (int*)take(cnt_bytes(L, nt));
+    xs = (float*)take((size_t)L * 8 * 4);
     bytes = off;
   }
+  static size_t cnt_bytes(int L, int nt) { return ((size_t)L * nt * 4 + 15) & ~size_t(15); }
   __device__ float& c_scale(int l, int k, int i) const { return csc[((int64_t)l * nt + k) * nt + i]; }
   __device__ float& t_scale(float* s, int l, int i, int j) const { return s[((int64_t)l * nt + i) * nt + j]; }
 };
@@ -219,30 +224,182 @@ __device__ inline void ci_pending_update(const float* __restrict__ T, int64_t np
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Split pivot (kCiPvG workgroups per dim, schedule (a)): the pending update's X = C_kb Y_kp^T is computed
+// by the dim's kCiPvG workgroups in row slabs of 256 / kCiPvG rows, each split at its own exact max into
+// the X planes (scale xs[l][h]); a ticket per (dim, pass) elects the LAST arriving workgroup (in-launch
+// hand-off, cdna_hip_programming.md's split-K recipe: plain stores, vmcnt drain, barrier, agent release,
+// relaxed agent ticket; the last: agent acquire, then plain loads), which goes on alone with A_kk - X X^T
+// (per-slab-pair scales), the Cholesky and the rest.  The others exit.  Placement is for speed only (a
+// dim's workgroups share blockIdx % 8: one XCD under round-robin dispatch, the slabs read from its L2).
+// ------------------------------------------------------------------------------------------
+constexpr int kCiPvG = 4;                 // workgroups per split pivot
+constexpr int kCiPvR = kSwB / kCiPvG;     // X rows per helper (64: 2 x 8 blocks of 32 x 32, one per wave)
+__device__ inline void ci_pending_slab(const CiScratch& S, int64_t np_, int l, int kb, int h, float* __restrict__ lf,
+                                       uint32_t* red) {
+  static_assert(kCiPvR / 32 * 8 == 16, "one 32 x 32 block of the slab per wave");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int kp = kb - 1;
+  const int64_t oc = (int64_t)l * np_ * kSwB + (int64_t)kb * kSwBB + (int64_t)h * kCiPvR * kSwB;
+  const int64_t od = ((int64_t)l * S.nt + kp) * kSwBB;
+  const _Float16* src[4] = {S.Ch[kp & 1] + oc, S.Cl[kp & 1] + oc, S.Dh + od, S.Dl + od};
+  _Float16* st = reinterpret_cast<_Float16*>(lf);
+  // staging per 64-deep chunk: A parts [2][64 rows][kPvKP], B parts [2][256 rows][kPvKP]; thread t loads A
+  // piece t (part t >> 9, row (t >> 3) & 63, 16-B chunk t & 7) and B pieces t + 1024 u (u < 4: part u >> 1,
+  // row ((t >> 3) & 127) + 128 (u & 1)); B rows < kc are zero (Y_kp lower triangular): not loaded
+  const int arow = (tid >> 3) & 63, ap = tid >> 9, c8 = tid & 7, brow0 = (tid >> 3) & 127;
+  auto aoff = [&](int p, int row) { return (p * kCiPvR + row) * kPvKP; };
+  auto boff = [&](int p, int row) { return (2 * kCiPvR + p * kSwB + row) * kPvKP; };
+  x3_half8 va, vb[4];
+  auto load = [&](int kc) {
+    va = *reinterpret_cast<const x3_half8*>(src[ap] + arow * kSwB + kc + 8 * c8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = brow0 + 128 * (u & 1);
+      if (row >= kc) vb[u] = *reinterpret_cast<const x3_half8*>(src[2 + (u >> 1)] + row * kSwB + kc + 8 * c8);
+    }
+  };
+  const int bi = w >> 3, bj = w & 7;
+  pv_f32x16 acc = {};
+  load(0);
+  for (int kc = 0; kc < kSwB; kc += kPvKC) {
+    __syncthreads();  // the previous chunk's readers are done
+    *reinterpret_cast<x3_half8*>(st + aoff(ap, arow) + 8 * c8) = va;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = brow0 + 128 * (u & 1);
+      if (row >= kc) *reinterpret_cast<x3_half8*>(st + boff(u >> 1, row) + 8 * c8) = vb[u];
+    }
+    __syncthreads();
+    if (kc + kPvKC < kSwB) load(kc + kPvKC);
+    if (32 * bj + 31 >= kc) {  // (wave-uniform) a non-zero chunk of Y_kp's row block bj
+      const _Float16* ar = st + aoff(0, 32 * bi + rl);
+      const _Float16* br = st + boff(0, 32 * bj + rl);
+#pragma unroll
+      for (int ks = 0; ks < kPvKC / 16; ++ks) {
+        const int ko = 16 * ks + 8 * hh;
+        const x3_half8 aH = *reinterpret_cast<const x3_half8*>(ar + ko);
+        const x3_half8 aL = *reinterpret_cast<const x3_half8*>(ar + kCiPvR * kPvKP + ko);
+        const x3_half8 bH = *reinterpret_cast<const x3_half8*>(br + ko);
+        const x3_half8 bL = *reinterpret_cast<const x3_half8*>(br + kSwB * kPvKP + ko);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH, acc, 0, 0, 0);
+      }
+    }
+  }
+  const float inv = 1.0f / (S.c_scale(l, kp, kb) * S.ysc[((int64_t)l * S.nt + kp) * S.nt + kp]);
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    acc[e] *= inv;
+    m = fmaxf(m, fabsf(acc[e]));
+  }
+  const float sx = x3_scale(sw_block_max(m, red));
+  const int64_t ox = (int64_t)l * kSwBB + (int64_t)h * kCiPvR * kSwB;
+  _Float16* xh = S.Xh + ox;
+  _Float16* xl = S.Xl + ox;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int r = 32 * bi + pv_row(e, hh), c = 32 * bj + rl;
+    const float y = acc[e] * sx;
+    const _Float16 yh = (_Float16)y;
+    xh[r * kSwB + c] = yh;
+    xl[r * kSwB + c] = (_Float16)(y - (float)yh);
+  }
+  if (tid == 0) S.xs[l * 8 + h] = sx;
+}
+
+// the last workgroup's A_kk - X X^T (X planes of kCiPvG slabs, slab h at scale xs[l][h]) into lf
+__device__ inline void ci_pending_reduce(const float* __restrict__ T, int64_t np_, const CiScratch& S, int l,
+                                         float* __restrict__ lf) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  const int64_t ox = (int64_t)l * kSwBB;
+  float xsl[kCiPvG];
+#pragma unroll
+  for (int h = 0; h < kCiPvG; ++h) xsl[h] = S.xs[l * 8 + h];
+  const _Float16* src[4] = {S.Xh + ox, S.Xl + ox, S.Xh + ox, S.Xl + ox};
+  int bi[3], bj[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n < 0) {
+      bi[h] = bj[h] = -1;
+    } else {
+      pv_ij(n, bi[h], bj[h]);
+    }
+  }
+  pv_f32x16 acc[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) acc[h] = pv_f32x16{};
+  pv_x3_gemm<3, true, LVAE_PV_SAMEAB != 0>(src, lf, bi, bj, acc);
+  float old[3][16];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    if (bi[h] < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) old[h][e] = T[(int64_t)(32 * bi[h] + pv_row(e, hh)) * np_ + 32 * bj[h] + rl];
+  }
+  __syncthreads();  // every wave's last staging read
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int n = kLauum[w][h];
+    if (n < 0) continue;
+    const float inv = 1.0f / (xsl[(32 * bi[h]) / kCiPvR] * xsl[(32 * bj[h]) / kCiPvR]);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) lf[n * kPvBlk + pv_row(e, hh) * kPvL + rl] = old[h][e] - acc[h][e] * inv;
+  }
+}
+
 // dev: phase timestamps of the pivots (s_memrealtime, 100 MHz) into prof[(kb * L + l) * 8 + phase] when
 // lvae_dev_pivot_prof set a buffer (scripts/pivot_prof.py); nullptr in the product
 static unsigned long long* g_pivot_prof = nullptr;
 #define CI_STAMP(q)                                                                     \
   do {                                                                                  \
-    if (prof && threadIdx.x == 0) prof[((int64_t)kb * gridDim.x + l) * 8 + (q)] = __builtin_amdgcn_s_memrealtime(); \
+    if (prof && threadIdx.x == 0) prof[((int64_t)kb * L + l) * 8 + (q)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
+// G == 1: one workgroup per dim (blockIdx = dim); G == kCiPvG (pending only): the split pivot, workgroup b
+// of dim b % Lr, slab b / Lr (Lr = gridDim.x / G, a multiple of 8; dims >= L exit)
+template <int G>
 __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict__ Aall, int np_, int kb, CiScratch S,
                                                         double* __restrict__ logdet, int32_t* __restrict__ info,
-                                                        int pending, unsigned long long* __restrict__ prof) {
+                                                        int pending, int L, unsigned long long* __restrict__ prof) {
   __shared__ float lf[kPvBlocks * kPvBlk];
   __shared__ uint32_t ymax_s, xmax_s, dmax_s;
   __shared__ float bsc[kPvBlocks];
-  __shared__ int bad_s;
-  const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
+  __shared__ int bad_s, last_s;
+  const int Lr = gridDim.x / G, l = G == 1 ? blockIdx.x : blockIdx.x % Lr, hs = G == 1 ? 0 : blockIdx.x / Lr;
+  if (l >= L) return;  // (uniform; padding dims of the split grid)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
-  CI_STAMP(0);
+  if (hs == 0) CI_STAMP(0);
   if (tid == 0) {
     bad_s = INT_MAX;
     ymax_s = 0u;
     xmax_s = 0u;
   }
-  if (pending) {
+  if (G > 1) {  // (pending) the slab, the hand-off, then only the last arriving workgroup goes on
+    __syncthreads();  // xmax_s
+    ci_pending_slab(S, np_, l, kb, hs, lf, &xmax_s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slab stores done
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(S.cnt + (int64_t)l * S.nt + kb, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      last_s = t == G - 1;
+    }
+    __syncthreads();
+    if (!last_s) return;  // (uniform)
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    ci_pending_reduce(T, np_, S, l, lf);
+  } else if (pending) {
     __syncthreads();  // xmax_s
     ci_pending_update(T, np_, S, l, kb, lf, &xmax_s);
   } else {
@@ -455,6 +612,30 @@ __device__ inline void ci_planes_out(const sx_f32x16 (&acc)[4][2], float mul, fl
         const _Float16 yh = (_Float16)y;
         hi[r * ld + c] = yh;
         lo[r * ld + c] = (_Float16)(y - (float)yh);
+      }
+}
+
+// as ci_planes_out through buffer stores (offsets from compile-time parts: fewer address registers beside the
+// c16 core's fragment sets)
+__device__ inline void ci_planes_out_buf(const sx_f32x16 (&acc)[4][2], float mul, float s, _Float16* __restrict__ hi,
+                                         _Float16* __restrict__ lo, int ld) {
+  const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(hi, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(lo, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int vb = (((w >> 2) * 128 + 4 * (lane >> 5)) * ld + (w & 3) * 64 + (lane & 31)) * 2;
+  const float m = mul * s;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float y = acc[a][b][e] * m;
+        const _Float16 yh = (_Float16)y;
+        const _Float16 yl = (_Float16)(y - (float)yh);
+        const int so = ((32 * a + (e & 3) + 8 * (e >> 2)) * ld + 32 * b) * 2;
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yh), rh, vb, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, yl), rl, vb, so, 0);
       }
 }
 
@@ -698,6 +879,14 @@ constexpr int kCiX = 0, kCiY = 1, kCiLauum = 2, kCiLauumKL = 3;
 //                    t >= g.inst0 (mode 2): Lupd(m), tile (I, J), J <= I <= m: K^-1_IJ (+)= Y_mI^T Y_mJ
 //                    (A, B = Y^T planes (I, m), (J, m); written at m == I) into g.Kinv
 constexpr int kCiTrY = 4, kCiTrX = 5;
+// potrf's panel and trailing update on the same core, for ci_pair_kernel launches of the pipelined schedule
+// (h = the pass m, dims interleaved: workgroup b of dim b % L):
+//   kCiPanel  tile i = m + 1 + t: L_im = C_i Y_mm^T   A = pass m's C planes (block i, row-major), B = D_m
+//             -> the L planes (i, m), scale lsc(i, m) (as ci_panel_kernel)
+//   kCiU12c   t < g.inst0: column m + 1's tile I = m + 2 + t, else a trailing tile I >= J >= m + 2:
+//             A_IJ - L_Im L_Jm^T (A = g.Kinv, the fp32 matrix), column tiles -> pass m + 1's C planes, scale
+//             csc(m + 1, I), trailing ones in place (as ci_update_kernel<kCiU12>, the A tile read after the K loop)
+constexpr int kCiPanel = 6, kCiU12c = 7;
 #ifndef LVAE_KL_MIRROR
 #define LVAE_KL_MIRROR 0  // 1: the KL lauum also writes the upper tiles of K^-1 (no reader needs them)
 #endif
@@ -814,27 +1003,44 @@ __device__ inline void ci_diag_t_piece(const CiScratch& S, int np_, int l, int k
   }
 }
 
+// the body of one workgroup of ci_gemm_kernel<MODE>, as workgroup `bid` of its launch, on the caller's
+// LDS objects (ci_pair_kernel runs two modes' bodies in one launch)
 template <int MODE>
-__global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S) {
-  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
-  __shared__ float sprod[64];
-  __shared__ uint32_t red;
-  __shared__ float kl_mu[2 * kSwB], kl_sv[2 * kSwB], kl_part[6 * kSwB];  // (kCiLauumKL only)
+__device__ inline void ci_gemm_body(const CiGemmArgs& g, const CiScratch& S, const int bid, _Float16* __restrict__ lds,
+                                    float* __restrict__ sprod, uint32_t* __restrict__ redp, float* __restrict__ kl_mu,
+                                    float* __restrict__ kl_sv, float* __restrict__ kl_part) {
+  uint32_t& red = *redp;
   const int nt = g.nt, np_ = g.np_;
   int l, i, j, kb0, kb1;
   if constexpr (MODE == kCiLauum || MODE == kCiLauumKL) {
     // XCD-contiguous remap, 4 x 8 blocks of tiles sharing their Y^T panels in an XCD's L2 (small I,
     // the longest K ranges, first)
-    const int orig = blockIdx.x, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
+    const int orig = bid, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
     l = wgid / g.per_dim;
     sx_tri_blocked(wgid % g.per_dim, nt, i, j);
     kb0 = i;
     kb1 = nt;
+  } else if constexpr (MODE == kCiPanel || MODE == kCiU12c) {
+    const int L = g.nwg / g.per_dim, t = bid / L, m = g.h;
+    l = bid % L;
+    if constexpr (MODE == kCiPanel) {
+      i = m + 1 + t;
+      j = m;
+    } else if (t < g.inst0) {
+      i = m + 2 + t;
+      j = m + 1;
+    } else {
+      sx_tri(t - g.inst0, i, j);
+      i += m + 2;
+      j += m + 2;
+    }
+    kb0 = m;
+    kb1 = m + 1;
   } else if constexpr (MODE == kCiTrY || MODE == kCiTrX) {
     // dims interleaved (block b: dim b % L): the first L (m + 1) workgroups of Xupd are row m + 1's tiles
-    const int L = g.nwg / g.per_dim, t = blockIdx.x / L, m = g.h;
-    l = blockIdx.x % L;
+    const int L = g.nwg / g.per_dim, t = bid / L, m = g.h;
+    l = bid % L;
     if constexpr (MODE == kCiTrY) {
       i = m;
       j = t;
@@ -855,8 +1061,8 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     // takes latent dim b % L (an XCD then keeps the dims b % 8 selects, and their panels) and the
     // t = b / L-th tile of a K-descending order -- X: K = o + h - j, so j_off = j - o ascending; Y:
     // K = i - o - h + 1, so i_off = i - o - h descending; then the instance, then the other index
-    const int L = g.nwg / g.per_dim, t = blockIdx.x / L, h = g.h, ninst = g.per_dim / (h * h);
-    l = blockIdx.x % L;
+    const int L = g.nwg / g.per_dim, t = bid / L, h = g.h, ninst = g.per_dim / (h * h);
+    l = bid % L;
     const int slow = t / (ninst * h), rem = t % (ninst * h), m = g.inst0 + rem / h, fast = rem % h, o = 2 * h * m;
     if constexpr (MODE == kCiX) {
       j = o + slow;
@@ -886,11 +1092,17 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     } else if constexpr (MODE == kCiY) {
       sa = S.ysc[sl + (int64_t)i * nt + kb];
       sb = S.xsc[sl + (int64_t)kb * nt + j];
+    } else if constexpr (MODE == kCiPanel) {  // (kb = m)
+      sa = S.csc[((int64_t)l * nt + kb) * nt + i];
+      sb = S.ysc[sl + (int64_t)kb * nt + kb];
+    } else if constexpr (MODE == kCiU12c) {  // (kb = m)
+      sa = S.lsc[sl + (int64_t)i * nt + kb];
+      sb = S.lsc[sl + (int64_t)j * nt + kb];
     } else if constexpr (MODE == kCiTrY) {  // (kb = m = i)
       sa = S.ysc[sl + (int64_t)i * nt + i];
       sb = S.xsc[sl + (int64_t)i * nt + j];
     } else if constexpr (MODE == kCiTrX) {  // (kb = m)
-      sa = (int)(blockIdx.x / (g.nwg / g.per_dim)) < g.inst0 ? S.lsc[sl + (int64_t)i * nt + kb]
+      sa = (int)(bid / (g.nwg / g.per_dim)) < g.inst0 ? S.lsc[sl + (int64_t)i * nt + kb]
                                                             : S.ysc[sl + (int64_t)kb * nt + i];
       sb = S.ysc[sl + (int64_t)kb * nt + j];
     } else {
@@ -926,8 +1138,17 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
                                                : C16Opnd{g.ah + c16_panel(l, np_, i) + kc0, g.al - g.ah, 0};
     C16Opnd B{g.bh + c16_panel(l, np_, j) + kc0, g.bl - g.bh, 0};
     if constexpr (MODE == kCiTrX) {
-      if ((int)(blockIdx.x / (g.nwg / g.per_dim)) >= g.inst0)  // Lupd: A = Y^T planes (i, m)
+      if ((int)(bid / (g.nwg / g.per_dim)) >= g.inst0)  // Lupd: A = Y^T planes (i, m)
         A = C16Opnd{g.bh + c16_panel(l, np_, i) + kc0, g.bl - g.bh, 0};
+    }
+    if constexpr (MODE == kCiPanel) {  // A = C block i (pass m's planes, row-major 256 x 256), B = D_m
+      const int64_t oc = (int64_t)l * np_ * kSwB + (int64_t)i * kSwBB, od = ((int64_t)l * nt + kb0) * kSwBB;
+      A = C16Opnd{S.Ch[kb0 & 1] + oc, S.Cl[kb0 & 1] - S.Ch[kb0 & 1], kSwB};
+      B = C16Opnd{S.Dh + od, S.Dl - S.Dh, kSwB};
+    }
+    if constexpr (MODE == kCiU12c) {  // A, B = the L planes (i, m), (j, m), row-major (stride np)
+      A = C16Opnd{S.Lh + oa, S.Ll - S.Lh, np_};
+      B = C16Opnd{S.Lh + ob, S.Ll - S.Lh, np_};
     }
     if constexpr (MODE == kCiTrY) {  // A = D_m (row-major, stride 256), B = X^T row tile j (one chunk-major tile)
       const int64_t od = ((int64_t)l * nt + i) * kSwBB, ox = ((int64_t)l * nt + j) * kSwBB;
@@ -958,7 +1179,42 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
   } else {
     inv = 1.0f / sx_gemm_scaled(ah, al, bh, bl, np_, nkb, sprod, lds, acc);
   }
-  if constexpr (MODE == kCiTrY) {
+  if constexpr (MODE == kCiPanel) {
+    const float slc = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
+    const int64_t ot = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;
+    ci_planes_out_buf(acc, inv, slc, S.Lh + ot, S.Ll + ot, np_);
+    if (threadIdx.x == 0) S.lsc[sl + (int64_t)i * nt + j] = slc;
+  } else if constexpr (MODE == kCiU12c) {
+    const int m = g.h;
+    float* At = g.Kinv + l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(At, (short)0, 0x7fffffff, 0x00020000);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                             ra, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 2)) -
+                         acc[a][b][e] * inv;
+    if (j == m + 1) {  // (uniform) column m + 1: pass m + 1's C operand
+      const float sc = x3_scale(sw_block_max(ci_acc_absmax(acc), &red));
+      const int64_t on = (int64_t)l * np_ * kSwB + (int64_t)i * kSwBB;
+      ci_planes_out_buf(acc, 1.f, sc, S.Ch[(m + 1) & 1] + on, S.Cl[(m + 1) & 1] + on, kSwB);
+      if (threadIdx.x == 0) S.csc[((int64_t)l * nt + m + 1) * nt + i] = sc;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e]), ra, vo,
+                                                  ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 2);
+    }
+  } else if constexpr (MODE == kCiTrY) {
     const float sy = x3_scale(sw_block_max(ci_acc_absmax(acc) * inv, &red));
     ci_transposed_out(acc, -inv, lds, [&](int c, int r0, f32x4 v) {
       const int64_t o = c16_off(l, np_, j * kSwB + c, i * kSwB + r0);  // Y^T tile (j, m)
@@ -967,7 +1223,7 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
     if (threadIdx.x == 0) S.ysc[sl + (int64_t)i * nt + j] = sy;
   } else if constexpr (MODE == kCiTrX) {
     const int m = g.h;
-    const bool lup = (int)(blockIdx.x / (g.nwg / g.per_dim)) >= g.inst0;
+    const bool lup = (int)(bid / (g.nwg / g.per_dim)) >= g.inst0;
     float* Xt = g.Kinv + l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;  // fp32 X / K^-1 tile (i, j)
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(Xt, (short)0, 0x7fffffff, 0x00020000);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1105,6 +1361,30 @@ __global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S)
   }
 }
 
+
+#define CI_GEMM_LDS                                                                     \
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];                \
+  __shared__ float sprod[64];                                                           \
+  __shared__ uint32_t red;                                                              \
+  __shared__ float kl_mu[2 * kSwB], kl_sv[2 * kSwB], kl_part[6 * kSwB]; /* (kCiLauumKL only) */
+
+template <int MODE>
+__global__ __launch_bounds__(512) void ci_gemm_kernel(CiGemmArgs g, CiScratch S) {
+  CI_GEMM_LDS
+  ci_gemm_body<MODE>(g, S, blockIdx.x, lds, sprod, &red, kl_mu, kl_sv, kl_part);
+}
+
+// two modes in ONE launch (the pipelined schedule's passes: fewer, fuller launches on the caller's stream):
+// workgroups [0, n1) run M1 over g1, the rest M2 over g2
+template <int M1, int M2>
+__global__ __launch_bounds__(512) void ci_pair_kernel(CiGemmArgs g1, CiGemmArgs g2, CiScratch S, int n1) {
+  CI_GEMM_LDS
+  if ((int)blockIdx.x < n1)
+    ci_gemm_body<M1>(g1, S, blockIdx.x, lds, sprod, &red, kl_mu, kl_sv, kl_part);
+  else
+    ci_gemm_body<M2>(g2, S, blockIdx.x - n1, lds, sprod, &red, kl_mu, kl_sv, kl_part);
+}
+
 // ------------------------------------------------------------------------------------------
 // host sequencing
 // ------------------------------------------------------------------------------------------
@@ -1153,22 +1433,54 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     LVAE_TRY(side_stream(sd));
     (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
     (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
+    (void)hipMemsetAsync(S.cnt, 0, CiScratch::cnt_bytes(L, nt), st);  // the split pivots' tickets
     if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
     const bool fuse = L <= kCiFuseMaxL;
     const int pmode = ci_pipe_mode(np_, L);  // (implies fuse and the XR planes)
+    // the split pivot (kCiPvG workgroups per pending pivot); LVAE_PIVOT_SPLIT=0: one workgroup per dim
+    static const bool split_env = !getenv("LVAE_PIVOT_SPLIT") || atoi(getenv("LVAE_PIVOT_SPLIT")) != 0;
+    const bool split = split_env;
+    // LVAE_CI_PAIR=1: the pipelined passes as two ci_pair_kernel launches each instead of four (measured
+    // slower: the fused update launch ends later, and the next-but-one pivot waits for it -- scripts/inv_ab.py,
+    // L = 2: 2.51 vs 2.18 ms for the inverse)
+    static const bool pair = getenv("LVAE_CI_PAIR") && atoi(getenv("LVAE_CI_PAIR")) != 0;
     pipe = pmode > 0;
     if (fuse) {
-      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, g_pivot_prof);
+      ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, L, g_pivot_prof);
       if (!ok(hipEventRecord(sd->piv[0], sd->s))) return LVAE_ERR_LAUNCH;
       if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, st>>>(A, np_, S);
       if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
       for (int m = 0; m < nt; ++m) {
         if (m + 1 < nt) {
           if (!ok(hipStreamWaitEvent(sd->s, m == 0 ? sd->c : sd->u2p[(m - 1) & 1], 0))) return LVAE_ERR_LAUNCH;
-          ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1, g_pivot_prof);
+          if (split) {
+            const int Lr = (L + 7) / 8 * 8;
+            ci_pivot_kernel<kCiPvG><<<kCiPvG * Lr, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1, L, g_pivot_prof);
+          } else {
+            ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, m + 1, S, logdet, info, 1, L, g_pivot_prof);
+          }
           if (!ok(hipEventRecord(sd->piv[(m + 1) & 1], sd->s))) return LVAE_ERR_LAUNCH;
         }
         if (!ok(hipStreamWaitEvent(st, sd->piv[m & 1], 0))) return LVAE_ERR_LAUNCH;
+        if (pipe && pair) {
+          // two launches per pass: [panel(m) + rowY(m)] then [U1 + U2(m) + Xupd(m) (+ Lupd(m))] -- the
+          // caller's stream keeps up with the pivot chain (four separate launches per pass did not)
+          ProfScope pt(LVAE_PH_POTRI, st);
+          const int npn = nt - m - 1, ny = m + 16;
+          CiGemmArgs gp{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, np_, nt, m,
+                        max(npn, 1), npn * L, 0};
+          CiGemmArgs gy{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, YTh, YTl, nullptr, np_, nt, m, ny, ny * L, 0};
+          ci_pair_kernel<kCiPanel, kCiTrY><<<(npn + ny) * L, 512, 0, st>>>(gp, gy, S, npn * L);
+          const int n1 = max(nt - m - 2, 0), n2 = max(nt - m - 2, 0) * max(nt - m - 1, 0) / 2, nu = n1 + n2;
+          const int perx = (nt - m - 1) * (m + 1), perl = pmode == 2 ? (m + 1) * (m + 2) / 2 : 0;
+          CiGemmArgs gu{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, A, np_, nt, m,
+                        max(nu, 1), nu * L, n1};
+          CiGemmArgs gx{S.Lh, S.Ll, YTh, YTl, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, m, max(perx + perl, 1),
+                        (perx + perl) * L, perx};
+          if (nu + perx + perl > 0) ci_pair_kernel<kCiU12c, kCiTrX><<<(nu + perx + perl) * L, 512, 0, st>>>(gu, gx, S, nu * L);
+          if (m + 1 < nt && !ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
+          continue;
+        }
         if (m + 1 < nt) {
           ci_panel_kernel<<<dim3(nt - m - 1, L), 512, 0, st>>>(S, np_, m);
           // column m+1 without the pivot block + the trailing tiles, one launch
@@ -1196,7 +1508,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
       }
     } else {
       if (nt > 1) ci_prep0_kernel<<<dim3(nt - 1, L), 256, 0, sd->s>>>(A, np_, S);
-      ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, g_pivot_prof);
+      ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, L, g_pivot_prof);
       if (nt > 1) ci_panel_kernel<<<dim3(nt - 1, L), 512, 0, sd->s>>>(S, np_, 0);
       if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
       for (int k = 0; k + 1 < nt; ++k) {
@@ -1205,7 +1517,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
         ci_update_kernel<kCiU1><<<n1 * L, 512, 0, st>>>(A, S, np_, k, n1, n1 * L);
         if (!ok(hipEventRecord(sd->c, st))) return LVAE_ERR_LAUNCH;
         if (!ok(hipStreamWaitEvent(sd->s, sd->c, 0))) return LVAE_ERR_LAUNCH;
-        ci_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0, g_pivot_prof);
+        ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, k + 1, S, logdet, info, 0, L, g_pivot_prof);
         if (k + 2 < nt) ci_panel_kernel<<<dim3(nt - k - 2, L), 512, 0, sd->s>>>(S, np_, k + 1);
         if (!ok(hipEventRecord(sd->prep, sd->s))) return LVAE_ERR_LAUNCH;
         const int n2 = (nt - k - 2) * (nt - k - 1) / 2;

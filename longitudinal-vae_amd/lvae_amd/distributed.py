@@ -191,6 +191,8 @@ class LatentShardedClosedStep:
             mse, nll = self.vae.loss_function(recon, img, mask)
             recon_loss, nll_loss = mse.sum(), nll.sum()
             (recon_loss if self.loss_function == "mse" else nll_loss).backward()  # decoder + d/dz
+        if factor is not None:
+            factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
         main.wait_event(gathered)
         full.record_stream(main)
         coef = self.weight / L if self.loss_function == "mse" else 1.0

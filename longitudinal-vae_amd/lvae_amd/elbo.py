@@ -4,6 +4,8 @@ Each function takes the same arguments as its reference twin and returns autogra
 tensors; the arithmetic runs in the HIP library through a ``torch.autograd.Function`` whose
 backward is the analytic adjoint (also HIP).  No PyTorch / CPU fallback exists.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -51,6 +53,22 @@ def check_pending(pend=None):
 # ------------------------------------------------------------------------------------------
 # Regime B: exact KL (elbo_functions.py:8-34), batched over latent dims
 # ------------------------------------------------------------------------------------------
+# The factor's host-side enqueue (Gram, then per block column of the blocked Cholesky ~8 HIP calls across
+# two streams: ~1-2 ms of host time) runs on a worker thread (ctypes releases the GIL), so that the caller's
+# thread goes on enqueueing the ConvVAE meanwhile -- at a few latent dims per GPU the step is otherwise
+# host-bound.  Not under graph capture.  LVAE_ASYNC_FACTOR=0 enqueues in the caller's thread.
+_ASYNC_FACTOR = os.environ.get("LVAE_ASYNC_FACTOR", "1") != "0"
+_FACTOR_POOL = None
+
+
+def _factor_pool():
+    global _FACTOR_POOL
+    if _FACTOR_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _FACTOR_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="lvae-factor")
+    return _FACTOR_POOL
+
+
 class KLFactor:
     """K^-1 and log|K| of the L covariances, computed ahead of (mu, logvar) on a caller stream
     (lvae_kl_closed_factor_f32): kl_closed_prefactor launches it, KL_closed_batched(..., factor=)
@@ -72,16 +90,33 @@ class KLFactor:
             self.nz = noise.detach().to(torch.float64).reshape(L).contiguous()
             self.ws = torch.empty(int(lib.lvae_kl_closed_workspace_size(n, L)), dtype=torch.uint8, device=dev)
             self.info = torch.empty(L, dtype=torch.int32, device=dev)
-            rc = lib.lvae_kl_closed_factor_f32(spec, _lib.ptr(self.x64), self.x64.shape[1], n, L, _lib.ptr(self.p),
-                                               _lib.ptr(self.nz), _lib.ptr(self.info), _lib.ptr(self.ws),
-                                               _lib.stream_ptr())
-            _lib.check(rc, "kl_closed_factor")
+        args = (spec, _lib.ptr(self.x64), self.x64.shape[1], n, L, _lib.ptr(self.p), _lib.ptr(self.nz),
+                _lib.ptr(self.info), _lib.ptr(self.ws), _lib.ctypes.c_void_p(stream.cuda_stream))
+        self._fut = None
+        if _ASYNC_FACTOR and not torch.cuda.is_current_stream_capturing():
+            dix = dev.index if dev.index is not None else torch.cuda.current_device()
+
+            def enqueue():
+                torch.cuda.set_device(dix)  # (the worker thread's HIP device: the library keys its side stream on it)
+                return lib.lvae_kl_closed_factor_f32(*args)
+            self._fut = _factor_pool().submit(enqueue)
+        else:
+            _lib.check(lib.lvae_kl_closed_factor_f32(*args), "kl_closed_factor")
         self.stream = stream
         self.n, self.L = n, L
         self.consumed = False
 
+    def wait_enqueued(self):
+        """Block until the factor's launches are all enqueued (call before enqueueing anything else on its
+        stream, so that nothing lands between them)."""
+        if self._fut is not None:
+            rc = self._fut.result()
+            self._fut = None
+            _lib.check(rc, "kl_closed_factor")
+
     def join(self):
         """Make the current stream wait for the factorisation (and own its buffers)."""
+        self.wait_enqueued()
         cur = torch.cuda.current_stream(self.ws.device)
         cur.wait_stream(self.stream)
         for t in (self.ws, self.info, self.x64, self.p, self.nz):

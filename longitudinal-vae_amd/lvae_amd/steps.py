@@ -58,6 +58,7 @@ class ClosedStep:
                 recon = self.vae.decode(z)
                 mse, nll = self.vae.loss_function(recon, img, mask)
                 recon_loss, nll_loss = mse.sum(), nll.sum()
+            factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
             main.wait_event(enc_done)
             mu.record_stream(main)
             log_var.record_stream(main)
