@@ -99,7 +99,7 @@ class LatentShardedClosedStep:
     --rank-share); its numbers are not the union step's."""
 
     def __init__(self, vae, kernel, likelihood, optimiser, weight=0.15, loss_function="mse", constrain_scales=True,
-                 group=None, kl_fn=None, sim_world=None, vae_stream_priority=-1):
+                 group=None, kl_fn=None, sim_world=None, vae_stream_priority=-1, graph_vae=None):
         self.vae, self.kernel, self.lik, self.opt = vae, kernel, likelihood, optimiser
         self.weight, self.loss_function, self.constrain_scales = weight, loss_function, constrain_scales
         self.group = group
@@ -112,6 +112,9 @@ class LatentShardedClosedStep:
                        if p.requires_grad]
         self.hyper_params = [p for p in list(kernel.parameters()) + list(likelihood.parameters()) if p.requires_grad]
         self.vae_stream_priority = vae_stream_priority
+        from .steps import _graph_vae_default
+        from .vae import GraphedConvVAE
+        self.gvae = GraphedConvVAE(vae) if (_graph_vae_default() if graph_vae is None else graph_vae) else None
 
     # -- the collectives (or their single-process stand-ins) -----------------------------------
     def _all_gather(self, loc, N):
@@ -166,6 +169,7 @@ class LatentShardedClosedStep:
         W, r = self.world, self.rank
         self.opt.zero_grad(set_to_none=True)
         main = torch.cuda.current_stream(img.device)
+        capturing = torch.cuda.is_current_stream_capturing()  # (an outer graph capture: the ConvVAE eager)
         vst = self._stream(img.device)
         vst.wait_stream(main)  # the previous step's updates
         L = self.vae.latent_dim
@@ -179,7 +183,8 @@ class LatentShardedClosedStep:
             factor = KLFactor(spec, params[d0:d1], noise[d0:d1], X, main)
         gathered = torch.cuda.Event()
         with torch.cuda.stream(vst):
-            mu, log_var = self.vae.encode(img)
+            gv = None if capturing else self.gvae
+            mu, log_var = gv.encode(img, mask) if gv is not None else self.vae.encode(img)
             n_loc = mu.shape[0]
             if n_loc * W != N:
                 raise ValueError(f"rank rows {n_loc} x world {W} != N = {N} (equal image shards required)")
@@ -187,10 +192,14 @@ class LatentShardedClosedStep:
             full = self._all_gather(torch.cat([mu.detach(), log_var.detach()], 1).contiguous(), N)
             gathered.record(vst)
             z_d = z.detach().requires_grad_()
-            recon = self.vae.decode(z_d)
-            mse, nll = self.vae.loss_function(recon, img, mask)
-            recon_loss, nll_loss = mse.sum(), nll.sum()
+            if gv is not None:
+                recon_loss, nll_loss = gv.decode_loss(z_d, img, mask)
+            else:
+                recon = self.vae.decode(z_d)
+                mse, nll = self.vae.loss_function(recon, img, mask)
+                recon_loss, nll_loss = mse.sum(), nll.sum()
             (recon_loss if self.loss_function == "mse" else nll_loss).backward()  # decoder + d/dz
+            recon_loss, nll_loss = recon_loss.detach().clone(), nll_loss.detach().clone()
         if factor is not None:
             factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
         main.wait_event(gathered)

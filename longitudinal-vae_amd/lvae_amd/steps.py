@@ -17,10 +17,20 @@ from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_b
                    take_pending)
 
 
+def _graph_vae_default():
+    # opt-in (LVAE_GRAPH_VAE=1): measured SLOWER on ROCm 7 -- the ConvVAE's graph replays on its stream held
+    # back the other streams' kernels (rank share of 8 GPUs 3.8 -> 10.9 ms per step, headline 11.7 -> 16.6 ms)
+    import os
+    return os.environ.get("LVAE_GRAPH_VAE", "0") == "1"
+
+
 class ClosedStep:
     def __init__(self, vae, kernel, likelihood, optimiser, weight=0.15, loss_function="mse",
-                 constrain_scales=True, grad_hook=None, vae_stream_priority=-1):
+                 constrain_scales=True, grad_hook=None, vae_stream_priority=-1, graph_vae=None):
         self.vae, self.kernel, self.lik, self.opt = vae, kernel, likelihood, optimiser
+        # the ConvVAE as replayed graphs (GraphedConvVAE; opt-in, see _graph_vae_default)
+        from .vae import GraphedConvVAE
+        self.gvae = GraphedConvVAE(vae) if (_graph_vae_default() if graph_vae is None else graph_vae) else None
         self.weight, self.loss_function, self.constrain_scales = weight, loss_function, constrain_scales
         self.grad_hook = grad_hook  # e.g. the data-parallel all-reduce
         # The ConvVAE's stream is created with a high priority by default: its kernels are small and
@@ -47,17 +57,25 @@ class ClosedStep:
             # hyper-parameter half (S GEMM + Gram adjoint, elbo._KLHyperFn).  (Two extra streams at
             # most: the box exposes 4 hardware queues, and the inverse keeps one side stream of its own.)
             main = torch.cuda.current_stream(img.device)
+            capturing = torch.cuda.is_current_stream_capturing()  # (an outer graph capture: the ConvVAE eager)
             vst = self._stream("_vae_stream", img.device)
             vst.wait_stream(main)  # the previous step's updates, before the factorisation is queued
             factor = kl_closed_prefactor(self.kernel, X, self.lik, self.vae.latent_dim, main)
             enc_done = torch.cuda.Event()
             with torch.cuda.stream(vst):
-                mu, log_var = self.vae.encode(img)
+                gv = None if capturing else self.gvae
+                if gv is not None:
+                    mu, log_var = gv.encode(img, mask)
+                else:
+                    mu, log_var = self.vae.encode(img)
                 enc_done.record(vst)
                 z = self.vae.sample_latent(mu, log_var, eps)
-                recon = self.vae.decode(z)
-                mse, nll = self.vae.loss_function(recon, img, mask)
-                recon_loss, nll_loss = mse.sum(), nll.sum()
+                if gv is not None:
+                    recon_loss, nll_loss = gv.decode_loss(z, img, mask)
+                else:
+                    recon = self.vae.decode(z)
+                    mse, nll = self.vae.loss_function(recon, img, mask)
+                    recon_loss, nll_loss = mse.sum(), nll.sum()
             factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
             main.wait_event(enc_done)
             mu.record_stream(main)
@@ -80,7 +98,7 @@ class ClosedStep:
             for t in (recon_loss, nll_loss, rec_term):
                 t.record_stream(main)
             net = rec_term.detach() + gp_term.detach()
-            return net, recon_loss.detach(), nll_loss.detach(), gp.detach()
+            return net, recon_loss.detach().clone(), nll_loss.detach().clone(), gp.detach()
         else:
             recon, mu, log_var = self.vae(img, eps)
             mse, nll = self.vae.loss_function(recon, img, mask)
@@ -188,6 +206,8 @@ class GraphedStep:
 
     def __init__(self, step, inputs, warmup=3):
         self.step, self.inputs = step, inputs
+        if getattr(step, "gvae", None) is not None:
+            step.gvae = None  # (the whole step is one graph here: no graphed ConvVAE parts inside the capture)
         comm = getattr(step, "grad_hook", None) is not None or getattr(step, "ng_reduce", None) is not None
         self.stream = torch.cuda.Stream()
         self.stream.wait_stream(torch.cuda.current_stream())

@@ -264,3 +264,68 @@ class ConvVAE(nn.Module):
         mse = se.sum(1) / msum
         nll = se / (2 * torch.exp(self._log_vy)) + 0.5 * (math.log(2 * math.pi) + self._log_vy)
         return mse, nll.sum(1)
+
+
+class _EncoderPart(nn.Module):
+    """ConvVAE.encode as a module owning only the encoder's parameters (for make_graphed_callables)."""
+
+    def __init__(self, vae):
+        super().__init__()
+        for n in ("conv1", "conv2", "fc1", "fc21", "fc211", "fc221"):
+            setattr(self, n, getattr(vae, n))
+        self._vae = [vae]
+
+    def forward(self, x):
+        return self._vae[0].encode(x)
+
+
+class _DecoderLossPart(nn.Module):
+    """decode + loss_function summed over images: (sum of per-image MSE, sum of per-image NLL)."""
+
+    def __init__(self, vae):
+        super().__init__()
+        for n in ("fc3", "fc31", "fc4", "deconv1", "deconv2"):
+            setattr(self, n, getattr(vae, n))
+        self._log_vy = vae._log_vy
+        self._vae = [vae]
+
+    def forward(self, z, img, mask):
+        v = self._vae[0]
+        mse, nll = v.loss_function(v.decode(z), img, mask)
+        return mse.sum(), nll.sum()
+
+
+class GraphedConvVAE:
+    """The ConvVAE's encoder and its decoder + recon loss, each replayed as a HIP graph forward and a HIP graph
+    backward (torch.cuda.make_graphed_callables: torch.cuda.CUDAGraph is a hipGraph on ROCm), for the exact-KL
+    step's ConvVAE stream.  Eager, the ConvVAE is ~100 small launches a step, which host overhead paces once
+    the GPU work per launch is small (a rank's share of the images on several GPUs).  The graphs are built on
+    first use for the batch's shapes (and rebuilt when they change); the arithmetic is the eager modules'."""
+
+    def __init__(self, vae, warmup=3):
+        self.vae = vae
+        self.warmup = warmup
+        self._key = None
+        self.enc = self.dec = None
+
+    def _build(self, img, mask):
+        n = img.shape[0]
+        L = self.vae.latent_dim
+        x = img.detach().clone()
+        z = torch.zeros(n, L, device=img.device, dtype=img.dtype, requires_grad=True)
+        m = mask.detach().clone()
+        self.enc, self.dec = torch.cuda.make_graphed_callables(
+            (_EncoderPart(self.vae), _DecoderLossPart(self.vae)), ((x,), (z, x, m)), num_warmup_iters=self.warmup)
+        self._key = (tuple(img.shape), tuple(mask.shape), img.dtype, img.device, self.vae.training)
+
+    def _ensure(self, img, mask):
+        if self._key != (tuple(img.shape), tuple(mask.shape), img.dtype, img.device, self.vae.training):
+            self._build(img, mask)
+
+    def encode(self, img, mask):
+        self._ensure(img, mask)
+        return self.enc(img)
+
+    def decode_loss(self, z, img, mask):
+        self._ensure(img, mask)
+        return self.dec(z, img, mask)
