@@ -70,7 +70,7 @@ constexpr bool kCiC16 = LVAE_CI_C16 != 0;
 // of under-filled tiles after potrf).  Same flops; the Y planes (row-major Y, read only by the doubling's
 // Y step) are not produced.
 #ifndef LVAE_CI_PIPE_MAX_L
-#define LVAE_CI_PIPE_MAX_L 4
+#define LVAE_CI_PIPE_MAX_L 2  // (scripts/inv_ab.py: L = 2 2.18 vs 2.60 ms for the inverse; L = 4 2.84 either way)
 #endif
 // the latent-dim bound of the pipelined schedule: LVAE_CI_PIPE_L overrides it for A/B runs (read once per
 // process, so the workspace size query and the calls agree)
@@ -716,7 +716,7 @@ constexpr int kCiU2 = 0, kCiU1 = 1, kCiU12 = 2;  // kCiU12: U1 (without the pivo
 constexpr int kCiFuseMaxL = 16; // latent dims per call up to which the pivot updates its own block
 template <int MODE>
 __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall, CiScratch S, int np_, int k,
-                                                        int ntl, int nwg, int n1 = 0) {
+                                                        int ntl, int nwg, int n1 = 0, int t0 = 0) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kSxPart];
   __shared__ uint32_t red;
   if (MODE != kCiU2 && threadIdx.x == 0) red = 0u;
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall
     const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
     l = wgid / ntl;
-    const int t = wgid % ntl;
+    const int t = t0 + wgid % ntl;  // (t0: the launch's first trailing tile, lookahead split)
     if constexpr (MODE == kCiU1) {
       I = (ntl == nt - k - 1) ? k + 1 + t : k + 2 + t;  // with / without the pivot block
       J = k + 1;
@@ -1444,6 +1444,8 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     // slower: the fused update launch ends later, and the next-but-one pivot waits for it -- scripts/inv_ab.py,
     // L = 2: 2.51 vs 2.18 ms for the inverse)
     static const bool pair = getenv("LVAE_CI_PAIR") && atoi(getenv("LVAE_CI_PAIR")) != 0;
+    // LVAE_CI_LOOKAHEAD=0: one update launch per pass (the next pivot then waits for the whole update)
+    static const bool la = !getenv("LVAE_CI_LOOKAHEAD") || atoi(getenv("LVAE_CI_LOOKAHEAD")) != 0;
     pipe = pmode > 0;
     if (fuse) {
       ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, L, g_pivot_prof);
@@ -1483,13 +1485,22 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
         }
         if (m + 1 < nt) {
           ci_panel_kernel<<<dim3(nt - m - 1, L), 512, 0, st>>>(S, np_, m);
-          // column m+1 without the pivot block + the trailing tiles, one launch
+          // column m+1 without the pivot block + the trailing tiles
           const int n1 = nt - m - 2, n2 = (nt - m - 2) * (nt - m - 1) / 2;
-          if (n2 > 0) {
-            ProfScope pu(LVAE_PH_SWEEP_UPD, st);
-            ci_update_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
+          if (n2 > 0 && la && n2 > 1) {
+            // lookahead split: first what pivot(m+2) reads -- column m+1 (the next C planes) and the trailing
+            // tile (m+2, m+2) (sx_tri_blocked's tile 0) -- then the rest, which runs beside pivot(m+2)
+            ProfScope pu(LVAE_PH_SWEEP_UPD, st);  // (both launches: the pass's whole trailing update)
+            ci_update_kernel<kCiU12><<<(n1 + 1) * L, 512, 0, st>>>(A, S, np_, m, 1, L, n1, 0);
+            if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
+            ci_update_kernel<kCiU12><<<(n2 - 1) * L, 512, 0, st>>>(A, S, np_, m, n2 - 1, (n2 - 1) * L, 0, 1);
+          } else {
+            if (n2 > 0) {
+              ProfScope pu(LVAE_PH_SWEEP_UPD, st);
+              ci_update_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
+            }
+            if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
           }
-          if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
         }
         if (pipe) {  // trtri by block rows beside the chain (after U2(m): off pivot(m+2)'s path)
           ProfScope pt(LVAE_PH_POTRI, st);

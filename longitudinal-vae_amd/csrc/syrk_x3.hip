@@ -24,6 +24,10 @@
 // (r3, scripts/gemm_ab.py: 3.19 vs 3.46 ms at np = 4096, L = 16 against the row-major order; 51.1 vs
 // 55.9 ms at np = 16384, L = 4).
 #include "x3_c16.hpp"
+
+#ifndef LVAE_SYRK_RESERVE
+#define LVAE_SYRK_RESERVE 0
+#endif
 #include "x3_dma.hpp"
 #include "x3_gemm4.hpp"
 
@@ -293,36 +297,58 @@ __global__ __launch_bounds__(512) void syrk_c16_kernel(const _Float16* __restric
                                                        const float* __restrict__ bsc, float* __restrict__ S,
                                                        float* __restrict__ Sx, int np_, int ntl, int nwg, int L, int ns) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[NS * kC16Stage];
-  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int sp = wgid / (ntl * L), l = (wgid / ntl) % L, nt = np_ / kSxT;
-  int I, J;
-  sx_tri_blocked(wgid % ntl, nt, I, J);
-  const int kb0 = sp * nt / ns, kb1 = (sp + 1) * nt / ns;
-  const int64_t ld = np_;
-  const int64_t base = (int64_t)l * np_ * np_, c0 = (int64_t)kb0 * (kSxT / kC16BK) * kC16Part;
-  sx_f32x16 acc[4][2];
+  // tiles v = blockIdx.x, + gridDim.x, ...: one each with the full grid (nwg workgroups); a grid of fewer
+  // (a multiple of 8: v keeps its blockIdx's XCD) leaves CUs to the ConvVAE stream (syrk_tiles_f32)
+  for (int v = blockIdx.x; v < nwg; v += gridDim.x) {
+    if (v != (int)blockIdx.x) __syncthreads();  // every wave's reads of the previous tile's stages are done
+    const int orig = v, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int sp = wgid / (ntl * L), l = (wgid / ntl) % L, nt = np_ / kSxT;
+    int I, J;
+    sx_tri_blocked(wgid % ntl, nt, I, J);
+    const int kb0 = sp * nt / ns, kb1 = (sp + 1) * nt / ns;
+    const int64_t ld = np_;
+    const int64_t base = (int64_t)l * np_ * np_, c0 = (int64_t)kb0 * (kSxT / kC16BK) * kC16Part;
+    sx_f32x16 acc[4][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
-  if (kb1 > kb0) {
-    const int64_t pa = c16_panel(l, np_, I) + c0, pb = c16_panel(l, np_, J) + c0;
-    c16_gemm<NS>(C16Opnd{Bh + pa, Bl - Bh, 0}, C16Opnd{Bh + pb, Bl - Bh, 0}, (kb1 - kb0) * (kSxT / kC16BK), lds, acc);
+      for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+    if (kb1 > kb0) {
+      const int64_t pa = c16_panel(l, np_, I) + c0, pb = c16_panel(l, np_, J) + c0;
+      c16_gemm<NS>(C16Opnd{Bh + pa, Bl - Bh, 0}, C16Opnd{Bh + pb, Bl - Bh, 0}, (kb1 - kb0) * (kSxT / kC16BK), lds, acc);
+    }
+    const float sc = bsc[l], inv = 1.0f / (sc * sc);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float* C = (sp == 0 ? S : Sx + (int64_t)(sp - 1) * L * np_ * np_) + base + (int64_t)I * kSxT * ld + J * kSxT;
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+    const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), rc, vo,
+                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
   }
-  const float sc = bsc[l], inv = 1.0f / (sc * sc);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float* C = (sp == 0 ? S : Sx + (int64_t)(sp - 1) * L * np_ * np_) + base + (int64_t)I * kSxT * ld + J * kSxT;
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
-  const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int e = 0; e < 16; ++e)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * inv), rc, vo,
-                                              ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, 0);
+}
+
+// CUs the S GEMM leaves free when its tiles outnumber the chip (LVAE_SYRK_RESERVE, default below): the
+// exact KL's backward runs the S GEMM on the caller's stream while the encoder backward runs on the ConvVAE
+// stream; with one 160 KB-LDS workgroup on every CU those small kernels wait for whole S-GEMM tiles
+static int syrk_grid(int nwg) {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    hipDeviceProp_t pr;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) ? pr.multiProcessorCount
+                                                                                                : 256;
+  }
+  static const int reserve = getenv("LVAE_SYRK_RESERVE") ? atoi(getenv("LVAE_SYRK_RESERVE")) : LVAE_SYRK_RESERVE;
+  if (reserve <= 0 || nwg <= cus) return nwg;
+  const int g = (cus - reserve) / 8 * 8;
+  return g >= 8 ? g : nwg;
 }
 
 int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st) {
@@ -332,7 +358,8 @@ int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, flo
   if (ns > 1 && !Sx) return -2;
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L * ns;
   if (kCiBC16)
-    syrk_c16_kernel<kC16NS><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
+    syrk_c16_kernel<kC16NS><<<syrk_grid(nwg), 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl,
+                                                            nwg, L, ns);
   else
     syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
   LVAE_CHECK_LAUNCH();

@@ -220,15 +220,16 @@ class LatentShardedClosedStep:
             gmv[:, L + d0:L + d1] = lv_own.grad.to(gmv.dtype)
         vst.wait_stream(main)
         gmv.record_stream(vst)
+        # ... then the hyper-parameter half (S GEMM + Gram adjoint: a few launches) is ENQUEUED first, so that
+        # the GPU starts it while the host is still issuing the encoder backward's ~40 small kernels ...
+        if own and self.hyper_params:
+            torch.autograd.backward(tail, inputs=self.hyper_params)
         with torch.cuda.stream(vst):
-            # ... so that the all-reduce and the encoder backward run on the ConvVAE stream beside the
-            # hyper-parameter half below
+            # ... and the all-reduce and the encoder backward run on the ConvVAE stream beside it
             self._all_reduce(gmv)
             g_loc = gmv[r * n_loc:(r + 1) * n_loc]
             gz = z_d.grad
             ((z * gz).sum() + (mu * g_loc[:, :L]).sum() + (log_var * g_loc[:, L:]).sum()).backward()
-        if own and self.hyper_params:
-            torch.autograd.backward(tail, inputs=self.hyper_params)  # S GEMM + Gram adjoint
         main.wait_stream(vst)
         for t in (recon_loss, nll_loss):
             t.record_stream(main)

@@ -834,3 +834,46 @@ def test_closed_step_three_epochs_vs_reference(hip):
     sd = dict(vae.named_parameters())
     for name in ("conv1.weight", "fc211.bias", "deconv2.weight", "_log_vy"):
         assert rel(sd[name], g["vae_" + name]) < 1e-5, name
+
+
+def test_kl_factor_single_use_and_rank_share_rehearsal(hip):
+    """(1) A KLFactor is consumed by its reduce (the backward overwrites its operands): a second
+    KL_closed_batched(..., factor=) on it raises.  (2) The rank-share rehearsal (LatentShardedClosedStep
+    with sim_world = 2: rank 0's dims and images, collectives replaced by local stand-ins -- bench.py
+    --rank-share) returns the KL of its own dims over the stand-in all-gather (its rows tiled), which the
+    batched KL of those rows reproduces."""
+    import lvae_amd as la
+    from lvae_amd.distributed import LatentShardedClosedStep
+    from lvae_amd.elbo import kl_closed_prefactor
+    from lvae_amd.vae import ConvVAE
+    from lvae_amd.data import health_mnist_batch
+    L, P, T = 4, 32, 16
+    img, mask, X = health_mnist_batch(P, T, seed=5, device=DEV)
+    k = la.generate_kernel(**CFG, latent_dim=L).to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+    mu = torch.randn(P * T, L, device=DEV, dtype=torch.float64)
+    lv = 0.1 * torch.randn(P * T, L, device=DEV, dtype=torch.float64)
+    f = kl_closed_prefactor(k, X, lik, L, torch.cuda.current_stream())
+    kl1 = la.KL_closed_batched(k, X, lik, mu, lv, factor=f)
+    kl0 = la.KL_closed_batched(k, X, lik, mu, lv)
+    assert rel(kl1, kl0) < 1e-6
+    with pytest.raises(RuntimeError, match="already used"):
+        la.KL_closed_batched(k, X, lik, mu, lv, factor=f)
+    # the rank-share rehearsal, rank 0 of 2
+    torch.manual_seed(3)
+    vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+    opt = torch.optim.SGD(list(vae.parameters()) + list(k.parameters()), lr=0.0)
+    W, n = 2, P * T // 2
+    eps = torch.randn(n, L, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    step = LatentShardedClosedStep(vae, k, lik, opt, weight=0.15, loss_function="mse", sim_world=W)
+    net, rl, nl, gp = step(img[:n], mask[:n], X, eps)
+    with torch.no_grad():
+        m_, v_ = vae.encode(img[:n])
+        full = torch.cat([m_, v_], 1).repeat(W, 1).double()
+    spec, params = la.kernel_spec_and_params(k)
+    from lvae_amd.elbo import _kl_closed_apply, _noise_vector
+    with torch.no_grad():
+        nz = _noise_vector(lik, L).to(params.device)
+        ref = _kl_closed_apply(params[:L // W], nz[:L // W], full[:, :L // W], full[:, L:L + L // W], X, spec, None)
+    assert torch.isfinite(torch.stack([net, rl, nl, gp])).all()
+    assert rel(gp * L, ref.sum()) < 1e-6
