@@ -46,7 +46,7 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3s3f_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r4_pmc_summary.json")
 # The committed rocprofv3 --kernel-trace --stats summary of the default closed bench on the final tree
 # (scripts/gpu_r4a.sh): the roofline's `frac` is priced on its average launch duration of the dominant
 # kernel, so that it recomputes from profiles/; the live HIP-event figure is reported beside it.
@@ -177,10 +177,12 @@ def max_over_ranks(x, world, dev):
 # ------------------------------------------------------------------------------------------
 # CPU baselines (the oracle, fp64 torch-CPU, the reference's op sequence) -- rank 0, N = 1 only
 # ------------------------------------------------------------------------------------------
-def cpu_baseline_closed(P, T, L, threads8_dims=1):
-    """All L latent dims of the C3 step: ConvVAE fwd/bwd on all N images + KL_closed fwd/bwd of
-    every dim (fp64), timed once at the box's thread count; plus an 8-thread figure (ConvVAE + one
-    dim, extrapolated to L dims) for comparison with the survey container's numbers."""
+def cpu_baseline_closed(P, T, L, threads8_dims=1, reps=3):
+    """The C3 step on the CPU port (fp64), by BASELINE.md's method bounded to ~25 s: one warm-up, then
+    the median of `reps` timings of the ConvVAE fwd/bwd on all N images and of one latent dim's
+    KL_closed fwd/bwd (every dim costs the same: same N, same kernel), the step = ConvVAE + L x dim;
+    plus an 8-thread figure (ConvVAE + one dim, x L dims) for comparison with the survey container's
+    numbers."""
     from oracle import lvae_oracle as O
     from lvae_amd.data import health_mnist_batch
     img, mask, X = health_mnist_batch(P, T, seed=0, dtype=torch.float64)
@@ -191,7 +193,7 @@ def cpu_baseline_closed(P, T, L, threads8_dims=1):
     N = P * T
     eps = torch.randn(N, L, dtype=torch.float64)
 
-    def step(dims):
+    def step(dims, l0=0):
         t0 = time.perf_counter()
         mu, logv = vae.encode(img)
         recon = vae.decode(mu + eps * torch.exp(0.5 * logv))
@@ -199,19 +201,23 @@ def cpu_baseline_closed(P, T, L, threads8_dims=1):
         mse.sum().backward(retain_graph=True)
         t_vae = time.perf_counter() - t0
         t0 = time.perf_counter()
-        for l in range(dims):
-            r = raw[l].clone().requires_grad_()
-            m_ = mu[:, l].detach().clone().requires_grad_()
-            v_ = logv[:, l].detach().clone().requires_grad_()
+        for l in range(l0, l0 + dims):
+            r = raw[l % L].clone().requires_grad_()
+            m_ = mu[:, l % L].detach().clone().requires_grad_()
+            v_ = logv[:, l % L].detach().clone().requires_grad_()
             O.kl_closed(spec, O.constrain(r), X, 1.0, m_, v_).backward()
         return t_vae, time.perf_counter() - t0
 
     nthreads = torch.get_num_threads()
-    t_vae, t_kl = step(L)
-    t_step = t_vae + t_kl
+    step(1)  # warm-up (allocator, thread pool, first touch)
+    runs = [step(1, l0=1 + k) for k in range(reps)]
+    t_vae = sorted(r[0] for r in runs)[reps // 2]
+    t_dim = sorted(r[1] for r in runs)[reps // 2]
+    t_step = t_vae + L * t_dim
     res = dict(value=1.0 / t_step, unit="ELBO-steps/s", cores=nthreads, kind="port",
-               sample=(f"oracle fp64 torch-CPU, {nthreads} threads: ConvVAE fwd/bwd on all {N} images ({t_vae:.2f} s) "
-                       f"+ KL_closed fwd/bwd of all {L} latent dims ({t_kl:.2f} s) = {t_step:.1f} s per step"))
+               sample=(f"oracle fp64 torch-CPU, {nthreads} threads, median of {reps} after 1 warm-up: ConvVAE "
+                       f"fwd/bwd on all {N} images ({t_vae:.2f} s) + KL_closed fwd/bwd of one latent dim "
+                       f"({t_dim:.2f} s) x {L} dims = {t_step:.1f} s per step"))
     try:
         torch.set_num_threads(8)
         v8, k8 = step(threads8_dims)

@@ -152,6 +152,14 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
                                  const double* params, const double* gkl, double* dparams, double* dnoise,
                                  void* workspace, void* stream);
 
+/* diag(K^-1) in fp64 for ill-conditioned dims (kl_refine.hip): the reduce estimates each dim's
+ * diagonal error by est_l = max_i K_ii max_i (K^-1)_ii and where est_l > tau (env LVAE_KL_REFINE_TAU,
+ * default 16; LVAE_KL_REFINE=0 never, =1 always) replaces diag K^-1 by one fp64 Newton step,
+ * 2 X_jj - (X K X)_jj (the trace term and dlogv; the reference's cholesky_solve(I) is fp64,
+ * elbo_functions.py:27-31).  This copies the last reduce's est [L] (fp64) and flag [L] (int32, 1:
+ * refined) to device buffers, on `stream`.  No reference counterpart (diagnostic).                  */
+int lvae_kl_closed_refine_state(int n, int L, const void* workspace, double* est, int32_t* flag, void* stream);
+
 /* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
  * 256-wide pivot blocks (the r1-r2 Regime B inverse; lvae_kl_closed_* now use lvae_spd_inv_chol_f32's
  * blocked Cholesky, which is ~100x more accurate at cond 1e5; kept as a C-ABI entry): per pivot block k,

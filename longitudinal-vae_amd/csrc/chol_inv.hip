@@ -1444,8 +1444,11 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     // slower: the fused update launch ends later, and the next-but-one pivot waits for it -- scripts/inv_ab.py,
     // L = 2: 2.51 vs 2.18 ms for the inverse)
     static const bool pair = getenv("LVAE_CI_PAIR") && atoi(getenv("LVAE_CI_PAIR")) != 0;
-    // LVAE_CI_LOOKAHEAD=0: one update launch per pass (the next pivot then waits for the whole update)
-    static const bool la = !getenv("LVAE_CI_LOOKAHEAD") || atoi(getenv("LVAE_CI_LOOKAHEAD")) != 0;
+    // LVAE_CI_LOOKAHEAD=1: each pass's trailing update in two launches, the next pivot's column first (the
+    // next pivot waits only for that part).  Measured slower (scripts/inv_ab.py, inverse alone: L = 16
+    // 5.70 vs 5.59 ms, L = 8 3.60 vs 3.53, L = 4 2.85 vs 2.87; profiles/r4_lookahead_ab.txt): the second
+    // launch's tail and the extra launch outweigh the earlier pivot start.  Off by default.
+    static const bool la = getenv("LVAE_CI_LOOKAHEAD") && atoi(getenv("LVAE_CI_LOOKAHEAD")) != 0;
     pipe = pmode > 0;
     if (fuse) {
       ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, L, g_pivot_prof);

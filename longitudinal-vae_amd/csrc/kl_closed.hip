@@ -57,6 +57,11 @@ size_t kl_resid_bins_bytes(int np_, int L, int ncomp);
 bool kl_resid_bins_enabled(const lvae_kernel_spec* spec, int n);
 int kl_resid_bins_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, void* wsbuf,
                        hipStream_t st);
+size_t kl_refine_bytes(int np_, int L);
+size_t kl_refine_part_bytes(int np_, int L);
+int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                   const double* params, const double* noise, const float* Kinv, double* kdiag, double* K64,
+                   double* part, double* est, int* flag, hipStream_t st);
 
 struct KLWorkspace {
   float *A, *Kinv, *v, *sv;
@@ -69,6 +74,9 @@ struct KLWorkspace {
   double *mu, *alpha, *res, *kdiag, *logdet, *part, *rpart;
   int* covflag;      // 1: integer covariates (the Gram kernels' fp32 covariate path; set by the factor)
   char* rb;          // the binned residual's plan / bin sums (kl_resid_bins.hip)
+  double* K64;       // [L, np, np] fp64 K of the dims whose diag K^-1 is refined (kl_refine.hip)
+  double* rest;      // [L] the refinement gate's estimate max K_ii max (K^-1)_ii
+  int* rflag;        // [L] 1: diag K^-1 refined
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
     size_t off = 0;
@@ -97,6 +105,9 @@ struct KLWorkspace {
     covflag = (int*)take(sizeof(int));
     rb = take(kl_resid_bins_bytes(np_, L, LVAE_MAX_COMP));
     Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
+    K64 = (double*)take(kl_refine_bytes(np_, L));
+    rest = (double*)take((size_t)L * sizeof(double));
+    rflag = (int*)take((size_t)L * sizeof(int));
     bytes = off;
   }
 };
@@ -354,6 +365,10 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
     kl_alpha_sym_kernel<<<dim3(G, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.rpart, ntiles);
     kl_alpha_reduce<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.rpart, ws.alpha, np_, ws.alpha);
   }
+  // diag K^-1 in fp64 for the dims whose max K_ii max (K^-1)_ii says the fp32 inverse's diagonal is not
+  // enough (kl_refine.hip; the partials buffer is free again)
+  LVAE_TRY(kl_refine_diag(spec, x, ldx, n, np_, L, params, noise, ws.Kinv, ws.kdiag, ws.K64, ws.rpart, ws.rest,
+                          ws.rflag, st));
   kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
   LVAE_CHECK_LAUNCH();
   return 0;
@@ -424,6 +439,20 @@ int lvae_kl_closed_bwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
   (void)mu;
   LVAE_TRY(lvae_kl_closed_bwd_latent_f32(n, L, logv, ld_mu, gkl, dmu, dlogv, workspace, stream));
   return lvae_kl_closed_bwd_hyper_f32(spec, x, ldx, n, L, params, gkl, dparams, dnoise, workspace, stream);
+}
+
+int lvae_kl_closed_refine_state(int n, int L, const void* workspace, double* est, int32_t* flag, void* stream) {
+  if (n <= 0) return -1;
+  if (L <= 0) return -2;
+  if (!workspace || ((uintptr_t)workspace & 255)) return -3;
+  if (!est || !flag) return -4;
+  const int np_ = lvae_kl_closed_padded_n(n);
+  KLWorkspace ws((char*)workspace, np_, L);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(est, ws.rest, (size_t)L * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(flag, ws.rflag, (size_t)L * sizeof(int32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return LVAE_ERR_LAUNCH;
+  return 0;
 }
 
 const char* lvae_version(void) { return "lvae_hip 0.1.0 gfx950"; }

@@ -4,6 +4,7 @@ Each function takes the same arguments as its reference twin and returns autogra
 tensors; the arithmetic runs in the HIP library through a ``torch.autograd.Function`` whose
 backward is the analytic adjoint (also HIP).  No PyTorch / CPU fallback exists.
 """
+import contextlib
 import os
 
 import torch
@@ -139,6 +140,31 @@ class _KLState:
     n = L = 0
 
 
+_refine_log = None  # a list while kl_closed_refine_log() is active
+
+
+@contextlib.contextmanager
+def kl_closed_refine_log():
+    """Yields a list that gets, per KL_closed forward inside the block, the fp64 diag(K^-1) refinement's
+    gate (kl_refine.hip): (est [L] fp64 = max K_ii max (K^-1)_ii, the proxy of the fp32 inverse's
+    diagonal error; flag [L] int32, 1 where diag K^-1 was refined in fp64).  Device tensors, filled in
+    stream order."""
+    global _refine_log
+    prev, _refine_log = _refine_log, []
+    try:
+        yield _refine_log
+    finally:
+        _refine_log = prev
+
+
+def _log_refine(lib, ws, n, L, dev):
+    est = torch.zeros(L, dtype=torch.float64, device=dev)
+    flag = torch.zeros(L, dtype=torch.int32, device=dev)
+    _lib.check(lib.lvae_kl_closed_refine_state(n, L, _lib.ptr(ws), _lib.ptr(est), _lib.ptr(flag), _lib.stream_ptr()),
+               "kl_closed_refine_state")
+    _refine_log.append((est, flag))
+
+
 class _KLHyperFn(torch.autograd.Function):
     """A zero-valued [L] term carrying d kl / d (params, noise) (lvae_kl_closed_bwd_hyper_f32: the S GEMM
     and the Gram adjoint, ~all of the KL backward's time) as a node of its own.  Created before the
@@ -205,6 +231,8 @@ class _KLClosedFn(torch.autograd.Function):
                                             _lib.ptr(ws), need_bwd, _lib.stream_ptr())
             _lib.check(rc, "kl_closed_fwd")
         _check_info(info, "KL_closed cholesky")
+        if _refine_log is not None:
+            _log_refine(lib, ws, n, L, dev)
         state.ws, state.p, state.x64, state.spec, state.n, state.L = ws, p, x64, spec, n, L
         ctx.save_for_backward(lv64, ws)
         ctx.in_dtypes = (mu.dtype, logv.dtype)
