@@ -37,3 +37,7 @@ grep -i "syrk" $OUT/pmc/pmc_summary.txt | head -4
 echo "[$(date +%T)] default bench"
 timeout -k 10 600 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('$OUT/bench.json')); print(d['value'], d['ms_per_step'], json.dumps(d['roofline'])[:700]); print(json.dumps(d.get('c2'))[:500])"
+echo "[$(date +%T)] closed bench with every dim's diag(K^-1) refined (LVAE_KL_REFINE=1: the cost of the fp64 path)"
+LVAE_KL_REFINE=1 timeout -k 10 300 python3 bench.py --regime closed --steps 5 --warmup 2 --no-cpu-baseline --no-c2 \
+  > $OUT/b_refine_all.json 2> $OUT/b_refine_all.err || { tail -20 $OUT/b_refine_all.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/b_refine_all.json')); print('refine-all', round(d['ms_per_step'],3), 'ms', {k: round(v,3) for k,v in d.get('phase_ms_per_step',{}).items()})"
