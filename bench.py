@@ -160,6 +160,59 @@ def host_info():
     return info
 
 
+class ClockSampler:
+    """The GFX clock of this process's GPU (amdsmi, matched by PCI bus) sampled by a thread every
+    `period` s while the timed steps run: the evidence for kernel averages that differ between runs (a
+    rocprofv3-traced run against an untraced one).  Reports nothing if amdsmi or the match is missing;
+    LVAE_BENCH_CLOCKS=0 switches it off."""
+
+    def __init__(self, dev, period=0.02):
+        import threading
+        self.samples, self.h, self.period = [], None, period
+        self._stop = threading.Event()
+        self._thread = None
+        if os.environ.get("LVAE_BENCH_CLOCKS", "1") == "0":
+            return
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            props = torch.cuda.get_device_properties(dev)
+            bus = getattr(props, "pci_bus_id", None)
+            for h in amdsmi.amdsmi_get_processor_handles():
+                if bus is not None and int(amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")[1], 16) == bus:
+                    self.h, self._smi = h, amdsmi
+        except Exception as e:  # noqa: BLE001 -- diagnostics only
+            log(f"clock sampler off: {e}")
+
+    def _run(self):
+        smi = self._smi
+        while not self._stop.is_set():
+            try:
+                self.samples.append(smi.amdsmi_get_clock_info(self.h, smi.AmdSmiClkType.GFX)["clk"])
+            except Exception:  # noqa: BLE001
+                return
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self.h is not None:
+            import threading
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join()
+
+    def record(self):
+        v = sorted(x for x in self.samples if isinstance(x, (int, float)))
+        if not v:
+            return None
+        return {"gfx_mhz_median": v[len(v) // 2], "gfx_mhz_min": v[0], "gfx_mhz_max": v[-1], "samples": len(v),
+                "source": f"amdsmi GFX clock of this GPU every {1000 * self.period:.0f} ms over the timed steps"}
+
+
 def sync_barrier(world):
     if world > 1:
         dist.barrier()
@@ -317,12 +370,17 @@ def run_closed(args, world, rank, dev):
     if not args.no_phase_timing and not use_graph:
         _lib.prof_enable(True)
         _lib.prof_collect()
+    clocks = ClockSampler(dev) if rank == 0 else None
     sync_barrier(world)
+    if clocks:
+        clocks.__enter__()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = run()
     sync_barrier(world)
     elapsed = time.perf_counter() - t0
+    if clocks:
+        clocks.__exit__(None, None, None)
     if use_graph:
         graph.check()
     phase = {}
@@ -360,6 +418,8 @@ def run_closed(args, world, rank, dev):
                                       if world == 1 else
                                       f"latent dims sharded over {world} ranks ({Lr} dims/rank on rank 0), images "
                                       f"split {N // world}/rank, 1 all-gather + 2 all-reduces per step")}}
+    if clocks and clocks.record():
+        res["clock"] = clocks.record()
     if phase and Lr > 0:
         np_ = _lib.load().lvae_kl_closed_padded_n(N)
         potrf_ms = phase["potrf"][0] / args.steps
