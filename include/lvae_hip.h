@@ -324,6 +324,37 @@ int lvae_prof_collect(double* ms, int32_t* count, int n_phases);
 /* library identification: "lvae_hip <version> gfx950" */
 const char* lvae_version(void);
 
+/* ---------------------------------------------------------------------------------------- */
+/* Glue (glue.hip): the elementwise pieces around the GP and ConvVAE kernels, one launch each    */
+/* instead of a chain of framework ops (the steps are launch-paced at small shares).            */
+/* ---------------------------------------------------------------------------------------- */
+/* ConvVAE.loss_function (VAE.py:144-162) on [B, d] fp32 recon / x / mask, log_vy [d]:
+ *   mse[i] = sum_j m (r - x)^2 / (sum_j m, or 1 where that is 0),
+ *   nll[i] = sum_j (m (r - x)^2 / (2 exp(log_vy_j)) + (log 2 pi + log_vy_j) / 2);  msum[i] saved for the
+ * backward.  The backward takes d mse / d nll (element i at g[i * stride]; stride 0 broadcasts) and writes
+ * d recon [B, d] and per-pixel partials of d log_vy, dlv_part [lvae_vae_loss_bwd_partials(B), d] (their
+ * column sums are d log_vy).                                                                     */
+int lvae_vae_loss_fwd_f32(const float* recon, const float* x, const float* mask, const float* log_vy, int B, int d,
+                          float* mse, float* nll, float* msum, void* stream);
+size_t lvae_vae_loss_bwd_partials(int B);
+int lvae_vae_loss_bwd_f32(const float* recon, const float* x, const float* mask, const float* log_vy, const float* msum,
+                          const float* g_mse, int64_t g_mse_stride, const float* g_nll, int64_t g_nll_stride, int B,
+                          int d, float* d_recon, float* dlv_part, void* stream);
+/* ConvVAE.sample_latent (VAE.py:132-136): z = mu + eps exp(log_var / 2), n fp32 elements; backward
+ * d log_var = d z eps exp(log_var / 2) / 2 (d mu = d z).                                         */
+int lvae_reparam_fwd_f32(const float* mu, const float* log_var, const float* eps, int64_t n, float* z, void* stream);
+int lvae_reparam_bwd_f32(const float* gz, const float* log_var, const float* eps, int64_t n, float* g_log_var,
+                         void* stream);
+/* The kernels' positivity transform exp(m + softplus(raw - m)) (GP_model.py:31-144) of n_raw [L] fp64
+ * parameter tensors into column cols[k] of the [L, P] fp64 matrix out (other columns 1; raws[k], mlogs[k]:
+ * host arrays of device pointers, mlogs[k] -> the [1] floor m).  Backward: grad [n_raw, L] =
+ * g[l, cols[k]] exp(m + softplus(t)) sigmoid(t), t = raw - m (g element (l, p) at g[l s0 + p s1]).       */
+int lvae_param_pack_fwd_f64(int n_raw, int L, int P, const int* cols, const double* const* raws,
+                            const double* const* mlogs, double* out, void* stream);
+int lvae_param_pack_bwd_f64(int n_raw, int L, int P, const int* cols, const double* const* raws,
+                            const double* const* mlogs, const double* g, int64_t g_stride0, int64_t g_stride1,
+                            double* grad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

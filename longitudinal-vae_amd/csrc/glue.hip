@@ -1,0 +1,211 @@
+// glue.hip -- the small elementwise pieces around the GP and ConvVAE kernels, one launch each instead of the
+// chains of PyTorch ops they replace (the steps are launch-paced at a rank's share of the exact-KL step and
+// in the graphed Hensman step, where every op is a ~4.5 us kernel on one queue):
+//
+//   vae_loss        per-image masked MSE and Gaussian NLL (VAE.py:144-162): one workgroup per image;
+//                   backward: d recon and the per-pixel d log_vy partials in one pass over (pixel, image
+//                   chunk) tiles
+//   reparam         z = mu + eps exp(log_var / 2) (VAE.py:132-136); backward: d log_var (d mu = d z)
+//   param_pack      the kernel hyper-parameters exp(m + softplus(raw - m)) (GP_model.py:31-144's
+//                   positivity transform) gathered from their separate [L] tensors into the [L, P] matrix
+//                   the GP kernels read; backward: d raw, scattered back per tensor
+#include "common.hpp"
+
+namespace lvae {
+
+constexpr float kLog2Pi = 1.8378770664093453f;  // log(2 pi)
+
+// mse[i] = sum_j m (r - x)^2 / max(sum_j m, 1 if 0); nll[i] = sum_j m (r - x)^2 / (2 e^lv_j) + (log 2pi + lv_j) / 2
+__global__ __launch_bounds__(256) void vae_loss_fwd_kernel(const float* __restrict__ r, const float* __restrict__ x,
+                                                           const float* __restrict__ m, const float* __restrict__ lv,
+                                                           int d, float* __restrict__ mse, float* __restrict__ nll,
+                                                           float* __restrict__ msum) {
+  __shared__ float red[3][4];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int64_t o = (int64_t)i * d;
+  float se = 0.f, ms = 0.f, nl = 0.f;
+  for (int j = tid; j < d; j += 256) {
+    const float df = r[o + j] - x[o + j], mk = m[o + j], l = lv[j];
+    const float s = df * df * mk;
+    se += s;
+    ms += mk;
+    nl += s / (2.f * expf(l)) + 0.5f * (kLog2Pi + l);
+  }
+  se = wave_sum(se);
+  ms = wave_sum(ms);
+  nl = wave_sum(nl);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = se;
+    red[1][tid >> 6] = ms;
+    red[2][tid >> 6] = nl;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float S = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    float M = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    M = M == 0.f ? 1.f : M;
+    mse[i] = S / M;
+    nll[i] = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
+    msum[i] = M;
+  }
+}
+
+// grid (cdiv(d, 256), cdiv(B, kLossChunk)): thread j of chunk c writes d recon[i, j] for the chunk's images
+// and the partial dlv_part[c][j] = sum_i g_nll[i] (1/2 - m (r - x)^2 / (2 e^lv_j))
+constexpr int kLossChunk = 64;
+__global__ __launch_bounds__(256) void vae_loss_bwd_kernel(const float* __restrict__ r, const float* __restrict__ x,
+                                                           const float* __restrict__ m, const float* __restrict__ lv,
+                                                           const float* __restrict__ msum, const float* __restrict__ gm,
+                                                           int64_t gms, const float* __restrict__ gn, int64_t gns,
+                                                           int B, int d, float* __restrict__ dr,
+                                                           float* __restrict__ dlv_part) {
+  const int j = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+  if (j >= d) return;
+  const float ie = 1.f / (2.f * expf(lv[j]));
+  const int i1 = min(B, (c + 1) * kLossChunk);
+  float acc = 0.f;
+  for (int i = c * kLossChunk; i < i1; ++i) {
+    const int64_t o = (int64_t)i * d + j;
+    const float df = r[o] - x[o], mk = m[o], g_m = gm[i * gms], g_n = gn[i * gns];
+    dr[o] = 2.f * df * mk * (g_m / msum[i] + g_n * ie);
+    acc += g_n * (0.5f - df * df * mk * ie);
+  }
+  dlv_part[(int64_t)c * d + j] = acc;
+}
+
+__global__ void reparam_fwd_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
+                                   const float* __restrict__ eps, int64_t n, float* __restrict__ z) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) z[e] = mu[e] + eps[e] * expf(0.5f * lv[e]);
+}
+
+__global__ void reparam_bwd_kernel(const float* __restrict__ gz, const float* __restrict__ lv,
+                                   const float* __restrict__ eps, int64_t n, float* __restrict__ glv) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) glv[e] = 0.5f * gz[e] * eps[e] * expf(0.5f * lv[e]);
+}
+
+struct ParamPack {
+  int n_raw, L, P;
+  int col[64];               // column of raw k in the [L, P] matrix (other columns: 1)
+  const double* raw[64];     // [L] each
+  const double* mlog[64];    // [1] each: the transform's floor m (log space)
+};
+
+// softplus(t) = max(t, 0) + log1p(exp(-|t|)) (PyTorch's threshold 20 form agrees to fp64 rounding)
+__device__ inline double softplus64(double t) { return t > 20.0 ? t : log1p(exp(t)); }
+
+__global__ void param_pack_fwd_kernel(ParamPack pk, double* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= pk.L * pk.P) return;
+  const int l = e / pk.P, p = e % pk.P;
+  double v = 1.0;
+  for (int k = 0; k < pk.n_raw; ++k)
+    if (pk.col[k] == p) {
+      const double mm = pk.mlog[k][0];
+      v = exp(mm + softplus64(pk.raw[k][l] - mm));
+    }
+  out[e] = v;
+}
+
+// d raw_k[l] = g[l, col_k] exp(m + softplus(t)) sigmoid(t), t = raw - m;  grad [n_raw, L]
+__global__ void param_pack_bwd_kernel(ParamPack pk, const double* __restrict__ g, int64_t gs0, int64_t gs1,
+                                      double* __restrict__ grad) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= pk.n_raw * pk.L) return;
+  const int k = e / pk.L, l = e % pk.L;
+  const double mm = pk.mlog[k][0], t = pk.raw[k][l] - mm;
+  const double z = exp(t), sig = t > 20.0 ? 1.0 : z / (z + 1.0);  // (PyTorch's softplus backward)
+  grad[e] = g[l * gs0 + (int64_t)pk.col[k] * gs1] * exp(mm + softplus64(t)) * sig;
+}
+
+}  // namespace lvae
+
+using namespace lvae;
+
+extern "C" {
+
+int lvae_vae_loss_fwd_f32(const float* recon, const float* x, const float* mask, const float* log_vy, int B, int d,
+                          float* mse, float* nll, float* msum, void* stream) {
+  if (!recon || !x || !mask || !log_vy || !mse || !nll || !msum) return -1;
+  if (B < 0 || d <= 0) return -2;
+  if (B == 0) return 0;
+  vae_loss_fwd_kernel<<<B, 256, 0, (hipStream_t)stream>>>(recon, x, mask, log_vy, d, mse, nll, msum);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t lvae_vae_loss_bwd_partials(int B) { return (size_t)((B + kLossChunk - 1) / kLossChunk); }
+
+int lvae_vae_loss_bwd_f32(const float* recon, const float* x, const float* mask, const float* log_vy, const float* msum,
+                          const float* g_mse, int64_t g_mse_stride, const float* g_nll, int64_t g_nll_stride, int B,
+                          int d, float* d_recon, float* dlv_part, void* stream) {
+  if (!recon || !x || !mask || !log_vy || !msum || !g_mse || !g_nll || !d_recon || !dlv_part) return -1;
+  if (B < 0 || d <= 0) return -2;
+  if (B == 0) return 0;
+  const dim3 grid(cdiv(d, 256), cdiv(B, kLossChunk));
+  vae_loss_bwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(recon, x, mask, log_vy, msum, g_mse, g_mse_stride, g_nll,
+                                                             g_nll_stride, B, d, d_recon, dlv_part);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_reparam_fwd_f32(const float* mu, const float* log_var, const float* eps, int64_t n, float* z, void* stream) {
+  if (!mu || !log_var || !eps || !z) return -1;
+  if (n < 0) return -2;
+  if (n == 0) return 0;
+  reparam_fwd_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(mu, log_var, eps, n, z);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_reparam_bwd_f32(const float* gz, const float* log_var, const float* eps, int64_t n, float* g_log_var,
+                         void* stream) {
+  if (!gz || !log_var || !eps || !g_log_var) return -1;
+  if (n < 0) return -2;
+  if (n == 0) return 0;
+  reparam_bwd_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(gz, log_var, eps, n, g_log_var);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+static int param_pack_make(int n_raw, int L, int P, const int* cols, const double* const* raws,
+                           const double* const* mlogs, ParamPack& pk) {
+  if (n_raw < 0 || n_raw > 64 || L <= 0 || P <= 0 || P > 64) return -2;
+  if (n_raw > 0 && (!cols || !raws || !mlogs)) return -1;
+  pk.n_raw = n_raw;
+  pk.L = L;
+  pk.P = P;
+  for (int k = 0; k < n_raw; ++k) {
+    if (!raws[k] || !mlogs[k] || cols[k] < 0 || cols[k] >= P) return -3;
+    pk.col[k] = cols[k];
+    pk.raw[k] = raws[k];
+    pk.mlog[k] = mlogs[k];
+  }
+  return 0;
+}
+
+int lvae_param_pack_fwd_f64(int n_raw, int L, int P, const int* cols, const double* const* raws,
+                            const double* const* mlogs, double* out, void* stream) {
+  if (!out) return -1;
+  ParamPack pk;
+  LVAE_TRY(param_pack_make(n_raw, L, P, cols, raws, mlogs, pk));
+  param_pack_fwd_kernel<<<cdiv((int64_t)L * P, 256), 256, 0, (hipStream_t)stream>>>(pk, out);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_param_pack_bwd_f64(int n_raw, int L, int P, const int* cols, const double* const* raws,
+                            const double* const* mlogs, const double* g, int64_t g_stride0, int64_t g_stride1,
+                            double* grad, void* stream) {
+  if (!g || !grad) return -1;
+  ParamPack pk;
+  LVAE_TRY(param_pack_make(n_raw, L, P, cols, raws, mlogs, pk));
+  if (n_raw == 0) return 0;
+  param_pack_bwd_kernel<<<cdiv((int64_t)n_raw * L, 256), 256, 0, (hipStream_t)stream>>>(pk, g, g_stride0, g_stride1,
+                                                                                        grad);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

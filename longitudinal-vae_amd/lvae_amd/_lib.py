@@ -93,6 +93,13 @@ SIGNATURES = {
     "lvae_kl_closed_bwd_latent_f32": (_I32, [_I32, _I32, _VP, _I32, _VP, _VP, _VP, _VP, _VP]),
     "lvae_kl_closed_bwd_hyper_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_kl_closed_refine_state": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP]),
+    "lvae_vae_loss_fwd_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _VP, _VP, _VP, _VP]),
+    "lvae_vae_loss_bwd_partials": (_SZ, [_I32]),
+    "lvae_vae_loss_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _VP]),
+    "lvae_reparam_fwd_f32": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
+    "lvae_reparam_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
+    "lvae_param_pack_fwd_f64": (_I32, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
+    "lvae_param_pack_bwd_f64": (_I32, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "lvae_spd_inv_small_f64": (_I32, [_I32, _I32, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),
     "lvae_gemm_small_f64": (_I32, [_I32, _I32, _I32, _I32, _I32, _D, _VP, _I32, _I64, _I64, _VP, _I32, _I64,
                                    _I64, _D, _VP, _I32, _I64, _I64, _I32, _I32, _VP]),

@@ -9,6 +9,7 @@ The arithmetic never runs in PyTorch: a kernel compiles itself into an ``lvae_ke
 (component list) plus a ``[L, P]`` parameter matrix, and the Gram / its adjoint run in the HIP
 library (``lvae_gram_f64`` / ``lvae_gram_bwd_f64``).  The ELBO functions consume the spec directly.
 """
+import ctypes
 import math
 
 import torch
@@ -257,6 +258,40 @@ class AdditiveKernel(nn.Module):
         return AdditiveKernel(list(self.kernels) + list(other.kernels))
 
 
+class _ParamPackFn(torch.autograd.Function):
+    """[L, P] = exp(m + softplus(raw - m)) of the raw [L] fp64 tensors into their columns (1 elsewhere), one
+    HIP launch each way (glue.hip) instead of the stack / transform / transpose chain."""
+
+    @staticmethod
+    def forward(ctx, meta, *raws):
+        lib = _lib.lib()
+        cols, mlogs, L, P = meta
+        n = len(raws)
+        out = torch.empty(L, P, dtype=torch.float64, device=raws[0].device)
+        ca = (ctypes.c_int32 * n)(*cols)
+        ra = (ctypes.c_void_p * n)(*[r.data_ptr() for r in raws])
+        ma = (ctypes.c_void_p * n)(*[m.data_ptr() for m in mlogs])
+        _lib.check(lib.lvae_param_pack_fwd_f64(n, L, P, ca, ra, ma, _lib.ptr(out), _lib.stream_ptr()), "param_pack_fwd")
+        ctx.meta = meta
+        ctx.save_for_backward(*raws)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.lib()
+        raws = ctx.saved_tensors
+        cols, mlogs, L, P = ctx.meta
+        n = len(raws)
+        g = g.to(torch.float64)
+        grad = torch.empty(n, L, dtype=torch.float64, device=g.device)
+        ca = (ctypes.c_int32 * n)(*cols)
+        ra = (ctypes.c_void_p * n)(*[r.data_ptr() for r in raws])
+        ma = (ctypes.c_void_p * n)(*[m.data_ptr() for m in mlogs])
+        _lib.check(lib.lvae_param_pack_bwd_f64(n, L, P, ca, ra, ma, _lib.ptr(g), g.stride(0), g.stride(1),
+                                               _lib.ptr(grad), _lib.stream_ptr()), "param_pack_bwd")
+        return (None,) + tuple(grad[k] for k in range(n))
+
+
 def kernel_spec_and_params(kernel):
     """(KernelSpec, [L, P] parameter matrix) of an AdditiveKernel / ScaleKernel.
 
@@ -270,6 +305,12 @@ def kernel_spec_and_params(kernel):
     if not raws:
         return spec, torch.ones(1, len(refs), dtype=torch.float64)
     L = raws[0][0].shape[0]
+    if (len(raws) <= 64 and len(refs) <= 64 and
+            all(r.is_cuda and r.dtype == torch.float64 and r.dim() == 1 and r.shape[0] == L and r.is_contiguous()
+                and m.is_cuda and m.dtype == torch.float64 for r, m in raws)):
+        cols = [j for j, r in enumerate(refs) if r is not None]
+        meta = (cols, [m for _, m in raws], L, len(refs))
+        return spec, _ParamPackFn.apply(meta, *[r for r, _ in raws])  # (glue.hip: one launch each way)
     R = torch.stack([r[0] for r in raws], 0).to(torch.float64)          # [P', L]
     m = torch.cat([r[1] for r in raws]).to(torch.float64).unsqueeze(1)  # [P', 1]
     C = torch.exp(m + F.softplus(R - m))

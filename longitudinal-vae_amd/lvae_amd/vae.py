@@ -246,10 +246,11 @@ class ConvVAE(nn.Module):
         return deconv_sigmoid(self.deconv2, x)
 
     def sample_latent(self, mu, log_var, eps=None):
-        std = torch.exp(0.5 * log_var)
         if eps is None:
-            eps = torch.randn_like(std)
-        return mu + eps * std
+            eps = torch.randn_like(log_var)
+        if _glue_ok(mu, log_var, eps) and mu.shape == log_var.shape == eps.shape:
+            return _ReparamFn.apply(mu, log_var, eps)  # (glue.hip: one launch each way)
+        return mu + eps * torch.exp(0.5 * log_var)
 
     def forward(self, x, eps=None):
         mu, log_var = self.encode(x)
@@ -258,12 +259,80 @@ class ConvVAE(nn.Module):
     def loss_function(self, recon_x, x, mask):
         """(per-image masked MSE, per-image NLL) -- VAE.py:144-162."""
         d = self.num_dim
+        if _glue_ok(recon_x, x, mask, self._log_vy) and self._log_vy.numel() == d:
+            return _VaeLossFn.apply(recon_x, x, mask, self._log_vy)  # (glue.hip: one launch each way)
         se = (recon_x.reshape(-1, d) - x.reshape(-1, d)) ** 2 * mask.reshape(-1, d)
         msum = mask.reshape(-1, d).sum(1)
         msum = torch.where(msum == 0, torch.ones_like(msum), msum)
         mse = se.sum(1) / msum
         nll = se / (2 * torch.exp(self._log_vy)) + 0.5 * (math.log(2 * math.pi) + self._log_vy)
         return mse, nll.sum(1)
+
+
+class _VaeLossFn(torch.autograd.Function):
+    """(mse [B], nll [B]) of ConvVAE.loss_function in one HIP launch (glue.hip); backward: d recon and
+    d log_vy in one launch + the column sum of the d log_vy partials."""
+
+    @staticmethod
+    def forward(ctx, recon, x, mask, log_vy):
+        from . import _lib
+        lib = _lib.lib()
+        d = log_vy.numel()
+        r, xx, mm = (t.reshape(-1, d).contiguous() for t in (recon, x, mask))
+        lv = log_vy.contiguous()
+        B = r.shape[0]
+        mse, nll, msum = (torch.empty(B, dtype=torch.float32, device=r.device) for _ in range(3))
+        _lib.check(lib.lvae_vae_loss_fwd_f32(_lib.ptr(r), _lib.ptr(xx), _lib.ptr(mm), _lib.ptr(lv), B, d, _lib.ptr(mse),
+                                             _lib.ptr(nll), _lib.ptr(msum), _lib.stream_ptr()), "vae_loss_fwd")
+        ctx.save_for_backward(r, xx, mm, lv, msum)
+        ctx.rshape = recon.shape
+        ctx.need_lv = log_vy.requires_grad
+        return mse, nll
+
+    @staticmethod
+    def backward(ctx, g_mse, g_nll):
+        from . import _lib
+        lib = _lib.lib()
+        r, xx, mm, lv, msum = ctx.saved_tensors
+        B, d = r.shape
+        g_mse, g_nll = (g.to(torch.float32).reshape(B) for g in (g_mse, g_nll))  # (stride 0 kept: broadcasts)
+        dr = torch.empty_like(r)
+        part = torch.empty(int(lib.lvae_vae_loss_bwd_partials(B)), d, dtype=torch.float32, device=r.device)
+        _lib.check(lib.lvae_vae_loss_bwd_f32(_lib.ptr(r), _lib.ptr(xx), _lib.ptr(mm), _lib.ptr(lv), _lib.ptr(msum),
+                                             _lib.ptr(g_mse), g_mse.stride(0), _lib.ptr(g_nll), g_nll.stride(0), B, d,
+                                             _lib.ptr(dr), _lib.ptr(part), _lib.stream_ptr()), "vae_loss_bwd")
+        dlv = part.sum(0) if ctx.need_lv else None
+        return dr.reshape(ctx.rshape), None, None, dlv
+
+
+class _ReparamFn(torch.autograd.Function):
+    """z = mu + eps exp(log_var / 2) in one HIP launch (glue.hip); backward: d log_var in one launch."""
+
+    @staticmethod
+    def forward(ctx, mu, log_var, eps):
+        from . import _lib
+        lib = _lib.lib()
+        mu_, lv_, e_ = (t.contiguous() for t in (mu, log_var, eps))
+        z = torch.empty_like(mu_)
+        _lib.check(lib.lvae_reparam_fwd_f32(_lib.ptr(mu_), _lib.ptr(lv_), _lib.ptr(e_), mu_.numel(), _lib.ptr(z),
+                                            _lib.stream_ptr()), "reparam_fwd")
+        ctx.save_for_backward(lv_, e_)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        from . import _lib
+        lib = _lib.lib()
+        lv_, e_ = ctx.saved_tensors
+        gz = gz.contiguous()
+        glv = torch.empty_like(lv_)
+        _lib.check(lib.lvae_reparam_bwd_f32(_lib.ptr(gz), _lib.ptr(lv_), _lib.ptr(e_), lv_.numel(), _lib.ptr(glv),
+                                            _lib.stream_ptr()), "reparam_bwd")
+        return gz, glv, None
+
+
+def _glue_ok(*ts):
+    return all(t.is_cuda and t.dtype == torch.float32 for t in ts)
 
 
 class _EncoderPart(nn.Module):

@@ -1,0 +1,108 @@
+"""The glue launches (glue.hip) against the PyTorch formulas they replace, fp64 on the CPU as the reference:
+ConvVAE.loss_function (VAE.py:144-162), sample_latent (VAE.py:132-136) and the kernels' positivity
+transform exp(m + softplus(raw - m)) (GP_model.py:31-144), values and gradients."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().cpu().double()
+    b = b.detach().cpu().double()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-300))
+
+
+def _loss_ref(r, x, m, lv):
+    d = lv.numel()
+    se = (r.reshape(-1, d) - x.reshape(-1, d)) ** 2 * m.reshape(-1, d)
+    msum = m.reshape(-1, d).sum(1)
+    msum = torch.where(msum == 0, torch.ones_like(msum), msum)
+    return se.sum(1) / msum, (se / (2 * torch.exp(lv)) + 0.5 * (math.log(2 * math.pi) + lv)).sum(1)
+
+
+@pytest.mark.parametrize("B", [1, 67, 300])
+def test_vae_loss_fused(hip, B):
+    """Per-image masked MSE / NLL and d recon, d log_vy: ragged image counts (the backward's 64-image
+    chunks), one image with an all-zero mask (msum -> 1), weights on both outputs."""
+    from lvae_amd.vae import ConvVAE
+    torch.manual_seed(B)
+    vae = ConvVAE(2, 1296).cuda()
+    with torch.no_grad():
+        vae._log_vy.copy_(0.3 * torch.randn(1296))
+    r = torch.rand(B, 1, 36, 36, device="cuda", requires_grad=True)
+    x = torch.rand(B, 1, 36, 36, device="cuda")
+    m = (torch.rand(B, 1, 36, 36, device="cuda") > 0.2).float()
+    m[0] = 0.0
+    mse, nll = vae.loss_function(r, x, m)
+    w1, w2 = torch.rand(B, device="cuda"), torch.rand(B, device="cuda")
+    ((mse * w1).sum() + (nll * w2).sum()).backward()
+    r64 = r.detach().cpu().double().requires_grad_()
+    lv64 = vae._log_vy.detach().cpu().double().requires_grad_()
+    mse_r, nll_r = _loss_ref(r64, x.cpu().double(), m.cpu().double(), lv64)
+    ((mse_r * w1.cpu().double()).sum() + (nll_r * w2.cpu().double()).sum()).backward()
+    errs = dict(mse=rel(mse, mse_r), nll=rel(nll, nll_r), dr=rel(r.grad, r64.grad), dlv=rel(vae._log_vy.grad, lv64.grad))
+    print(B, errs)
+    for k, e in errs.items():
+        assert e < 2e-5, (k, e)
+    # the reduction-only use (the steps' mse.sum() / nll.sum(): the backward sees stride-0 gradients)
+    r.grad = None
+    vae._log_vy.grad = None
+    mse, nll = vae.loss_function(r, x, m)
+    (mse.sum() + 0.5 * nll.sum()).backward()
+    r64.grad = None
+    lv64.grad = None
+    mse_r, nll_r = _loss_ref(r64, x.cpu().double(), m.cpu().double(), lv64)
+    (mse_r.sum() + 0.5 * nll_r.sum()).backward()
+    assert rel(r.grad, r64.grad) < 2e-5 and rel(vae._log_vy.grad, lv64.grad) < 2e-5
+
+
+def test_reparam_fused(hip):
+    from lvae_amd.vae import ConvVAE
+    vae = ConvVAE(16, 1296).cuda()
+    torch.manual_seed(3)
+    mu = torch.randn(1000, 16, device="cuda", requires_grad=True)
+    lv = torch.randn(1000, 16, device="cuda", requires_grad=True)
+    eps = torch.randn(1000, 16, device="cuda")
+    z = vae.sample_latent(mu, lv, eps)
+    g = torch.randn_like(z)
+    (z * g).sum().backward()
+    mu64, lv64 = mu.detach().cpu().double().requires_grad_(), lv.detach().cpu().double().requires_grad_()
+    z64 = mu64 + eps.cpu().double() * torch.exp(0.5 * lv64)
+    (z64 * g.cpu().double()).sum().backward()
+    assert rel(z, z64) < 1e-6 and rel(mu.grad, mu64.grad) < 1e-6 and rel(lv.grad, lv64.grad) < 1e-6
+
+
+def test_param_pack_fused(hip):
+    """kernel_spec_and_params through the fused launch (fp64 CUDA raws) against the stacked PyTorch
+    transform (the same module on the CPU): the [L, P] matrix to fp64 rounding, the raw gradients to
+    1e-13, one raw parameter on softplus' linear branch."""
+    import lvae_amd as la
+    from lvae_amd.kernels import kernel_spec_and_params
+    CFG = dict(cat_kernel=[2], bin_kernel=[], sqexp_kernel=[0],
+               cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 2},
+                               {'cont_covariate': 0, 'cat_covariate': 3},
+                               {'cont_covariate': 1, 'cat_covariate': 4}],
+               bin_int_kernel=[], covariate_missing_val=[])
+    for L in (1, 16):
+        k = la.generate_kernel(**CFG, latent_dim=L).double()
+        rng = np.random.default_rng(L)
+        with torch.no_grad():
+            for p in k.parameters():
+                p.copy_(torch.as_tensor(rng.normal(0.0, 1.5, p.shape)))
+            next(iter(k.parameters()))[0] = 30.0  # softplus' linear branch
+        kc = la.generate_kernel(**CFG, latent_dim=L).double()
+        kc.load_state_dict(k.state_dict())
+        kg = k.cuda()
+        spec_g, Pg = kernel_spec_and_params(kg)
+        spec_c, Pc = kernel_spec_and_params(kc)
+        assert Pg.shape == Pc.shape and Pg.is_contiguous()
+        assert rel(Pg, Pc) < 1e-15
+        W = torch.randn(Pc.shape, dtype=torch.float64)
+        (Pg * W.cuda()).sum().backward()
+        (Pc * W).sum().backward()
+        for (n, pg), (_, pc) in zip(kg.named_parameters(), kc.named_parameters()):
+            assert rel(pg.grad, pc.grad) < 1e-13, n
