@@ -463,6 +463,22 @@ size_t lvae_natgrad_workspace_size(int L, int M) {
   return 3 * mm + 3 * v + align256((size_t)L * sizeof(double)) + align256((size_t)2 * L * sizeof(int32_t));
 }
 
+// iHn = iH + lr (gH + gH^T) in one pass (was a copy, an axpy and a transpose-add)
+__global__ void natgrad_ih_kernel(int L, int M, double lr, const double* __restrict__ iH, const double* __restrict__ gH,
+                                  double* __restrict__ iHn) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, MM = (int64_t)M * M;
+  if (e >= L * MM) return;
+  const int64_t b = e / MM, r = (e % MM) / M, c = e % M;
+  iHn[e] = iH[e] + lr * (gH[e] + gH[b * MM + c * M + r]);
+}
+
+// y = v - lr gm + 2 lr gw
+__global__ void natgrad_y_kernel(int64_t n, double lr, const double* __restrict__ v, const double* __restrict__ gm,
+                                 const double* __restrict__ gw, double* __restrict__ y) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) y[e] = v[e] - lr * gm[e] + 2.0 * lr * gw[e];
+}
+
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m, const double* grad_H, double lr,
                             const double* iH_in, int32_t* info, void* workspace, void* stream) {
   if (L < 1) return -1;
@@ -488,17 +504,15 @@ int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* gr
     LVAE_TRY(spd_inv_small_f64(M, L, H, MM, iH, MM, ld, inf, st));
   }
   // iH' = iH + lr (gH + gH^T)
-  axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 1.0, iHc, 0.0, iHn, nullptr, nullptr);
-  lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, lr, grad_H, 1.0, iHn, iHn, nullptr, 0, 0);
-  add_transpose_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, grad_H, iHn);
-  LVAE_TRY(spd_inv_small_f64(M, L, iHn, MM, Hn, MM, ld, inf + L, st));
-  // v = iH m ; gw = gH m ; y = v - lr gm + 2 lr gw ; m = Hn y ; H = Hn
+  natgrad_ih_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, iHc, grad_H, iHn);
+  // v = iH m ; gw = gH m (before m and H are overwritten: iHc is the old H's inverse, H itself is not read
+  // again); H = iH'^-1 in place; y = v - lr gm + 2 lr gw ; m = H y
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, iHc, M, MM, 0, m, 1, M, 0, 0.0, v, 1, M, 0, L, 1, st));
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, grad_H, M, MM, 0, m, 1, M, 0, 0.0, gw, 1, M, 0, L, 1, st));
-  lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 1.0, v, -lr, grad_m, y, nullptr, 0, 0);
-  lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 2.0 * lr, gw, 1.0, y, y, nullptr, 0, 0);
-  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, Hn, M, MM, 0, y, 1, M, 0, 0.0, m, 1, M, 0, L, 1, st));
-  (void)hipMemcpyAsync(H, Hn, sizeof(double) * L * MM, hipMemcpyDeviceToDevice, st);
+  LVAE_TRY(spd_inv_small_f64(M, L, iHn, MM, H, MM, ld, inf + L, st));
+  natgrad_y_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, lr, v, grad_m, gw, y);
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, H, M, MM, 0, y, 1, M, 0, 0.0, m, 1, M, 0, L, 1, st));
+  (void)Hn;
   if (info) (void)hipMemcpyAsync(info, inf, sizeof(int32_t) * L, hipMemcpyDeviceToDevice, st);
   LVAE_CHECK_LAUNCH();
   return 0;

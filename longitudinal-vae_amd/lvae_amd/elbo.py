@@ -446,6 +446,31 @@ def minibatch_KLD_upper_bound_iter(covar_module0, covar_module1, likelihood, lat
     return kld, gm, gH
 
 
+def natural_gradient_update_(m, H, grad_m, grad_H, natural_gradient_lr):
+    """natural_gradient_update IN PLACE on m [L, M, 1] / H [L, M, M] (fp64, contiguous, on the device): the
+    library updates the buffers it reads (lvae_natgrad_update_f64 reads m and H before writing them), no
+    clones and no copies back.  Returns False (nothing done) when m / H do not qualify."""
+    if not (m.dtype == H.dtype == torch.float64 and m.is_contiguous() and H.is_contiguous() and m.is_cuda):
+        return False
+    lib = _lib.lib()
+    L, M = H.shape[0], H.shape[-1]
+    gm = grad_m.detach().to(torch.float64).contiguous()
+    gH = grad_H.detach().to(torch.float64).contiguous()
+    ws = torch.empty(int(lib.lvae_natgrad_workspace_size(L, M)), dtype=torch.uint8, device=H.device)
+    info = torch.empty(L, dtype=torch.int32, device=H.device)
+    iH = None
+    cached = getattr(grad_H, "_lvae_iH", None)
+    if cached is not None and cached[1] is H and cached[1]._version == cached[2]:
+        iH = cached[0]
+    with torch.no_grad():
+        rc = lib.lvae_natgrad_update_f64(L, M, _lib.ptr(m.detach()), _lib.ptr(H.detach()), _lib.ptr(gm), _lib.ptr(gH),
+                                         float(natural_gradient_lr), _lib.ptr(iH), _lib.ptr(info), _lib.ptr(ws),
+                                         _lib.stream_ptr())
+    _lib.check(rc, "natgrad_update")
+    _check_info(info, "natural-gradient update cholesky")
+    return True
+
+
 def natural_gradient_update(m, H, grad_m, grad_H, natural_gradient_lr):
     """training.py:129-135 on the device: returns the updated (m, H) (new tensors, detached)."""
     lib = _lib.lib()

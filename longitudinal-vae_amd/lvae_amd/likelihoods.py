@@ -35,6 +35,10 @@ class GaussianLikelihood(nn.Module):
 
     @property
     def noise(self):
+        r = self._log_noise
+        if r.is_cuda and r.dtype == torch.float64 and r.dim() == 1 and r.is_contiguous() and self.min_log_noise.is_cuda:
+            from .kernels import _ParamPackFn  # (glue.hip: one launch each way)
+            return _ParamPackFn.apply(([0], [self.min_log_noise], r.shape[0], 1), r).reshape(-1)
         return torch.exp(self.min_log_noise + F.softplus(self._log_noise - self.min_log_noise))
 
     @noise.setter

@@ -14,7 +14,7 @@ updates) so that a data-parallel all-reduce can sit between two captured graphs.
 import torch
 
 from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_bound, natural_gradient_update,
-                   take_pending)
+                   natural_gradient_update_, take_pending)
 
 
 def _graph_vae_default():
@@ -182,10 +182,12 @@ class HensmanStep:
     def apply(self):
         self.opt.step()
         if self.ng:
-            m2, H2 = natural_gradient_update(self.m, self.H, self._gm, self._gH, self.ng_lr)
-            with torch.no_grad():
-                self.m.copy_(m2.reshape(self.m.shape).to(self.m.dtype))
-                self.H.copy_(H2.to(self.H.dtype))
+            # (fp64 state: updated in place by the library, no clones / copies back)
+            if not natural_gradient_update_(self.m, self.H, self._gm, self._gH, self.ng_lr):
+                m2, H2 = natural_gradient_update(self.m, self.H, self._gm, self._gH, self.ng_lr)
+                with torch.no_grad():
+                    self.m.copy_(m2.reshape(self.m.shape).to(self.m.dtype))
+                    self.H.copy_(H2.to(self.H.dtype))
 
     def __call__(self, img, mask, X, eps=None):
         out = self.forward_backward(img, mask, X, eps)
