@@ -1020,146 +1020,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
     part[((int64_t)l * kBwdSlots + sl) * G + g0] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
 }
 
-// kl_gram_bwd_tab_kernel with the table stride a compile-time constant (B gate bits) and the parameter loop
-// unrolled (at most kTabMaxPG parameters per distance group): every table read of element e and parameter k
-// is one ds_read_b32 at (the element's row + distance) + an immediate k * TS, the gate bits are computed
-// once per tile (not per group), and the per-parameter sums stay in registers between the fp64 folds (no
-// LDS read-modify-write per parameter and tile).  Same tiles, g, slots, fold cadence and partials.
-constexpr int kTabMaxPG = 8;
-template <int B>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WPE))) void kl_gram_bwd_tab2_kernel(
-    GramTab tb, const double* __restrict__ x, int ldx, int n, int np_, int qs, const double* __restrict__ params,
-    const float* __restrict__ Kinv, const float* __restrict__ S, const float* __restrict__ Sx, int nsplit,
-    const double* __restrict__ alpha, double* __restrict__ part, int ntiles, const int* __restrict__ covflag) {
-  if (*covflag != 2) return;  // (uniform, before any barrier)
-  constexpr int TS = (1 << B) * kTabR;
-  __shared__ float sx1[kGT * kMaxQB];
-  __shared__ float sx2[kGT * kMaxQB];
-  __shared__ float sp[64];
-  __shared__ float sa1[kGT], sa2[kGT];
-  __shared__ double wred[4][kBwdSlots];
-  extern __shared__ float tab[];  // the tables, group-major (tb.porder)
-  const int G = gridDim.x, g0 = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
-  const int lane = tid & 63, wv = tid >> 6, np_s = tb.n_params;
-  if (tid < np_s) sp[tid] = float(params[(int64_t)l * np_s + tid]);
-  for (int e = tid; e < 4 * kBwdSlots; e += 256) (&wred[0][0])[e] = 0.0;
-  __syncthreads();
-  tab_build_bwd(tb, sp, tab);
-  const float* ki = Kinv + (int64_t)l * np_ * np_;
-  const float* si = S + (int64_t)l * np_ * np_;
-  const double* al = alpha + (int64_t)l * np_;
-  auto load_ks = [&](int i0, int j0, g_f32x4 (&kv4)[4], g_f32x4 (&sv4)[4]) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int64_t o = (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc;
-      kv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(ki + o));
-      sv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(si + o));
-    }
-    for (int q = 1; q < nsplit; ++q) {
-      const float* sq = Sx + (int64_t)(q - 1) * gridDim.y * np_ * np_ + (int64_t)l * np_ * np_;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-        sv4[a] += __builtin_nontemporal_load(
-            reinterpret_cast<const g_f32x4*>(sq + (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc));
-    }
-  };
-  float accr[kTabMaxG][kTabMaxPG];
-#pragma unroll
-  for (int gi = 0; gi < kTabMaxG; ++gi)
-#pragma unroll
-    for (int kk = 0; kk < kTabMaxPG; ++kk) accr[gi][kk] = 0.f;
-  float dd = 0.f;
-  int since_flush = 0;
-  int t = g0, I = 0, J = 0;
-  g_f32x4 kv4[4], sv4[4];
-  CovPrefetchF pf;
-  double an = 0.0;
-  if (t < ntiles) {
-    tri_index(t, I, J);
-    load_ks(I * kGT, J * kGT, kv4, sv4);
-    pf.load(x, ldx, n, qs, I * kGT, J * kGT);
-    if (tid < 2 * kGT) an = al[(tid < kGT ? I : J) * kGT + (tid & (kGT - 1))];
-    pf.store(qs, sx1, sx2);
-    if (tid < kGT) sa1[tid] = float(an);
-    else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
-  }
-  __syncthreads();  // the tables and the first tile's LDS
-  for (; t < ntiles; t += G) {
-    const int i0 = I * kGT, j0 = J * kGT;
-    const bool more = t + G < ntiles;
-    int In = 0, Jn = 0;
-    if (t != g0) load_ks(i0, j0, kv4, sv4);
-    if (more) {
-      tri_index(t + G, In, Jn);
-      pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
-      if (tid < 2 * kGT) an = al[(tid < kGT ? In : Jn) * kGT + (tid & (kGT - 1))];
-    }
-    float g[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int i = i0 + 4 * tr + a;
-      const g_f32x4 kv = kv4[a], sv = sv4[a];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int j = j0 + 4 * tc + c;
-        const float gv = 0.5f * (kv[c] - sv[c] - sa1[4 * tr + a] * sa2[4 * tc + c]);
-        const bool in = i < n && j < n && j <= i;
-        if (in && i == j) dd += gv;
-        g[a][c] = in ? ((i == j) ? gv : 2.f * gv) : 0.f;
-      }
-    }
-    int bits[4][4];
-    tab_bits(tb, sx1, sx2, tr, tc, bits);
-#pragma unroll
-    for (int gi = 0; gi < kTabMaxG; ++gi) {
-      if (gi < tb.ng) {  // (uniform)
-        int idx[4][4];
-        tab_index(tb, gi, sx1, sx2, tr, tc, bits, idx);
-        const float* tg = tab + tb.pbeg[gi] * TS;
-        const int cnt = tb.pbeg[gi + 1] - tb.pbeg[gi];
-#pragma unroll
-        for (int kk = 0; kk < kTabMaxPG; ++kk) {
-          if (kk < cnt) {  // (uniform)
-            float acc = 0.f;
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-              for (int c = 0; c < 4; ++c) acc += g[a][c] * tg[idx[a][c] + kk * TS];
-            accr[gi][kk] += acc;
-          }
-        }
-      }
-    }
-    if (++since_flush == 4 || t + G >= ntiles) {  // fold the fp32 sums into the fp64 wave slots
-      since_flush = 0;
-      const float wd = wave_sum(dd);
-      if (lane == 0) wred[wv][kNoiseSlot] += (double)wd;
-      dd = 0.f;
-#pragma unroll
-      for (int gi = 0; gi < kTabMaxG; ++gi)
-#pragma unroll
-        for (int kk = 0; kk < kTabMaxPG; ++kk) {
-          if (gi < tb.ng && kk < tb.pbeg[gi + 1] - tb.pbeg[gi]) {  // (uniform)
-            const float w = wave_sum(accr[gi][kk]);
-            if (lane == 0) wred[wv][tb.porder[tb.pbeg[gi] + kk]] += (double)w;
-            accr[gi][kk] = 0.f;
-          }
-        }
-    }
-    if (more) {
-      __syncthreads();  // every reader of this tile's LDS is done
-      pf.store(qs, sx1, sx2);
-      if (tid < kGT) sa1[tid] = float(an);
-      else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
-      __syncthreads();
-      I = In, J = Jn;
-    }
-  }
-  __syncthreads();
-  for (int sl = tid; sl < kBwdSlots; sl += 256)
-    part[((int64_t)l * kBwdSlots + sl) * G + g0] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
-}
-
 // fp64 residual of the exact-KL solve, r = mu - K alpha0 (K = Gram + noise I, alpha0 = K^-1 mu from the
 // fp32 inverse), the matrix never materialised: every lower 64-tile's kernel values are evaluated in
 // fp64 (fp64 exp / sin, covariate tests and differences exact, as the reference's double arithmetic)
@@ -1539,24 +1399,9 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
   const size_t dyn = (size_t)(spec->n_params + 1) * 256 * sizeof(float);
   GramTab tb;
   if (gram_tab_build(spec, tb) && !getenv_off("LVAE_GRAM_TAB")) {  // (the same decision as kl_gram_fill's)
-    const size_t tabb = (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
-    bool unrolled = !getenv_off("LVAE_GRAM_TAB2");  // LVAE_GRAM_TAB2=0: the r3 loop (A/B runs)
-    for (int g = 0; g < tb.ng; ++g) unrolled = unrolled && tb.pbeg[g + 1] - tb.pbeg[g] <= kTabMaxPG;
-#define LVAE_TAB2(BB)                                                                                             \
-  case BB:                                                                                                        \
-    kl_gram_bwd_tab2_kernel<BB><<<dim3(G, L), 256, tabb, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit, \
-                                                               alpha, part, ntiles, covflag);                    \
-    break;
-    if (unrolled) {
-      switch (tb.nbits) {
-        LVAE_TAB2(0) LVAE_TAB2(1) LVAE_TAB2(2) LVAE_TAB2(3) LVAE_TAB2(4) LVAE_TAB2(5)
-        default: unrolled = false;
-      }
-    }
-#undef LVAE_TAB2
-    if (!unrolled)
-      kl_gram_bwd_tab_kernel<<<dim3(G, L), 256, dyn + tabb, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
-                                                                  alpha, part, ntiles, covflag);
+    const size_t tdyn = dyn + (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
+    kl_gram_bwd_tab_kernel<<<dim3(G, L), 256, tdyn, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                          alpha, part, ntiles, covflag);
   }
   if (bucket == 1) {
     kl_gram_bwd_tiles<8, 2, float><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
