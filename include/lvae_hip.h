@@ -153,7 +153,7 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
                                  void* workspace, void* stream);
 
 /* diag(K^-1) in fp64 for ill-conditioned dims (kl_refine.hip): the reduce estimates each dim's
- * diagonal error by est_l = max_i K_ii max_i (K^-1)_ii and where est_l > tau (env LVAE_KL_REFINE_TAU,
+ * diagonal error by est_l = (sum_r s_r + noise_l) max_i (K^-1)_ii (the first factor bounds max_i K_ii) and where est_l > tau (env LVAE_KL_REFINE_TAU,
  * default 16; LVAE_KL_REFINE=0 never, =1 always) replaces diag K^-1 by one fp64 Newton step,
  * 2 X_jj - (X K X)_jj (the trace term and dlogv; the reference's cholesky_solve(I) is fp64,
  * elbo_functions.py:27-31).  This copies the last reduce's est [L] (fp64) and flag [L] (int32, 1:

@@ -75,7 +75,7 @@ struct KLWorkspace {
   int* covflag;      // 1: integer covariates (the Gram kernels' fp32 covariate path; set by the factor)
   char* rb;          // the binned residual's plan / bin sums (kl_resid_bins.hip)
   double* K64;       // [L, np, np] fp64 K of the dims whose diag K^-1 is refined (kl_refine.hip)
-  double* rest;      // [L] the refinement gate's estimate max K_ii max (K^-1)_ii
+  double* rest;      // [L] the refinement gate's estimate (sum_r s_r + noise) max (K^-1)_ii
   int* rflag;        // [L] 1: diag K^-1 refined
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
@@ -365,7 +365,7 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
     kl_alpha_sym_kernel<<<dim3(G, L), 256, 0, st>>>(ws.Kinv, ws.res, np_, ws.rpart, ntiles);
     kl_alpha_reduce<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.rpart, ws.alpha, np_, ws.alpha);
   }
-  // diag K^-1 in fp64 for the dims whose max K_ii max (K^-1)_ii says the fp32 inverse's diagonal is not
+  // diag K^-1 in fp64 for the dims whose (sum_r s_r + noise) max (K^-1)_ii says the fp32 inverse's diagonal is not
   // enough (kl_refine.hip; the partials buffer is free again)
   LVAE_TRY(kl_refine_diag(spec, x, ldx, n, np_, L, params, noise, ws.Kinv, ws.kdiag, ws.K64, ws.rpart, ws.rest,
                           ws.rflag, st));

@@ -146,7 +146,7 @@ _refine_log = None  # a list while kl_closed_refine_log() is active
 @contextlib.contextmanager
 def kl_closed_refine_log():
     """Yields a list that gets, per KL_closed forward inside the block, the fp64 diag(K^-1) refinement's
-    gate (kl_refine.hip): (est [L] fp64 = max K_ii max (K^-1)_ii, the proxy of the fp32 inverse's
+    gate (kl_refine.hip): (est [L] fp64 = (sum of the scales + noise) max (K^-1)_ii, the proxy of the fp32 inverse's
     diagonal error; flag [L] int32, 1 where diag K^-1 was refined in fp64).  Device tensors, filled in
     stream order."""
     global _refine_log
