@@ -76,6 +76,19 @@ class ClosedStep:
                     recon = self.vae.decode(z)
                     mse, nll = self.vae.loss_function(recon, img, mask)
                     recon_loss, nll_loss = mse.sum(), nll.sum()
+                # The decoder's backward does not depend on the KL: d rec / d z and the decoder's parameter
+                # gradients are enqueued here, on the ConvVAE stream, so they run while the factorisation
+                # occupies the caller's stream (enqueued with the step's backward they start only once the
+                # host has queued the whole KL forward, and then queue behind the LDS-heavy lauum / S GEMM
+                # grids); the step's backward later starts at z with this gradient
+                early = gv is None and z.requires_grad
+                if early:
+                    rec_early = recon_loss if self.loss_function == "mse" else nll_loss
+                    dec = [q for q in self.vae.decoder_parameters() if q.requires_grad]
+                    gz, *gdec = torch.autograd.grad(rec_early, [z] + dec, allow_unused=True)
+                    for q, g in zip(dec, gdec):
+                        if g is not None:
+                            q.grad = g if q.grad is None else q.grad + g
             factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
             main.wait_event(enc_done)
             mu.record_stream(main)
@@ -93,7 +106,10 @@ class ClosedStep:
             # on the caller's stream, instead of behind it (a root summed on the caller's stream
             # would hand the decoder its gradient only after everything queued there).
             with torch.cuda.stream(vst):
-                torch.autograd.backward([rec_term, gp_term])
+                if early:
+                    torch.autograd.backward([z, gp_term], [gz, None])
+                else:
+                    torch.autograd.backward([rec_term, gp_term])
             main.wait_stream(vst)
             for t in (recon_loss, nll_loss, rec_term):
                 t.record_stream(main)

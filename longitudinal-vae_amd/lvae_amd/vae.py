@@ -226,6 +226,13 @@ class ConvVAE(nn.Module):
         self.deconv2 = nn.ConvTranspose2d(16, 1, kernel_size=4, stride=2, padding=1)
         self.register_buffer("min_log_vy", torch.full((1,), -8.0))
 
+    def decoder_parameters(self):
+        """The parameters the reconstruction loss depends on besides z: the decoder's and log_vy."""
+        ps = [self._log_vy]
+        for m in (self.fc3, self.fc31, self.fc4, self.deconv1, self.deconv2):
+            ps += list(m.parameters())
+        return ps
+
     @property
     def vy(self):
         return torch.exp(self.min_log_vy + F.softplus(self._log_vy - self.min_log_vy))
