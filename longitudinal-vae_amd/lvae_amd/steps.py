@@ -17,6 +17,13 @@ from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_b
                    natural_gradient_update_, take_pending)
 
 
+def _enc_first_default():
+    # LVAE_ENC_FIRST=1: the encoder's backward before the KL's hyper-parameter half (S GEMM + Gram adjoint) on
+    # the caller's stream, which then waits for it (A/B; see ClosedStep.forward_backward)
+    import os
+    return os.environ.get("LVAE_ENC_FIRST", "0") == "1"
+
+
 def _graph_vae_default():
     # opt-in (LVAE_GRAPH_VAE=1): measured SLOWER on ROCm 7 -- the ConvVAE's graph replays on its stream held
     # back the other streams' kernels (rank share of 8 GPUs 3.8 -> 10.9 ms per step, headline 11.7 -> 16.6 ms)
@@ -105,12 +112,22 @@ class ClosedStep:
             # the decoder's backward then starts as soon as its forward is done, beside the KL reduce
             # on the caller's stream, instead of behind it (a root summed on the caller's stream
             # would hand the decoder its gradient only after everything queued there).
+            hyper = [q for q in list(self.kernel.parameters()) + list(self.lik.parameters()) if q.requires_grad]
+            enc_first = early and _enc_first_default() and hyper
             with torch.cuda.stream(vst):
-                if early:
+                if enc_first:
+                    # the encoder's gradients only (the KL's hyper-parameter node is off their path) ...
+                    enc = [q for q in self.vae.encoder_parameters() if q.requires_grad]
+                    torch.autograd.backward([z, gp_term], [gz, None], inputs=enc, retain_graph=True)
+                elif early:
                     torch.autograd.backward([z, gp_term], [gz, None])
                 else:
                     torch.autograd.backward([rec_term, gp_term])
             main.wait_stream(vst)
+            if enc_first:
+                # ... then the S GEMM and the Gram adjoint, behind the encoder's backward on the caller's stream
+                # (instead of beside it: its ~20 small kernels otherwise wait for whole S-GEMM tiles)
+                torch.autograd.backward(gp_term, inputs=hyper)
             for t in (recon_loss, nll_loss, rec_term):
                 t.record_stream(main)
             net = rec_term.detach() + gp_term.detach()

@@ -178,3 +178,47 @@ def test_graphed_closed_step_matches_eager(hip):
         assert np.allclose(a, b, rtol=1e-6), (a, b)
     for (n, p), (_, q) in zip(k_g.named_parameters(), k_e.named_parameters()):
         assert rel(p, q) < 1e-6, n
+
+
+@pytest.mark.parametrize("enc_first", ["0", "1"])
+def test_closed_step_backward_orders_agree(hip, monkeypatch, enc_first):
+    """ClosedStep's backward orders -- the decoder's backward enqueued right after the forward (d rec / d z)
+    and the encoder's backward beside the KL's hyper-parameter half (default) or ahead of it
+    (LVAE_ENC_FIRST=1) -- against one plain backward from the summed loss on the same models and data:
+    every parameter after two Adam steps within 1e-6."""
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_batch
+    from lvae_amd.steps import ClosedStep
+    from lvae_amd.vae import ConvVAE
+    L, P, T = 4, 32, 16
+    img, mask, X = health_mnist_batch(P, T, seed=13, device=DEV)
+    eps = torch.randn(P * T, L, generator=torch.Generator().manual_seed(7)).to(DEV)
+
+    def make():
+        torch.manual_seed(11)
+        vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+        k = la.generate_kernel(**CFG, latent_dim=L).to(DEV)
+        lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+        opt = torch.optim.Adam(list(k.parameters()) + list(vae.parameters()), lr=1e-3)
+        return vae, k, lik, opt
+
+    # reference: the same step as one plain backward from the loss (no streams, no early decoder pass)
+    vae_r, k_r, lik_r, opt_r = make()
+    for _ in range(2):
+        opt_r.zero_grad(set_to_none=True)
+        mu, lv = vae_r.encode(img)
+        z = vae_r.sample_latent(mu, lv, eps)
+        mse, _ = vae_r.loss_function(vae_r.decode(z), img, mask)
+        kl = la.KL_closed_batched(k_r, X, lik_r, mu, lv)
+        (mse.sum() + 0.15 * kl.sum() / L).backward()
+        opt_r.step()
+        lik_r.noise = 1.0
+    monkeypatch.setenv("LVAE_ENC_FIRST", enc_first)
+    vae_s, k_s, lik_s, opt_s = make()
+    step = ClosedStep(vae_s, k_s, lik_s, opt_s, weight=0.15)
+    for _ in range(2):
+        step(img, mask, X, eps)
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(list(vae_s.named_parameters()) + list(k_s.named_parameters()),
+                              list(vae_r.named_parameters()) + list(k_r.named_parameters())):
+        assert rel(p, q) < 1e-6, n
