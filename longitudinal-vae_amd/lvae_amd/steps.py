@@ -17,6 +17,12 @@ from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_b
                    natural_gradient_update_, take_pending)
 
 
+def _early_dec_default():
+    # LVAE_EARLY_DEC=0: the decoder's backward with the step's backward (A/B; see ClosedStep.forward_backward)
+    import os
+    return os.environ.get("LVAE_EARLY_DEC", "1") != "0"
+
+
 def _enc_first_default():
     # LVAE_ENC_FIRST=1: the encoder's backward before the KL's hyper-parameter half (S GEMM + Gram adjoint) on
     # the caller's stream, which then waits for it (A/B; see ClosedStep.forward_backward)
@@ -88,7 +94,7 @@ class ClosedStep:
                 # occupies the caller's stream (enqueued with the step's backward they start only once the
                 # host has queued the whole KL forward, and then queue behind the LDS-heavy lauum / S GEMM
                 # grids); the step's backward later starts at z with this gradient
-                early = gv is None and z.requires_grad
+                early = gv is None and z.requires_grad and _early_dec_default()
                 if early:
                     rec_early = recon_loss if self.loss_function == "mse" else nll_loss
                     dec = [q for q in self.vae.decoder_parameters() if q.requires_grad]
