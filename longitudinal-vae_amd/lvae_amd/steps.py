@@ -17,19 +17,6 @@ from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_b
                    natural_gradient_update_, take_pending)
 
 
-def _early_dec_default():
-    # LVAE_EARLY_DEC=0: the decoder's backward with the step's backward (A/B; see ClosedStep.forward_backward)
-    import os
-    return os.environ.get("LVAE_EARLY_DEC", "1") != "0"
-
-
-def _enc_first_default():
-    # LVAE_ENC_FIRST=1: the encoder's backward before the KL's hyper-parameter half (S GEMM + Gram adjoint) on
-    # the caller's stream, which then waits for it (A/B; see ClosedStep.forward_backward)
-    import os
-    return os.environ.get("LVAE_ENC_FIRST", "0") == "1"
-
-
 def _graph_vae_default():
     # opt-in (LVAE_GRAPH_VAE=1): measured SLOWER on ROCm 7 -- the ConvVAE's graph replays on its stream held
     # back the other streams' kernels (rank share of 8 GPUs 3.8 -> 10.9 ms per step, headline 11.7 -> 16.6 ms)
@@ -89,19 +76,6 @@ class ClosedStep:
                     recon = self.vae.decode(z)
                     mse, nll = self.vae.loss_function(recon, img, mask)
                     recon_loss, nll_loss = mse.sum(), nll.sum()
-                # The decoder's backward does not depend on the KL: d rec / d z and the decoder's parameter
-                # gradients are enqueued here, on the ConvVAE stream, so they run while the factorisation
-                # occupies the caller's stream (enqueued with the step's backward they start only once the
-                # host has queued the whole KL forward, and then queue behind the LDS-heavy lauum / S GEMM
-                # grids); the step's backward later starts at z with this gradient
-                early = gv is None and z.requires_grad and _early_dec_default()
-                if early:
-                    rec_early = recon_loss if self.loss_function == "mse" else nll_loss
-                    dec = [q for q in self.vae.decoder_parameters() if q.requires_grad]
-                    gz, *gdec = torch.autograd.grad(rec_early, [z] + dec, allow_unused=True)
-                    for q, g in zip(dec, gdec):
-                        if g is not None:
-                            q.grad = g if q.grad is None else q.grad + g
             factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
             main.wait_event(enc_done)
             mu.record_stream(main)
@@ -118,22 +92,9 @@ class ClosedStep:
             # the decoder's backward then starts as soon as its forward is done, beside the KL reduce
             # on the caller's stream, instead of behind it (a root summed on the caller's stream
             # would hand the decoder its gradient only after everything queued there).
-            hyper = [q for q in list(self.kernel.parameters()) + list(self.lik.parameters()) if q.requires_grad]
-            enc_first = early and _enc_first_default() and hyper
             with torch.cuda.stream(vst):
-                if enc_first:
-                    # the encoder's gradients only (the KL's hyper-parameter node is off their path) ...
-                    enc = [q for q in self.vae.encoder_parameters() if q.requires_grad]
-                    torch.autograd.backward([z, gp_term], [gz, None], inputs=enc, retain_graph=True)
-                elif early:
-                    torch.autograd.backward([z, gp_term], [gz, None])
-                else:
-                    torch.autograd.backward([rec_term, gp_term])
+                torch.autograd.backward([rec_term, gp_term])
             main.wait_stream(vst)
-            if enc_first:
-                # ... then the S GEMM and the Gram adjoint, behind the encoder's backward on the caller's stream
-                # (instead of beside it: its ~20 small kernels otherwise wait for whole S-GEMM tiles)
-                torch.autograd.backward(gp_term, inputs=hyper)
             for t in (recon_loss, nll_loss, rec_term):
                 t.record_stream(main)
             net = rec_term.detach() + gp_term.detach()

@@ -180,13 +180,12 @@ def test_graphed_closed_step_matches_eager(hip):
         assert rel(p, q) < 1e-6, n
 
 
-@pytest.mark.parametrize("enc_first", ["0", "1"])
-def test_closed_step_backward_orders_agree(hip, monkeypatch, enc_first):
-    """ClosedStep's backward orders -- the decoder's backward enqueued right after the forward (d rec / d z)
-    and the encoder's backward beside the KL's hyper-parameter half (default) or ahead of it
-    (LVAE_ENC_FIRST=1) -- against one plain backward from the summed loss on the same models and data:
-    every parameter after two Adam steps within 1e-5 (the orders sum the same fp32 terms on different
-    streams; Adam's normalised steps carry that rounding into the parameters at ~1e-6)."""
+def test_closed_step_backward_order_agrees(hip):
+    """ClosedStep's overlapped order (the factor first, the ConvVAE on its own stream, the backward from
+    the two loss terms as separate roots, the KL backward split into its (mu, logvar) and hyper-parameter
+    nodes) against one plain backward from the summed loss on the same models and data: every parameter
+    after two Adam steps within 1e-5 (the same fp32 terms summed on different streams; Adam's normalised
+    steps carry that rounding into the parameters at ~1e-6)."""
     import lvae_amd as la
     from lvae_amd.data import health_mnist_batch
     from lvae_amd.steps import ClosedStep
@@ -214,7 +213,6 @@ def test_closed_step_backward_orders_agree(hip, monkeypatch, enc_first):
         (mse.sum() + 0.15 * kl.sum() / L).backward()
         opt_r.step()
         lik_r.noise = 1.0
-    monkeypatch.setenv("LVAE_ENC_FIRST", enc_first)
     vae_s, k_s, lik_s, opt_s = make()
     step = ClosedStep(vae_s, k_s, lik_s, opt_s, weight=0.15)
     for _ in range(2):
