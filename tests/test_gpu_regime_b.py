@@ -581,6 +581,24 @@ def test_kl_refine_forced(hip, monkeypatch, mode):
         assert per[1]["est"] == 0.0
 
 
+def test_kl_closed_c5_refined(hip, monkeypatch):
+    """The fp64 diag(K^-1) refinement (kl_refine.hip) forced on at the C5 size (N = 16384, one dim: the
+    fp64 K is 2 GiB, 128-wide tiles of K X over 16384^2) against the GPU-evaluated fp64 oracle: every
+    value and gradient within 1e-4, dlogv far below the unrefined dim's 1.4e-5."""
+    import lvae_amd as la
+    monkeypatch.setenv("LVAE_KL_REFINE", "1")
+    P, L = 1024, 1
+    rng = np.random.default_rng(1025)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    raw = _random_hypers(k, L, rng)
+    worst, per = _kl_vs_oracle(P, L, raw, 1.0, seed=1025, oracle_dev="cuda", return_per_dim=True)
+    print("C5 refined:", per[0])
+    assert per[0]["refined"] == 1
+    for key, e in worst.items():
+        assert e < 1e-4, (key, e)
+    assert worst["dlogv"] < 1e-6, worst
+
+
 @pytest.mark.parametrize("L", [1, 4])
 def test_kl_closed_c5(hip, L):
     """C5 shape (N = 16384: P = 1024 x T = 16), the reference kernel set: one latent dim, and L = 4 --
