@@ -351,6 +351,14 @@ int lvae_reparam_bwd_f32(const float* gz, const float* log_var, const float* eps
  * g[l, cols[k]] exp(m + softplus(t)) sigmoid(t), t = raw - m (g element (l, p) at g[l s0 + p s1]).       */
 int lvae_param_pack_fwd_f64(int n_raw, int L, int P, const int* cols, const double* const* raws,
                             const double* const* mlogs, double* out, void* stream);
+/* The Hensman step's loss terms (training.py:100-120) from the per-image mse / nll [B] (fp32) and the KL
+ * bound kld [1] (fp64): rec = c sum mse, nl = c sum nll (fp32), kd = ks kld, net = nl + kd (use_nll) or
+ * rec + w kd (fp64).  Backward: d/d mse_i, d/d nll_i (the same for every image, fp32) and d/d kld from the
+ * gradients of net / rec / nl / kd (nullptr: zero).                                                   */
+int lvae_step_terms_fwd(const float* mse, const float* nll, int B, const double* kld, float c, double ks, double w,
+                        int use_nll, float* rec, float* nl, double* net, double* kd, void* stream);
+int lvae_step_terms_bwd(const double* g_net, const float* g_rec, const float* g_nl, const double* g_kd, float c,
+                        double ks, double w, int use_nll, float* g_mse, float* g_nll, double* g_kld, void* stream);
 int lvae_param_pack_bwd_f64(int n_raw, int L, int P, const int* cols, const double* const* raws,
                             const double* const* mlogs, const double* g, int64_t g_stride0, int64_t g_stride1,
                             double* grad, void* stream);

@@ -119,6 +119,53 @@ __global__ void param_pack_bwd_kernel(ParamPack pk, const double* __restrict__ g
   grad[e] = g[l * gs0 + (int64_t)pk.col[k] * gs1] * exp(mm + softplus64(t)) * sig;
 }
 
+// the Hensman step's loss terms (training.py:100-120): rec = c sum mse, nl = c sum nll (fp32, as the framework
+// ops on fp32 sums), kd = ks kld (fp64), net = (use_nll ? nl + kd : rec + w kd); one workgroup
+__global__ __launch_bounds__(256) void step_terms_fwd_kernel(const float* __restrict__ mse,
+                                                             const float* __restrict__ nll, int B,
+                                                             const double* __restrict__ kld, float c, double ks,
+                                                             double w, int use_nll, float* __restrict__ rec_out,
+                                                             float* __restrict__ nl_out, double* __restrict__ net_out,
+                                                             double* __restrict__ kd_out) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x;
+  float a = 0.f, b = 0.f;
+  for (int i = tid; i < B; i += 256) {
+    a += mse[i];
+    b += nll[i];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = a;
+    red[1][tid >> 6] = b;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float rec = (((red[0][0] + red[0][1]) + red[0][2]) + red[0][3]) * c;
+    const float nl = (((red[1][0] + red[1][1]) + red[1][2]) + red[1][3]) * c;
+    const double kd = kld[0] * ks;
+    rec_out[0] = rec;
+    nl_out[0] = nl;
+    net_out[0] = use_nll ? (double)nl + kd : (double)rec + w * kd;
+    kd_out[0] = kd;
+  }
+}
+
+// the three gradients of the terms' inputs as scalars: d/d mse_i, d/d nll_i (fp32, the same for every
+// image), d/d kld; the output gradients may be absent (nullptr: zero)
+__global__ void step_terms_bwd_kernel(const double* __restrict__ g_net, const float* __restrict__ g_rec,
+                                      const float* __restrict__ g_nl, const double* __restrict__ g_kd, float c,
+                                      double ks, double w, int use_nll, float* __restrict__ g_mse,
+                                      float* __restrict__ g_nll, double* __restrict__ g_kld) {
+  if (threadIdx.x != 0) return;
+  const double gn = g_net ? g_net[0] : 0.0;
+  const float gr = g_rec ? g_rec[0] : 0.f, gl = g_nl ? g_nl[0] : 0.f;
+  g_mse[0] = c * ((use_nll ? 0.f : (float)gn) + gr);
+  g_nll[0] = c * ((use_nll ? (float)gn : 0.f) + gl);
+  g_kld[0] = ks * ((use_nll ? gn : w * gn) + (g_kd ? g_kd[0] : 0.0));
+}
+
 }  // namespace lvae
 
 using namespace lvae;
@@ -204,6 +251,24 @@ int lvae_param_pack_bwd_f64(int n_raw, int L, int P, const int* cols, const doub
   if (n_raw == 0) return 0;
   param_pack_bwd_kernel<<<cdiv((int64_t)n_raw * L, 256), 256, 0, (hipStream_t)stream>>>(pk, g, g_stride0, g_stride1,
                                                                                         grad);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_step_terms_fwd(const float* mse, const float* nll, int B, const double* kld, float c, double ks, double w,
+                        int use_nll, float* rec, float* nl, double* net, double* kd, void* stream) {
+  if (!mse || !nll || !kld || !rec || !nl || !net || !kd) return -1;
+  if (B < 0) return -2;
+  step_terms_fwd_kernel<<<1, 256, 0, (hipStream_t)stream>>>(mse, nll, B, kld, c, ks, w, use_nll, rec, nl, net, kd);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_step_terms_bwd(const double* g_net, const float* g_rec, const float* g_nl, const double* g_kd, float c,
+                        double ks, double w, int use_nll, float* g_mse, float* g_nll, double* g_kld, void* stream) {
+  if (!g_mse || !g_nll || !g_kld) return -1;
+  step_terms_bwd_kernel<<<1, 64, 0, (hipStream_t)stream>>>(g_net, g_rec, g_nl, g_kd, c, ks, w, use_nll, g_mse, g_nll,
+                                                           g_kld);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -98,6 +98,8 @@ SIGNATURES = {
     "lvae_vae_loss_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _VP]),
     "lvae_reparam_fwd_f32": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
     "lvae_reparam_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
+    "lvae_step_terms_fwd": (_I32, [_VP, _VP, _I32, _VP, ctypes.c_float, _D, _D, _I32, _VP, _VP, _VP, _VP, _VP]),
+    "lvae_step_terms_bwd": (_I32, [_VP, _VP, _VP, _VP, ctypes.c_float, _D, _D, _I32, _VP, _VP, _VP, _VP]),
     "lvae_param_pack_fwd_f64": (_I32, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
     "lvae_param_pack_bwd_f64": (_I32, [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "lvae_spd_inv_small_f64": (_I32, [_I32, _I32, _VP, _I64, _VP, _I64, _VP, _VP, _VP]),

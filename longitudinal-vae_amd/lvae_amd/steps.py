@@ -130,6 +130,42 @@ class ClosedStep:
         return out
 
 
+class _StepTermsFn(torch.autograd.Function):
+    """(net, rec, nll, kld') of the Hensman step from (mse [B], nll [B], kld) in one launch each way
+    (glue.hip: lvae_step_terms_fwd / _bwd) instead of the sums, scalings and their backward ops."""
+
+    @staticmethod
+    def forward(ctx, mse, nll, kld, c, ks, w, use_nll):
+        from . import _lib
+        lib = _lib.lib()
+        dev = mse.device
+        m, n, k = mse.contiguous(), nll.contiguous(), kld.detach().to(torch.float64).contiguous()
+        rec, nl = torch.empty((), device=dev), torch.empty((), device=dev)
+        net, kd = torch.empty((), dtype=torch.float64, device=dev), torch.empty((), dtype=torch.float64, device=dev)
+        _lib.check(lib.lvae_step_terms_fwd(_lib.ptr(m), _lib.ptr(n), m.numel(), _lib.ptr(k), float(c), float(ks),
+                                           float(w), int(use_nll), _lib.ptr(rec), _lib.ptr(nl), _lib.ptr(net),
+                                           _lib.ptr(kd), _lib.stream_ptr()), "step_terms_fwd")
+        ctx.set_materialize_grads(False)
+        ctx.meta = (float(c), float(ks), float(w), int(use_nll), m.numel(), kld.shape, kld.dtype)
+        return net, rec, nl, kd
+
+    @staticmethod
+    def backward(ctx, g_net, g_rec, g_nl, g_kd):
+        from . import _lib
+        lib = _lib.lib()
+        c, ks, w, use_nll, B, kshape, kdtype = ctx.meta
+        dev = next(g for g in (g_net, g_rec, g_nl, g_kd) if g is not None).device
+        f64 = lambda g: None if g is None else g.detach().to(torch.float64).contiguous()
+        f32 = lambda g: None if g is None else g.detach().to(torch.float32).contiguous()
+        gn, gr, gl, gk = f64(g_net), f32(g_rec), f32(g_nl), f64(g_kd)
+        g_mse, g_nll = torch.empty((), device=dev), torch.empty((), device=dev)
+        g_kld = torch.empty((), dtype=torch.float64, device=dev)
+        _lib.check(lib.lvae_step_terms_bwd(_lib.ptr(gn), _lib.ptr(gr), _lib.ptr(gl), _lib.ptr(gk), c, ks, w, use_nll,
+                                           _lib.ptr(g_mse), _lib.ptr(g_nll), _lib.ptr(g_kld), _lib.stream_ptr()),
+                   "step_terms_bwd")
+        return (g_mse.expand(B), g_nll.expand(B), g_kld.reshape(kshape).to(kdtype), None, None, None, None)
+
+
 class HensmanStep:
     """hensman_training batch body (training.py:91-135), loss 'mse' or 'nll'.
 
@@ -155,20 +191,26 @@ class HensmanStep:
         self.opt.zero_grad(set_to_none=True)
         recon, mu, log_var = self.vae(img, eps)
         mse, nll = self.vae.loss_function(recon, img, mask)
-        recon_loss, nll_loss = mse.sum(), nll.sum()
         L = mu.shape[1]
         P_b = X.shape[0] // self.T
         PSD_H = self.H if self.ng else self.H @ self.H.transpose(-1, -2)
         kld, gm, gH = minibatch_KLD_upper_bound(self.k0, self.k1, self.lik, L, self.m, PSD_H, X, mu, log_var,
                                                 self.z, self.P_tot, P_b, self.T, self.ng, self.eps,
                                                 ng_prior_share=1.0 / self.world)
-        recon_loss = recon_loss * self.P_tot / P_b
-        nll_loss = nll_loss * self.P_tot / P_b
-        if self.loss_function == "mse":
-            kld = kld / L
-            net = recon_loss + self.weight * kld
+        mse_loss = self.loss_function == "mse"
+        if mse.is_cuda and mse.dtype == nll.dtype == torch.float32 and kld.numel() == 1:
+            # (glue.hip: the sums, scalings and their backward in one launch each way)
+            net, recon_loss, nll_loss, kld = _StepTermsFn.apply(mse, nll, kld, self.P_tot / P_b,
+                                                                1.0 / L if mse_loss else 1.0, self.weight,
+                                                                not mse_loss)
         else:
-            net = nll_loss + kld
+            recon_loss = mse.sum() * self.P_tot / P_b
+            nll_loss = nll.sum() * self.P_tot / P_b
+            if mse_loss:
+                kld = kld / L
+                net = recon_loss + self.weight * kld
+            else:
+                net = nll_loss + kld
         net.backward()
         self._gm, self._gH = gm, gH
         return net.detach(), recon_loss.detach(), nll_loss.detach(), kld.detach()
