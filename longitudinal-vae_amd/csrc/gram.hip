@@ -11,6 +11,53 @@ namespace lvae {
 constexpr int kGT = 64;     // Gram tile edge
 constexpr int kMaxQ = 32;   // staged covariate columns
 
+// The RBF / periodic factor of an integer distance m < kGTab, evaluated once per workgroup into an LDS
+// table with kernel_eval's own expression (so a table read equals the direct evaluation bit for bit): the
+// covariates of the reference's data (time points, ages) are integer-coded, and the Hensman Grams are
+// small tiles where the exp / sin per element and component dominated.
+constexpr int kGTab = 64;
+template <int MC, int MF, typename T>
+__device__ inline T factor_at(const DevSpec& s, int r, int f, const T* __restrict__ p, T ad) {
+  const T ell = p[s.param_idx[r][f]];
+  if (s.kind[r][f] == LVAE_RBF) return exp(-(ad * ad) / (T(2) * ell * ell));
+  const T per = p[s.param_idx[r][f] + 1];
+  const T sn = sin(T(M_PI) * ad / per);
+  return exp(T(-2) * sn * sn / (ell * ell));
+}
+
+template <int MC, int MF, typename T>
+__device__ inline T kernel_eval_tab(const DevSpec& s, const double* __restrict__ xi, const double* __restrict__ xj,
+                                    const T* __restrict__ p, const T* __restrict__ tab) {
+  T sum = T(0);
+#pragma unroll
+  for (int r = 0; r < MC; ++r) {
+    if (r < s.n_comp) {
+      T prod = p[s.scale_idx[r]];
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        if (f < s.n_fac[r]) {
+          const int d = s.dim[r][f];
+          const double a = xi[d], b = xj[d];
+          const int k = s.kind[r][f];
+          if (k == LVAE_CAT) {
+            prod = (a - b == 0.0) ? prod : T(0);
+          } else if (k == LVAE_BIN) {
+            prod = (a + b == 2.0) ? prod : T(0);
+          } else if (k == LVAE_RBF || k == LVAE_PER) {
+            const double ad = fabs(a - b);
+            prod *= (ad < (double)kGTab && ad == floor(ad)) ? tab[(r * MF + f) * kGTab + (int)ad]
+                                                            : factor_at<MC, MF, T>(s, r, f, p, T(ad));
+          } else {
+            prod *= T(a * b);  // LVAE_LIN
+          }
+        }
+      }
+      sum += prod;
+    }
+  }
+  return sum;
+}
+
 template <int MC, int MF, typename T>
 __global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lvae_xview x2, int L, int n1, int n2,
                                                    int qs, const double* __restrict__ params,
@@ -19,10 +66,19 @@ __global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lva
   __shared__ double sx1[kGT * kMaxQ];
   __shared__ double sx2[kGT * kMaxQ];
   __shared__ T sp[64];
+  __shared__ T tab[MC * MF * kGTab];
   const int bl = blockIdx.z, b = bl / L, l = bl % L;
   const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * kGT;
   const int tid = threadIdx.x;
   if (tid < s.n_params) sp[tid] = T(params[(int64_t)l * s.n_params + tid]);
+  __syncthreads();
+  for (int e = tid; e < MC * MF * kGTab; e += 256) {
+    const int r = e / (MF * kGTab), f = (e / kGTab) % MF, m = e % kGTab;
+    T v = T(0);
+    if (r < s.n_comp && f < s.n_fac[r] && (s.kind[r][f] == LVAE_RBF || s.kind[r][f] == LVAE_PER))
+      v = factor_at<MC, MF, T>(s, r, f, sp, T(m));
+    tab[e] = v;
+  }
   const double* p1 = x1.ptr + b * x1.stride_b + l * x1.stride_l;
   const double* p2 = x2.ptr + b * x2.stride_b + l * x2.stride_l;
   for (int e = tid; e < kGT * qs; e += 256) {
@@ -39,7 +95,7 @@ __global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lva
   for (int k = 0; k < kGT / 4; ++k) {
     const int ii = (tid >> 6) + 4 * k, i = i0 + ii;
     if (i >= n1) continue;
-    T v = kernel_eval<MC, MF, T>(s, &sx1[ii * kMaxQ], &sx2[jj * kMaxQ], sp);
+    T v = kernel_eval_tab<MC, MF, T>(s, &sx1[ii * kMaxQ], &sx2[jj * kMaxQ], sp, tab);
     if (i == j) v += dg;
     o[(int64_t)i * ldo + j] = v;
   }
