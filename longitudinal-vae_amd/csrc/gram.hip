@@ -118,11 +118,73 @@ struct GramBwdJobs {
   int njobs, total_chunks;
 };
 
+// kernel_grad_acc with the factors of integer distances m < kGTab read from per-workgroup tables of phi(m),
+// and for periodic factors sin(u) and sin(2u) (u = pi m / p), each with kernel_grad_acc's own expression:
+// bit-identical to it, without the exp / sin per element and component
+template <int MC, int MF>
+__device__ inline void kernel_grad_acc_tab(const DevSpec& s, const double* __restrict__ xi,
+                                           const double* __restrict__ xj, const double* __restrict__ p, double g,
+                                           double (&acc_s)[MC], double (&acc_f)[MC][MF][2],
+                                           const double* __restrict__ tphi, const double* __restrict__ tsn,
+                                           const double* __restrict__ ts2) {
+#pragma unroll
+  for (int r = 0; r < MC; ++r) {
+    if (r < s.n_comp) {
+      double prod = 1.0;
+      double dlog[MF][2];
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        dlog[f][0] = 0.0;
+        dlog[f][1] = 0.0;
+        if (f >= s.n_fac[r]) continue;
+        const int d = s.dim[r][f];
+        const double a = xi[d], b = xj[d];
+        const int k = s.kind[r][f];
+        if (k == LVAE_CAT) {
+          prod = (a - b == 0.0) ? prod : 0.0;
+        } else if (k == LVAE_BIN) {
+          prod = (a + b == 2.0) ? prod : 0.0;
+        } else if (k == LVAE_RBF || k == LVAE_PER) {
+          const double ad = fabs(a - b);
+          const bool hit = ad < (double)kGTab && ad == floor(ad);
+          const int ti = (r * MF + f) * kGTab + (hit ? (int)ad : 0);
+          const double ell = p[s.param_idx[r][f]];
+          if (k == LVAE_RBF) {
+            const double diff = a - b, d2 = diff * diff;
+            prod *= hit ? tphi[ti] : exp(-d2 / (2.0 * ell * ell));
+            dlog[f][0] = d2 / (ell * ell * ell);
+          } else {
+            const double per = p[s.param_idx[r][f] + 1];
+            const double u = M_PI * ad / per;
+            const double sn = hit ? tsn[ti] : sin(u);
+            prod *= hit ? tphi[ti] : exp(-2.0 * sn * sn / (ell * ell));
+            dlog[f][0] = 4.0 * sn * sn / (ell * ell * ell);
+            dlog[f][1] = 2.0 * M_PI * ad * (hit ? ts2[ti] : sin(2.0 * u)) / (ell * ell * per * per);
+          }
+        } else {
+          prod *= a * b;  // LVAE_LIN
+        }
+      }
+      const double gp = g * prod;
+      acc_s[r] += gp;
+      const double gc = gp * p[s.scale_idx[r]];
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        acc_f[r][f][0] += gc * dlog[f][0];
+        acc_f[r][f][1] += gc * dlog[f][1];
+      }
+    }
+  }
+}
+
 template <int MC, int MF>
 __global__ __launch_bounds__(256) void gram_bwd_part_kernel(GramBwdJobs J, int L, double* __restrict__ part) {
   constexpr int NS = MC + MC * MF * 2 + 1;
+  constexpr bool kTab = MC * MF <= 16;  // (the tables: 3 x 8 KB at the small bucket)
+  constexpr int NT = kTab ? MC * MF * kGTab : 1;
   __shared__ double sp[64];
   __shared__ double wred[4][NS];
+  __shared__ double tphi[NT], tsn[NT], ts2[NT];
   const int c = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
   int jb = 0;
   while (jb + 1 < J.njobs && c >= J.j[jb + 1].chunk0) ++jb;
@@ -130,6 +192,27 @@ __global__ __launch_bounds__(256) void gram_bwd_part_kernel(GramBwdJobs J, int L
   const DevSpec& s = J.s[job.spec];
   if (tid < job.n_params) sp[tid] = job.params[(int64_t)l * job.n_params + tid];
   __syncthreads();
+  if (kTab) {
+    for (int e = tid; e < NT; e += 256) {
+      const int r = e / (MF * kGTab), f = (e / kGTab) % MF, m = e % kGTab;
+      double phi = 0.0, sn = 0.0, s2 = 0.0;
+      if (r < s.n_comp && f < s.n_fac[r]) {
+        const double ell = sp[s.param_idx[r][f]], ad = (double)m;
+        if (s.kind[r][f] == LVAE_RBF) {
+          phi = exp(-(ad * ad) / (2.0 * ell * ell));
+        } else if (s.kind[r][f] == LVAE_PER) {
+          const double per = sp[s.param_idx[r][f] + 1], u = M_PI * ad / per;
+          sn = sin(u);
+          phi = exp(-2.0 * sn * sn / (ell * ell));
+          s2 = sin(2.0 * u);
+        }
+      }
+      tphi[e] = phi;
+      tsn[e] = sn;
+      ts2[e] = s2;
+    }
+    __syncthreads();
+  }
   double acc_s[MC];
   double acc_f[MC][MF][2];
 #pragma unroll
@@ -149,7 +232,10 @@ __global__ __launch_bounds__(256) void gram_bwd_part_kernel(GramBwdJobs J, int L
     if (g == 0.0) continue;
     const double* xi = job.x1.ptr + b * job.x1.stride_b + l * job.x1.stride_l + i * job.x1.ld;
     const double* xj = job.x2.ptr + b * job.x2.stride_b + l * job.x2.stride_l + j * job.x2.ld;
-    kernel_grad_acc<MC, MF, double, double>(s, xi, xj, sp, g, acc_s, acc_f);
+    if (kTab)
+      kernel_grad_acc_tab<MC, MF>(s, xi, xj, sp, g, acc_s, acc_f, tphi, tsn, ts2);
+    else
+      kernel_grad_acc<MC, MF, double, double>(s, xi, xj, sp, g, acc_s, acc_f);
     if (i == j) dd += g;
   }
   const int w = tid >> 6, lane = tid & 63;
