@@ -22,7 +22,12 @@ lv = (0.1 * torch.randn(P * T, L, generator=g, dtype=torch.float64)).to(dev).req
 k = la.generate_kernel(**cfg, latent_dim=L).to(dev)
 lik = la.GaussianLikelihood(L, noise=1.0).to(dev)
 for it in range(iters):
+    for p in list(k.parameters()) + list(lik.parameters()):
+        p.grad = None
     kl = la.KL_closed_batched(k, X, lik, mu, lv)
     kl.sum().backward()
 torch.cuda.synchronize()
 print(la._lib.LIB_PATH, [round(v, 4) for v in kl[:3].tolist()], float(mu.grad.abs().sum()))
+# the hyper-parameter gradients of the last iteration, in full (old / new library bit-identity check)
+print("hyper-grads", [repr(float(p.grad.double().sum())) for p in list(k.parameters()) + list(lik.parameters())
+                      if p.grad is not None])
