@@ -232,6 +232,15 @@ int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
                          const double* H, const double* mu, const double* logv, const double* params0,
                          const double* params1, const double* noise, double* kld, double* grad_m,
                          double* grad_H, int32_t* info, void* workspace, void* stream);
+/* The same forward in two parts on one workspace (part 0: both): part 1 needs neither mu nor logv
+ * (Grams, the K0zz / B_p / H inverses, iK m, K0xz iK m, Q = K0xz^T B^-1 K0xz, iK H iK and the
+ * data-independent natural-gradient terms incl. grad_H) and can run beside the encoder; part 2 (the
+ * residual, the sums -> kld, grad_m, info) then reads mu / logv.  Same results as the one call.    */
+int lvae_hensman_fwd_part_f64(int part, const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1,
+                              const lvae_hensman_dims* d, const double* x, const double* z, const double* m,
+                              const double* H, const double* mu, const double* logv, const double* params0,
+                              const double* params1, const double* noise, double* kld, double* grad_m,
+                              double* grad_H, int32_t* info, void* workspace, void* stream);
 
 /* Backward given dL/dkld = *gkld (device scalar): dmu, dlogv [P_b*T, L]; dparams0 [L,P0],
  * dparams1 [L,P1], dnoise [L]; dm [L,M], dH [L,M,M] when !natural_gradient (else may be NULL).

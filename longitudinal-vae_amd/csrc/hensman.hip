@@ -321,11 +321,16 @@ size_t lvae_hensman_iH_offset(const lvae_hensman_dims* d) {
   return (size_t)((char*)HWs(base, *d).iH - base);
 }
 
-int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, const lvae_hensman_dims* dp,
-                         const double* x, const double* z, const double* m, const double* H, const double* mu,
-                         const double* logv, const double* params0, const double* params1, const double* noise,
-                         double* kld, double* grad_m, double* grad_H, int32_t* info, void* workspace, void* stream) {
+// part 1: everything that needs neither mu nor logv (the Grams, the three inverses, t / y, iBK, Q, iK H iK
+// and the data-independent natural-gradient terms) -- a caller can run it beside the encoder; part 2: the
+// rest (the residual, s, the sums, u / w / a, grad_m, info); part 0: both, in that order.
+int lvae_hensman_fwd_part_f64(int part, const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1,
+                              const lvae_hensman_dims* dp, const double* x, const double* z, const double* m,
+                              const double* H, const double* mu, const double* logv, const double* params0,
+                              const double* params1, const double* noise, double* kld, double* grad_m,
+                              double* grad_H, int32_t* info, void* workspace, void* stream) {
   LVAE_TRY(hensman_check(spec0, spec1, dp));
+  if (part < 0 || part > 2) return -18;
   if (!workspace || ((uintptr_t)workspace & 255)) return -17;
   hipStream_t st = (hipStream_t)stream;
   ProfScope ps(LVAE_PH_HENSMAN_FWD, st);
@@ -333,54 +338,69 @@ int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   const int L = d.L, M = d.M, P_b = d.P_b, T = d.T, Q = d.Q, B = P_b * T;
   const int64_t MM = (int64_t)M * M, TT = (int64_t)T * T, BM = (int64_t)B * M;
   HWs w((char*)workspace, d);
-  // Grams (elbo_functions.py:171-176)
-  fill_kernel<<<blocks(L), 256, 0, st>>>(w.epsv, L, d.eps);
-  const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
-  LVAE_TRY(lvae_gram_f64(spec0, xv, zv, 1, L, B, M, params0, nullptr, w.K0xz, 0, BM, M, stream));
-  LVAE_TRY(lvae_gram_f64(spec0, zv, zv, 1, L, M, M, params0, w.epsv, w.K0zz, 0, MM, M, stream));
-  LVAE_TRY(lvae_gram_f64(spec0, xs, xs, P_b, L, T, T, params0, nullptr, w.K0st, TT, P_b * TT, T, stream));
-  LVAE_TRY(lvae_gram_f64(spec1, xs, xs, P_b, L, T, T, params1, noise, w.Bst, TT, P_b * TT, T, stream));
-  if (d.seg_len)
-    hn_seg_mask_kernel<<<blocks((int64_t)L * B * M + (int64_t)L * P_b * TT), 256, 0, st>>>(L, P_b, T, M, d.seg_len,
-                                                                                           w.K0xz, w.K0st, w.Bst);
-  // factor + inverse (177-186)
-  LVAE_TRY(spd_inv_small2_f64(M, L, w.K0zz, MM, w.iK, MM, w.ldK, w.info, L, H, MM, w.iH, MM, w.ldH,
-                              w.info + L + L * P_b, st));
-  LVAE_TRY(spd_inv_small_f64(T, L * P_b, w.Bst, TT, w.iB, TT, w.ldB, w.info + L, st));
-  // t = iK m ; r = K0xz t - mu ; s = iB r ; iBK = iB K0xz ; Q = K0xz^T iBK ; Y = iK H iK
-  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, m, 1, M, 0, 0.0, w.t, 1, M, 0, L, 1, st));
-  LVAE_TRY(gemm_small_f64(0, 0, B, 1, M, 1.0, w.K0xz, M, BM, 0, w.t, 1, M, 0, 0.0, w.y, 1, B, 0, L, 1, st));
-  resid_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(w.y, mu, B, L, T, d.seg_len, w.r);
-  LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, w.r, 1, B, T, 0.0, w.s, 1, B, T, L, P_b, st));
-  LVAE_TRY(gemm_small_f64(0, 0, T, M, T, 1.0, w.iB, T, P_b * TT, TT, w.K0xz, M, BM, (int64_t)T * M, 0.0, w.iBK, M,
-                          BM, (int64_t)T * M, L, P_b, st));
-  LVAE_TRY(gemm_small_f64(1, 0, M, M, B, 1.0, w.K0xz, M, BM, 0, w.iBK, M, BM, 0, 0.0, w.Q, M, MM, 0, L, 1, st));
-  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, H, M, MM, 0, 0.0, w.iKH, M, MM, 0, L, 1, st));
-  LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKH, M, MM, 0, w.iK, M, MM, 0, 0.0, w.Y, M, MM, 0, L, 1, st));
-  // partial sums + total (189-204)
-  hn_reduce_kernel<<<L, 256, 0, st>>>(M, P_b, T, L, w.r, w.s, w.iB, logv, w.ldB, w.K0st, w.Q, w.iK, w.Y, H, m, w.t,
-                                      w.ldK, w.ldH, d.seg_len, w.part);
-  hn_final_kernel<<<1, 64, 0, st>>>(L, M, d.P_tot, P_b, d.n_total > 0.0 ? d.n_total : d.P_tot * T, w.part, kld);
-  // natural-gradient directions (208-214)
-  if (d.natural_gradient && grad_m && grad_H) {
-    LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, mu, L, 1, (int64_t)T * L, 0.0, w.u, 1, B, T,
-                            L, P_b, st));
-    LVAE_TRY(gemm_small_f64(1, 0, M, 1, B, 1.0, w.K0xz, M, BM, 0, w.u, 1, B, 0, 0.0, w.w, 1, M, 0, L, 1, st));
-    LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, w.w, 1, M, 0, 0.0, w.a, 1, M, 0, L, 1, st));
-    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, w.Q, M, MM, 0, 0.0, w.iKQ, M, MM, 0, L, 1, st));
-    // Bn = iK Q iK + share iK ; grad_m = Bn m - a ; grad_H = 1/2 (Bn - share iH)
-    const double share = d.ng_prior_share;
-    axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, share, w.iK, 0.0, w.Bn, nullptr, nullptr);
-    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKQ, M, MM, 0, w.iK, M, MM, 0, 1.0, w.Bn, M, MM, 0, L, 1, st));
-    LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.Bn, M, MM, 0, m, 1, M, 0, 0.0, w.tM, 1, M, 0, L, 1, st));
-    lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 1.0, w.tM, -1.0, w.a, grad_m, nullptr,
-                                                            0, 0);
-    lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 0.5, w.Bn, -0.5 * share, w.iH, grad_H, nullptr, 0, 0);
+  const bool ng = d.natural_gradient && grad_m && grad_H;
+  const double share = d.ng_prior_share;
+  if (part != 2) {
+    // Grams (elbo_functions.py:171-176)
+    fill_kernel<<<blocks(L), 256, 0, st>>>(w.epsv, L, d.eps);
+    const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
+    LVAE_TRY(lvae_gram_f64(spec0, xv, zv, 1, L, B, M, params0, nullptr, w.K0xz, 0, BM, M, stream));
+    LVAE_TRY(lvae_gram_f64(spec0, zv, zv, 1, L, M, M, params0, w.epsv, w.K0zz, 0, MM, M, stream));
+    LVAE_TRY(lvae_gram_f64(spec0, xs, xs, P_b, L, T, T, params0, nullptr, w.K0st, TT, P_b * TT, T, stream));
+    LVAE_TRY(lvae_gram_f64(spec1, xs, xs, P_b, L, T, T, params1, noise, w.Bst, TT, P_b * TT, T, stream));
+    if (d.seg_len)
+      hn_seg_mask_kernel<<<blocks((int64_t)L * B * M + (int64_t)L * P_b * TT), 256, 0, st>>>(
+          L, P_b, T, M, d.seg_len, w.K0xz, w.K0st, w.Bst);
+    // factor + inverse (177-186)
+    LVAE_TRY(spd_inv_small2_f64(M, L, w.K0zz, MM, w.iK, MM, w.ldK, w.info, L, H, MM, w.iH, MM, w.ldH,
+                                w.info + L + L * P_b, st));
+    LVAE_TRY(spd_inv_small_f64(T, L * P_b, w.Bst, TT, w.iB, TT, w.ldB, w.info + L, st));
+    // t = iK m ; y = K0xz t ; iBK = iB K0xz ; Q = K0xz^T iBK ; Y = iK H iK
+    LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, m, 1, M, 0, 0.0, w.t, 1, M, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, B, 1, M, 1.0, w.K0xz, M, BM, 0, w.t, 1, M, 0, 0.0, w.y, 1, B, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, T, M, T, 1.0, w.iB, T, P_b * TT, TT, w.K0xz, M, BM, (int64_t)T * M, 0.0, w.iBK,
+                            M, BM, (int64_t)T * M, L, P_b, st));
+    LVAE_TRY(gemm_small_f64(1, 0, M, M, B, 1.0, w.K0xz, M, BM, 0, w.iBK, M, BM, 0, 0.0, w.Q, M, MM, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, H, M, MM, 0, 0.0, w.iKH, M, MM, 0, L, 1, st));
+    LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKH, M, MM, 0, w.iK, M, MM, 0, 0.0, w.Y, M, MM, 0, L, 1, st));
+    if (ng) {  // the data-independent natural-gradient terms (208-214)
+      // Bn = iK Q iK + share iK ; tM = Bn m ; grad_H = 1/2 (Bn - share iH)
+      LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iK, M, MM, 0, w.Q, M, MM, 0, 0.0, w.iKQ, M, MM, 0, L, 1, st));
+      axpby_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, share, w.iK, 0.0, w.Bn, nullptr, nullptr);
+      LVAE_TRY(gemm_small_f64(0, 0, M, M, M, 1.0, w.iKQ, M, MM, 0, w.iK, M, MM, 0, 1.0, w.Bn, M, MM, 0, L, 1, st));
+      LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.Bn, M, MM, 0, m, 1, M, 0, 0.0, w.tM, 1, M, 0, L, 1, st));
+      lincomb_kernel<<<blocks(L * MM), 256, 0, st>>>(L * MM, 0.5, w.Bn, -0.5 * share, w.iH, grad_H, nullptr, 0, 0);
+    }
   }
-  // info: first failing matrix (K0zz, then B_p, then H) per latent dim
-  if (info) hn_info_kernel<<<blocks(L), 256, 0, st>>>(L, P_b, w.info, info);
+  if (part != 1) {
+    // r = y - mu ; s = iB r
+    resid_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(w.y, mu, B, L, T, d.seg_len, w.r);
+    LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, w.r, 1, B, T, 0.0, w.s, 1, B, T, L, P_b, st));
+    // partial sums + total (189-204)
+    hn_reduce_kernel<<<L, 256, 0, st>>>(M, P_b, T, L, w.r, w.s, w.iB, logv, w.ldB, w.K0st, w.Q, w.iK, w.Y, H, m,
+                                        w.t, w.ldK, w.ldH, d.seg_len, w.part);
+    hn_final_kernel<<<1, 64, 0, st>>>(L, M, d.P_tot, P_b, d.n_total > 0.0 ? d.n_total : d.P_tot * T, w.part, kld);
+    if (ng) {  // u = iB mu ; w = K0xz^T u ; a = iK w ; grad_m = Bn m - a
+      LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, mu, L, 1, (int64_t)T * L, 0.0, w.u, 1, B,
+                              T, L, P_b, st));
+      LVAE_TRY(gemm_small_f64(1, 0, M, 1, B, 1.0, w.K0xz, M, BM, 0, w.u, 1, B, 0, 0.0, w.w, 1, M, 0, L, 1, st));
+      LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, w.iK, M, MM, 0, w.w, 1, M, 0, 0.0, w.a, 1, M, 0, L, 1, st));
+      lincomb_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, 1.0, w.tM, -1.0, w.a, grad_m, nullptr,
+                                                              0, 0);
+    }
+    // info: first failing matrix (K0zz, then B_p, then H) per latent dim
+    if (info) hn_info_kernel<<<blocks(L), 256, 0, st>>>(L, P_b, w.info, info);
+  }
   LVAE_CHECK_LAUNCH();
   return 0;
+}
+
+int lvae_hensman_fwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, const lvae_hensman_dims* dp,
+                         const double* x, const double* z, const double* m, const double* H, const double* mu,
+                         const double* logv, const double* params0, const double* params1, const double* noise,
+                         double* kld, double* grad_m, double* grad_H, int32_t* info, void* workspace, void* stream) {
+  return lvae_hensman_fwd_part_f64(0, spec0, spec1, dp, x, z, m, H, mu, logv, params0, params1, noise, kld, grad_m,
+                                   grad_H, info, workspace, stream);
 }
 
 int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec1, const lvae_hensman_dims* dp,

@@ -9,8 +9,9 @@ from .kernels import (AdditiveKernel, BinKernel, CatKernel, LinearKernel, Period
                       ProductKernel, RbfKernel, ScaleKernel, generate_kernel, generate_kernel_approx,
                       generate_kernel_batched, kernel_spec_and_params)
 from .likelihoods import GaussianLikelihood  # noqa: F401
-from .elbo import (KL_closed, KL_closed_batched, check_pending, kl_closed_prefactor, minibatch_KLD_upper_bound,  # noqa: F401
-                   minibatch_KLD_upper_bound_iter, natural_gradient_update, set_sync_checks)
+from .elbo import (HensmanPrior, KL_closed, KL_closed_batched, check_pending, kl_closed_prefactor,  # noqa: F401
+                   minibatch_KLD_upper_bound, minibatch_KLD_upper_bound_iter, natural_gradient_update,
+                   set_sync_checks)
 from .predict import batch_predict_varying_T  # noqa: F401
 from .gpapprox import deviance_upper_bound, elbo, spd_inverse, validation_dubo  # noqa: F401
 

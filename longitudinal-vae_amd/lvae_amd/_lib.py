@@ -108,6 +108,8 @@ SIGNATURES = {
     "lvae_hensman_workspace_size": (_SZ, [_DIMS]),
     "lvae_hensman_fwd_f64": (_I32, [_SPEC, _SPEC, _DIMS, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                     _VP, _VP, _VP, _VP]),
+    "lvae_hensman_fwd_part_f64": (_I32, [_I32, _SPEC, _SPEC, _DIMS, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
+                                         _VP, _VP, _VP, _VP, _VP]),
     "lvae_hensman_bwd_f64": (_I32, [_SPEC, _SPEC, _DIMS, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                                     _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_natgrad_workspace_size": (_SZ, [_I32, _I32]),

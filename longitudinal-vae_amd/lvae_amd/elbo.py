@@ -306,25 +306,83 @@ def KL_closed(covar_module, train_x, likelihoods, data, mu, log_var):
 # ------------------------------------------------------------------------------------------
 # Regime A: Hensman mini-batch KL upper bound (elbo_functions.py:144-216), fp64
 # ------------------------------------------------------------------------------------------
+class _HensmanPre:
+    """The fp64 operands, workspace and outputs of one Hensman forward, and (launch) its part 1 -- the
+    Grams, inverses and products that need neither mu nor logv (lvae_hensman_fwd_part_f64)."""
+
+    def __init__(self, params0, params1, noise, m, H, x, z, spec0, spec1, dims, want_ng, dev):
+        lib = _lib.lib()
+        f64 = lambda t: t.detach().to(torch.float64).contiguous()
+        self.p0, self.p1, self.nz = f64(params0), f64(params1), f64(noise).reshape(-1)
+        self.m64, self.H64, self.x64, self.z64 = f64(m), f64(H), f64(x), f64(z)
+        L, M = dims.L, dims.M
+        self.ws = torch.empty(int(lib.lvae_hensman_workspace_size(dims)), dtype=torch.uint8, device=dev)
+        self.kld = torch.empty((), dtype=torch.float64, device=dev)
+        self.gm = torch.empty(L, M, 1, dtype=torch.float64, device=dev) if want_ng else None
+        self.gH = torch.empty(L, M, M, dtype=torch.float64, device=dev) if want_ng else None
+        self.info = torch.empty(L, dtype=torch.int32, device=dev)
+        self.spec0, self.spec1, self.dims = spec0, spec1, dims
+
+    def run(self, part, mu64=None, lv64=None):
+        rc = _lib.lib().lvae_hensman_fwd_part_f64(
+            part, self.spec0, self.spec1, self.dims, _lib.ptr(self.x64), _lib.ptr(self.z64), _lib.ptr(self.m64),
+            _lib.ptr(self.H64), _lib.ptr(mu64), _lib.ptr(lv64), _lib.ptr(self.p0), _lib.ptr(self.p1),
+            _lib.ptr(self.nz), _lib.ptr(self.kld), _lib.ptr(self.gm), _lib.ptr(self.gH), _lib.ptr(self.info),
+            _lib.ptr(self.ws), _lib.stream_ptr())
+        _lib.check(rc, "hensman_fwd")
+
+
+class HensmanPrior:
+    """minibatch_KLD_upper_bound's (mu, logv)-independent part -- the Grams, the K0zz / B_p / H inverses
+    and the products of elbo_functions.py:171-186, 208-214 that do not read the batch's latents --
+    launched now, on ``stream`` (default: the current stream; the hyper-parameter transforms always run
+    on the current stream, so their backward stays there), so that the ConvVAE can run beside it; pass it
+    as minibatch_KLD_upper_bound(..., prior=) (single use; that call joins the current stream to it)."""
+
+    def __init__(self, covar_module0, covar_module1, likelihood, latent_dim, m, H, train_xt, z, P_tot, P_batch, T,
+                 natural_gradient, eps, ng_prior_share=1.0, stream=None):
+        a = _hensman_args(covar_module0, covar_module1, likelihood, latent_dim, H, train_xt, z, P_tot, P_batch, T,
+                          natural_gradient, eps, ng_prior_share)
+        self.params0, self.params1, self.noise, self.zz, self.spec0, self.spec1, self.dims = a
+        self.m, self.H, self.x = m, H, train_xt
+        self.want_ng = bool(natural_gradient)
+        self.stream = stream
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(train_xt.device))
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            self.pre = _HensmanPre(self.params0, self.params1, self.noise, m, H, train_xt, self.zz, self.spec0,
+                                   self.spec1, self.dims, self.want_ng, train_xt.device)
+            self.pre.run(1)
+        self.consumed = False
+
+    def join(self):
+        """Make the current stream wait for part 1 (and own its buffers)."""
+        if self.stream is None:
+            return
+        cur = torch.cuda.current_stream(self.pre.ws.device)
+        cur.wait_stream(self.stream)
+        pre = self.pre
+        for t in (pre.p0, pre.p1, pre.nz, pre.m64, pre.H64, pre.x64, pre.z64, pre.ws, pre.kld, pre.gm, pre.gH,
+                  pre.info):
+            if t is not None:
+                t.record_stream(cur)
+
+
 class _HensmanFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, params0, params1, noise, mu, logv, m, H, x, z, spec0, spec1, dims, want_ng):
-        lib = _lib.lib()
+    def forward(ctx, params0, params1, noise, mu, logv, m, H, x, z, spec0, spec1, dims, want_ng, pre=None):
         dev = mu.device
         f64 = lambda t: t.detach().to(torch.float64).contiguous()
-        p0, p1, nz = f64(params0), f64(params1), f64(noise).reshape(-1)
-        mu64, lv64, m64, H64, x64, z64 = f64(mu), f64(logv), f64(m), f64(H), f64(x), f64(z)
+        mu64, lv64 = f64(mu), f64(logv)
         L, M = dims.L, dims.M
-        ws = torch.empty(int(lib.lvae_hensman_workspace_size(dims)), dtype=torch.uint8, device=dev)
-        kld = torch.empty((), dtype=torch.float64, device=dev)
-        gm = torch.empty(L, M, 1, dtype=torch.float64, device=dev) if want_ng else None
-        gH = torch.empty(L, M, M, dtype=torch.float64, device=dev) if want_ng else None
-        info = torch.empty(L, dtype=torch.int32, device=dev)
-        rc = lib.lvae_hensman_fwd_f64(spec0, spec1, dims, _lib.ptr(x64), _lib.ptr(z64), _lib.ptr(m64),
-                                      _lib.ptr(H64), _lib.ptr(mu64), _lib.ptr(lv64), _lib.ptr(p0), _lib.ptr(p1),
-                                      _lib.ptr(nz), _lib.ptr(kld), _lib.ptr(gm), _lib.ptr(gH), _lib.ptr(info),
-                                      _lib.ptr(ws), _lib.stream_ptr())
-        _lib.check(rc, "hensman_fwd")
+        if pre is None:
+            pre = _HensmanPre(params0, params1, noise, m, H, x, z, spec0, spec1, dims, want_ng, dev)
+            pre.run(0, mu64, lv64)
+        else:  # part 1 ran ahead (HensmanPrior)
+            pre.run(2, mu64, lv64)
+        lib = _lib.lib()
+        p0, p1, nz, m64, H64, x64, z64, ws = pre.p0, pre.p1, pre.nz, pre.m64, pre.H64, pre.x64, pre.z64, pre.ws
+        kld, gm, gH, info = pre.kld, pre.gm, pre.gH, pre.info
         _check_info(info, "minibatch_KLD_upper_bound cholesky (10000+col: K0zz, 20000+col: B_st, 30000+col: H)")
         ctx.save_for_backward(p0, p1, nz, mu64, lv64, m64, H64, x64, z64, ws)
         ctx.spec0, ctx.spec1, ctx.dims = spec0, spec1, dims
@@ -358,16 +416,33 @@ class _HensmanFn(torch.autograd.Function):
         t0, t1, tn, nshape, tmu, tlv, tm, tH = ctx.dtypes
         return (dp0.to(t0), dp1.to(t1), dnz.to(tn).reshape(nshape), dmu.to(tmu), dlv.to(tlv),
                 None if dm is None else dm.to(tm), None if dH is None else dH.to(tH),
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def minibatch_KLD_upper_bound(covar_module0, covar_module1, likelihood, latent_dim, m, H, train_xt, mu, log_v, z,
-                              P_tot, P_batch, T, natural_gradient, eps, ng_prior_share=1.0):
+                              P_tot, P_batch, T, natural_gradient, eps, ng_prior_share=1.0, prior=None):
     """Unbiased mini-batch estimate of the KL upper bound and (natural_gradient) its natural-gradient
     directions wrt (m, H) -- same signature and return as elbo_functions.py:144-216.
 
     ng_prior_share (extension): weight of the data-independent part of grad_m / grad_H; 1/world
-    under data parallelism so that the SUM over ranks equals the union batch's directions."""
+    under data parallelism so that the SUM over ranks equals the union batch's directions.
+    prior (extension): a HensmanPrior of the same arguments, launched ahead (its part 1 is not redone)."""
+    if prior is not None:
+        if prior.consumed:
+            raise RuntimeError("minibatch_KLD_upper_bound: this HensmanPrior was already used")
+        prior.consumed = True
+        prior.join()
+        return _HensmanFn.apply(prior.params0, prior.params1, prior.noise, mu, log_v, prior.m, prior.H, prior.x,
+                                prior.zz, prior.spec0, prior.spec1, prior.dims, prior.want_ng, prior.pre)
+    a = _hensman_args(covar_module0, covar_module1, likelihood, latent_dim, H, train_xt, z, P_tot, P_batch, T,
+                      natural_gradient, eps, ng_prior_share)
+    params0, params1, noise, zz, spec0, spec1, dims = a
+    return _HensmanFn.apply(params0, params1, noise, mu, log_v, m, H, train_xt, zz, spec0, spec1, dims,
+                            bool(natural_gradient))
+
+
+def _hensman_args(covar_module0, covar_module1, likelihood, latent_dim, H, train_xt, z, P_tot, P_batch, T,
+                  natural_gradient, eps, ng_prior_share):
     spec0, params0 = kernel_spec_and_params(covar_module0)
     spec1, params1 = kernel_spec_and_params(covar_module1)
     L, M = latent_dim, H.shape[-1]
@@ -384,9 +459,7 @@ def minibatch_KLD_upper_bound(covar_module0, covar_module1, likelihood, latent_d
     zz = z if z.dim() == 3 else z.unsqueeze(0).expand(L, -1, -1)
     dims = _lib.HensmanDims(L, M, int(P_batch), int(T), int(Q), float(P_tot), float(eps), int(bool(natural_gradient)),
                             float(ng_prior_share))
-    kld, gm, gH = _HensmanFn.apply(params0, params1, noise, mu, log_v, m, H, train_xt, zz, spec0, spec1, dims,
-                                   bool(natural_gradient))
-    return kld, gm, gH
+    return params0, params1, noise, zz, spec0, spec1, dims
 
 
 def _subject_layout(ids):

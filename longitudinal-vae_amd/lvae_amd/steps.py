@@ -189,6 +189,8 @@ class HensmanStep:
 
     def forward_backward(self, img, mask, X, eps=None):
         self.opt.zero_grad(set_to_none=True)
+        # (one stream: HensmanPrior on a second stream beside the ConvVAE forward measured slower in the
+        # graphed step, 1.37-1.39 vs 1.34 ms)
         recon, mu, log_var = self.vae(img, eps)
         mse, nll = self.vae.loss_function(recon, img, mask)
         L = mu.shape[1]

@@ -80,6 +80,45 @@ def test_hensman_golden(hip, name):
         assert rel(H.grad, g["dH"]) < 1e-6
 
 
+@pytest.mark.parametrize("name", ["hensman_ng.npz", "hensman_adam.npz"])
+def test_hensman_prior_split_matches_one_call(hip, name):
+    """HensmanPrior (part 1 ahead of the latents, lvae_hensman_fwd_part_f64; on the caller's stream or a
+    second one) + the rest = the one-call forward, bit for bit: the same kernels on the same operands,
+    values and every gradient."""
+    import lvae_amd as la
+    from lvae_amd.elbo import minibatch_KLD_upper_bound
+    g = golden(name)
+    ng = bool(g["natural_gradient"])
+    args = dict(P_tot=int(g["P_tot"]), P_batch=int(g["P_b"]), T=int(g["T"]), natural_gradient=ng, eps=float(g["eps"]))
+    out = []
+    for split in (False, True, "stream"):
+        k0, k1, lik = build(g)
+        X = torch.tensor(g["X_all"][g["idx"]], device=DEV)
+        Z = torch.tensor(g["Z"], device=DEV)
+        mu = torch.tensor(g["mu"], device=DEV, requires_grad=True)
+        lv = torch.tensor(g["logv"], device=DEV, requires_grad=True)
+        m = torch.tensor(g["m"], device=DEV, requires_grad=not ng)
+        H = torch.tensor(g["H"], device=DEV, requires_grad=not ng)
+        L = int(g["L"])
+        if split:
+            st = torch.cuda.Stream() if split == "stream" else None
+            prior = la.HensmanPrior(k0, k1, lik, L, m, H, X, Z, **args, stream=st)
+            kld, gm, gH = minibatch_KLD_upper_bound(k0, k1, lik, L, m, H, X, mu, lv, Z, **args, prior=prior)
+            with pytest.raises(RuntimeError):
+                minibatch_KLD_upper_bound(k0, k1, lik, L, m, H, X, mu, lv, Z, **args, prior=prior)
+        else:
+            kld, gm, gH = minibatch_KLD_upper_bound(k0, k1, lik, L, m, H, X, mu, lv, Z, **args)
+        kld.backward()
+        grads = [mu.grad, lv.grad] + [p.grad for _, p in k0.named_parameters()] + \
+                [p.grad for _, p in k1.named_parameters()] + [lik._log_noise.grad]
+        grads += [gm, gH] if ng else [m.grad, H.grad]
+        out.append([kld.detach()] + [t.detach().clone() for t in grads])
+    assert rel(out[1][0], g["kld"]) < 1e-8
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("name", ["hensman_iter_ng.npz", "hensman_iter_adam.npz"])
 def test_hensman_iter_varying_T_golden(hip, name):
     """minibatch_KLD_upper_bound_iter (elbo_functions.py:219-307) on subjects of 5..16 time points,
