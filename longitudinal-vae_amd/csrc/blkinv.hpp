@@ -7,8 +7,8 @@
 //
 // Each 16x16 pivot block is factored by one wave entirely in registers (chol16_trinv): a
 // right-looking Cholesky with the factor inverse X = L^-1 built alongside by forward substitution.
-// Column broadcasts inside a 16-lane row use DPP row_newbcast (no LDS round trip); the two
-// cross-row transfers per pivot use ds_bpermute.  In fp64 the panel L_ik is formed by
+// Column broadcasts inside a 16-lane row use DPP row_newbcast, the two cross-row transfers per pivot
+// (row J's values to every lane group) v_permlane32_swap + v_permlane16_swap: no LDS round trip.  In fp64 the panel L_ik is formed by
 // substitution, as LAPACK's potrf (trsm) does; only the diagonal-block solves of passes 2/3 use the
 // explicit X_k (as LAPACK's blocked trtri).  Explicit-inverse panels (X_k or D_k^-1 = X_k^T X_k) or a
 // Gauss-Jordan sweep lose 1.5 to 5 digits at cond ~1e8 (K0zz with its 1e-6 jitter; scripts/micro).
@@ -75,6 +75,27 @@ struct BiTraits<double> {
   }
 };
 
+// lane (G, c) -> every lane (., c): the 16-lane group G's values in all four groups, by two half
+// exchanges (v_permlane32_swap of v with itself duplicates a half, v_permlane16_swap then a row of it)
+// instead of a ds_bpermute round trip through the LDS crossbar
+template <int G>
+__device__ inline unsigned bi_group_bcast32(unsigned v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  const unsigned h = (G >> 1) ? a[1] : a[0];
+  const auto b = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+  return (G & 1) ? b[1] : b[0];
+}
+template <int G>
+__device__ inline float bi_group_bcast(float v) {
+  return __uint_as_float(bi_group_bcast32<G>(__float_as_uint(v)));
+}
+template <int G>
+__device__ inline double bi_group_bcast(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = bi_group_bcast32<G>((unsigned)u), hi = bi_group_bcast32<G>((unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 template <typename T>
 __device__ inline T bi_pick4(T v0, T v1, T v2, T v3, int idx) {
   return idx == 0 ? v0 : (idx == 1 ? v1 : (idx == 2 ? v2 : v3));
@@ -87,8 +108,8 @@ struct Chol16Step {
   typedef BiTraits<T> Tr;
   typedef typename Tr::acc_t acc_t;
   __device__ __attribute__((always_inline)) static inline void run(acc_t& s, acc_t& x, int lane, const int (&irow)[4],
-                                                                   int rsel, int srcl, T* __restrict__ pd,
-                                                                   T* __restrict__ lk, T* __restrict__ ipv, int& bad) {
+                                                                   T* __restrict__ pd, T* __restrict__ lk,
+                                                                   T* __restrict__ ipv, int& bad) {
     constexpr int gj = Tr::grp(J), rj = Tr::reg(J);
     const int lc = lane & 15;
     const T d = Tr::rdlane(s[rj], gj * 16 + J);
@@ -97,8 +118,11 @@ struct Chol16Step {
     T cI[4];  // L[i][J] for this lane's rows i
 #pragma unroll
     for (int r = 0; r < 4; ++r) cI[r] = Tr::template bcast16<J>(s[r]) * ip;
-    const T cC = __shfl(bi_pick4(cI[0], cI[1], cI[2], cI[3], rsel), srcl, 64);  // L[c][J], c = lc
-    const T xj = __shfl(x[rj] * ip, gj * 16 + lc, 64);                           // X[J][c] (final)
+    // L[c][J] (c = lc) = s[J][c] / L_JJ by the symmetry of the Schur complement (both triangles are
+    // updated with the same products): row J's value in column c, held by group gj, broadcast to the
+    // other groups; likewise X[J][c] (final)
+    const T cC = bi_group_bcast<gj>(s[rj]) * ip;
+    const T xj = bi_group_bcast<gj>(x[rj] * ip);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = irow[r];
@@ -114,13 +138,13 @@ struct Chol16Step {
       pd[J] = p;
       ipv[J] = ip;
     }
-    Chol16Step<T, J + 1>::run(s, x, lane, irow, rsel, srcl, pd, lk, ipv, bad);
+    Chol16Step<T, J + 1>::run(s, x, lane, irow, pd, lk, ipv, bad);
   }
 };
 template <typename T>
 struct Chol16Step<T, 16> {
   __device__ static inline void run(typename BiTraits<T>::acc_t&, typename BiTraits<T>::acc_t&, int, const int (&)[4],
-                                    int, int, T*, T*, T*, int&) {}
+                                    T*, T*, T*, int&) {}
 };
 
 // One wave: Cholesky of the SPD 16x16 tile s (accumulator layout); writes X = L^-1 (lower) to
@@ -140,9 +164,8 @@ __device__ __attribute__((always_inline)) inline int chol16_trinv(typename BiTra
     irow[r] = Tr::row(lane, r);
     x[r] = (irow[r] == lc) ? T(1) : T(0);
   }
-  const int rsel = Tr::reg(lc), srcl = Tr::grp(lc) * 16 + lc;
   int bad = -1;
-  Chol16Step<T, 0>::run(s, x, lane, irow, rsel, srcl, pd, lk, ipv, bad);
+  Chol16Step<T, 0>::run(s, x, lane, irow, pd, lk, ipv, bad);
 #pragma unroll
   for (int r = 0; r < 4; ++r) xout[irow[r] * 17 + lc] = x[r];
   return bad;
