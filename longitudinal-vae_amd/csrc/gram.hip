@@ -1044,10 +1044,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
                                                               double* __restrict__ part, int ntiles,
                                                               const int* __restrict__ covflag) {
   if (*covflag != 2) return;  // (uniform, before any barrier)
-  __shared__ float sx1[kGT * kMaxQB];
-  __shared__ float sx2[kGT * kMaxQB];
+  __shared__ float sx1[2][kGT * kMaxQB];  // (two buffers: this tile's and the next one's)
+  __shared__ float sx2[2][kGT * kMaxQB];
   __shared__ float sp[64];
-  __shared__ float sa1[kGT], sa2[kGT];
+  __shared__ float sa1[2][kGT], sa2[2][kGT];
   __shared__ double wred[4][kBwdSlots];
   extern __shared__ float tdyn[];  // [(n_params + 1) x 256] per-thread sums, then the tables
   const int G = gridDim.x, g0 = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
@@ -1064,8 +1064,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
   const float* ki = Kinv + (int64_t)l * np_ * np_;
   const float* si = S + (int64_t)l * np_ * np_;
   const double* al = alpha + (int64_t)l * np_;
-  // tile t + G's covariates and alpha entries are loaded into registers while tile t is evaluated, and
-  // stored to LDS between two barriers at its end (holding its K^-1 / S rows too was slower: registers)
   auto load_ks = [&](int i0, int j0, g_f32x4 (&kv4)[4], g_f32x4 (&sv4)[4]) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -1083,30 +1081,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
   };
   float dd = 0.f;
   int since_flush = 0;
-  int t = g0, I = 0, J = 0;
+  int t = g0, I = 0, J = 0, In = 0, Jn = 0;
   g_f32x4 kv4[4], sv4[4];
   CovPrefetchF pf;
   double an = 0.0;
+  // software pipeline: tile t's K^-1 / S rows are loaded into registers during tile t - G and its
+  // covariates / alpha entries during tile t - 2G (stored to the other LDS buffer at the end of tile
+  // t - G), so that no tile waits for a global round trip and one barrier per tile suffices
   if (t < ntiles) {
     tri_index(t, I, J);
     load_ks(I * kGT, J * kGT, kv4, sv4);
     pf.load(x, ldx, n, qs, I * kGT, J * kGT);
     if (tid < 2 * kGT) an = al[(tid < kGT ? I : J) * kGT + (tid & (kGT - 1))];
-    pf.store(qs, sx1, sx2);
-    if (tid < kGT) sa1[tid] = float(an);
-    else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
-  }
-  __syncthreads();  // the tables and the first tile's LDS
-  for (; t < ntiles; t += G) {
-    const int i0 = I * kGT, j0 = J * kGT;
-    const bool more = t + G < ntiles;
-    int In = 0, Jn = 0;
-    if (t != g0) load_ks(i0, j0, kv4, sv4);
-    if (more) {
+    pf.store(qs, sx1[0], sx2[0]);
+    if (tid < kGT) sa1[0][tid] = float(an);
+    else if (tid < 2 * kGT) sa2[0][tid - kGT] = float(an);
+    if (t + G < ntiles) {
       tri_index(t + G, In, Jn);
       pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
       if (tid < 2 * kGT) an = al[(tid < kGT ? In : Jn) * kGT + (tid & (kGT - 1))];
     }
+  }
+  __syncthreads();  // the tables and the first tile's LDS
+  for (int b = 0; t < ntiles; t += G, b ^= 1) {
+    const int i0 = I * kGT, j0 = J * kGT;
+    const bool more = t + G < ntiles;
+    const float* __restrict__ cx1 = sx1[b];
+    const float* __restrict__ cx2 = sx2[b];
     float g[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -1115,17 +1116,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int j = j0 + 4 * tc + c;
-        const float gv = 0.5f * (kv[c] - sv[c] - sa1[4 * tr + a] * sa2[4 * tc + c]);
+        const float gv = 0.5f * (kv[c] - sv[c] - sa1[b][4 * tr + a] * sa2[b][4 * tc + c]);
         const bool in = i < n && j < n && j <= i;
         if (in && i == j) dd += gv;
         g[a][c] = in ? ((i == j) ? gv : 2.f * gv) : 0.f;
       }
     }
+    if (more) load_ks(In * kGT, Jn * kGT, kv4, sv4);  // (in flight under this tile's tables)
 #pragma unroll 1
     for (int gi = 0; gi < tb.ng; ++gi) {
       int idx[4][4];  // (the gate bits recomputed per group: fewer live registers)
-      tab_bits(tb, sx1, sx2, tr, tc, idx);
-      tab_index(tb, gi, sx1, sx2, tr, tc, idx, idx);
+      tab_bits(tb, cx1, cx2, tr, tc, idx);
+      tab_index(tb, gi, cx1, cx2, tr, tc, idx, idx);
 #pragma unroll 1
       for (int k = tb.pbeg[gi]; k < tb.pbeg[gi + 1]; ++k) {
         const float* tk = tab + k * tstride;
@@ -1149,12 +1151,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
       }
     }
     if (more) {
-      __syncthreads();  // every reader of this tile's LDS is done
-      pf.store(qs, sx1, sx2);
-      if (tid < kGT) sa1[tid] = float(an);
-      else if (tid < 2 * kGT) sa2[tid - kGT] = float(an);
-      __syncthreads();
-      I = In, J = Jn;
+      // tile t + G's covariates (loaded during the previous tile) to the other buffer, whose last
+      // readers finished before the previous barrier; then tile t + 2G's go in flight
+      pf.store(qs, sx1[b ^ 1], sx2[b ^ 1]);
+      if (tid < kGT) sa1[b ^ 1][tid] = float(an);
+      else if (tid < 2 * kGT) sa2[b ^ 1][tid - kGT] = float(an);
+      int I2 = 0, J2 = 0;
+      if (t + 2 * G < ntiles) {
+        tri_index(t + 2 * G, I2, J2);
+        pf.load(x, ldx, n, qs, I2 * kGT, J2 * kGT);
+        if (tid < 2 * kGT) an = al[(tid < kGT ? I2 : J2) * kGT + (tid & (kGT - 1))];
+      }
+      __syncthreads();  // buffer b ^ 1 written; every reader of buffer b done
+      I = In, J = Jn, In = I2, Jn = J2;
     }
   }
   __syncthreads();
