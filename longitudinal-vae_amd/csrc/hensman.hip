@@ -36,6 +36,8 @@ int gemm_small_f64(int ta, int tb, int m, int n, int k, double alpha, const doub
 
 namespace {
 
+constexpr int kHnSlices = 8;  // workgroups per latent dim of hn_reduce_kernel
+
 struct HWs {
   // [L,B,M]
   double *K0xz, *iBK, *dK0xz, *tBM;
@@ -70,7 +72,7 @@ struct HWs {
     ldB = take(L * d.P_b);
     ldH = take(L);
     epsv = take(L);
-    part = take(L * 16);
+    part = take(L * 16 * kHnSlices);
     info = (int32_t*)take(L * (2 + d.P_b));
     // Gram-adjoint partials of the four Grams (gram.hip, kGBChunk = 1024 elements per chunk, <= 145 slots)
     const size_t chunks = (B * M + 1023) / 1024 + (M * M + 1023) / 1024 + 2 * ((TT + 1023) / 1024);
@@ -115,7 +117,8 @@ __global__ void resid_kernel(const double* __restrict__ y, const double* __restr
   r[e] = seg_valid(seg, i / T, i % T) ? y[e] - mu[(int64_t)i * L + l] : 0.0;
 }
 
-// per-dim partial sums: part[l][0..] = A, Bt, C, D1, D2, E, F, tr1, qf1, ldK, ldH
+// per-dim partial sums, each dim's elements split over kHnSlices workgroups (more reads in flight than one
+// workgroup per dim): part[l][slice][0..] = A, Bt, C, D1, D2, E, F, tr1, qf1, ldK, ldH
 __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, int L, const double* __restrict__ r,
                                                         const double* __restrict__ s, const double* __restrict__ iB,
                                                         const double* __restrict__ logv,
@@ -128,11 +131,12 @@ __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, i
                                                         const double* __restrict__ ldH,
                                                         const int32_t* __restrict__ seg, double* __restrict__ part) {
   __shared__ double red[4];
-  const int l = blockIdx.x, tid = threadIdx.x;
+  const int l = blockIdx.x, sl = blockIdx.y, tid = threadIdx.x + 256 * sl;
+  constexpr int kStep = 256 * kHnSlices;
   const int B = P_b * T;
   const int64_t MM = (int64_t)M * M, TT = (int64_t)P_b * T * T;
   double A = 0, Bt = 0, C = 0, D1 = 0, D2 = 0, E = 0, F = 0, tr1 = 0, qf1 = 0;
-  for (int i = tid; i < B; i += 256) {
+  for (int i = tid; i < B; i += kStep) {
     A += r[(int64_t)l * B + i] * s[(int64_t)l * B + i];
     const int p = i / T, q = i % T;
     if (!seg_valid(seg, p, q)) continue;
@@ -140,9 +144,9 @@ __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, i
     Bt += iB[l * TT + (int64_t)p * T * T + q * T + q] * exp(lv);
     F += lv;
   }
-  for (int p = tid; p < P_b; p += 256) C += ldB[(int64_t)l * P_b + p];
-  for (int64_t e = tid; e < TT; e += 256) D1 += iB[l * TT + e] * K0st[l * TT + e];
-  for (int64_t e = tid; e < MM; e += 256) {
+  for (int p = tid; p < P_b; p += kStep) C += ldB[(int64_t)l * P_b + p];
+  for (int64_t e = tid; e < TT; e += kStep) D1 += iB[l * TT + e] * K0st[l * TT + e];
+  for (int64_t e = tid; e < MM; e += kStep) {
     const double q = Q[l * MM + e], ik = iK[l * MM + e];
     D2 += q * ik;
     // E = sum Y^T .* Q = sum Y .* Q (Y symmetric up to rounding: use the transposed element as the reference)
@@ -150,16 +154,17 @@ __global__ __launch_bounds__(256) void hn_reduce_kernel(int M, int P_b, int T, i
     E += Y[l * MM + (int64_t)j * M + i] * q;
     tr1 += ik * H[l * MM + (int64_t)j * M + i];
   }
-  for (int i = tid; i < M; i += 256) qf1 += m[(int64_t)l * M + i] * t[(int64_t)l * M + i];
+  for (int i = tid; i < M; i += kStep) qf1 += m[(int64_t)l * M + i] * t[(int64_t)l * M + i];
   double vals[9] = {A, Bt, C, D1, D2, E, F, tr1, qf1};
+  double* pp = part + ((int64_t)l * kHnSlices + sl) * 16;
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const double v = block_sum<256>(vals[q], red);
-    if (tid == 0) part[l * 16 + q] = v;
+    if (threadIdx.x == 0) pp[q] = v;
   }
-  if (tid == 0) {
-    part[l * 16 + 9] = ldK[l];
-    part[l * 16 + 10] = ldH[l];
+  if (threadIdx.x == 0) {
+    pp[9] = sl == 0 ? ldK[l] : 0.0;
+    pp[10] = sl == 0 ? ldH[l] : 0.0;
   }
 }
 
@@ -169,7 +174,11 @@ __global__ void hn_final_kernel(int L, int M, double P_tot, int P_b, double n_to
   double tot = 0.0;
   const double c0 = P_tot / (double)P_b;
   for (int l = 0; l < L; ++l) {
-    const double* p = part + l * 16;
+    double p[11];  // the slices' sums, in slice order
+    for (int q = 0; q < 11; ++q) {
+      p[q] = 0.0;
+      for (int sl = 0; sl < kHnSlices; ++sl) p[q] += part[((int64_t)l * kHnSlices + sl) * 16 + q];
+    }
     const double inner = p[0] + p[1] + p[2] + (p[3] - p[4]) + p[5] - p[6];
     const double klu = 0.5 * (p[7] + p[8] - (double)M + p[9] - p[10]);
     tot += c0 * 0.5 * inner + klu;
@@ -377,7 +386,7 @@ int lvae_hensman_fwd_part_f64(int part, const lvae_kernel_spec* spec0, const lva
     resid_kernel<<<blocks((int64_t)B * L), 256, 0, st>>>(w.y, mu, B, L, T, d.seg_len, w.r);
     LVAE_TRY(gemm_small_f64(0, 0, T, 1, T, 1.0, w.iB, T, P_b * TT, TT, w.r, 1, B, T, 0.0, w.s, 1, B, T, L, P_b, st));
     // partial sums + total (189-204)
-    hn_reduce_kernel<<<L, 256, 0, st>>>(M, P_b, T, L, w.r, w.s, w.iB, logv, w.ldB, w.K0st, w.Q, w.iK, w.Y, H, m,
+    hn_reduce_kernel<<<dim3(L, kHnSlices), 256, 0, st>>>(M, P_b, T, L, w.r, w.s, w.iB, logv, w.ldB, w.K0st, w.Q, w.iK, w.Y, H, m,
                                         w.t, w.ldK, w.ldH, d.seg_len, w.part);
     hn_final_kernel<<<1, 64, 0, st>>>(L, M, d.P_tot, P_b, d.n_total > 0.0 ? d.n_total : d.P_tot * T, w.part, kld);
     if (ng) {  // u = iB mu ; w = K0xz^T u ; a = iK w ; grad_m = Bn m - a
