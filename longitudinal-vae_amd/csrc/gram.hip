@@ -58,17 +58,20 @@ __device__ inline T kernel_eval_tab(const DevSpec& s, const double* __restrict__
   return sum;
 }
 
+// one 64 x 64 output block (bx, by) of Gram bz = b * L + l
 template <int MC, int MF, typename T>
-__global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lvae_xview x2, int L, int n1, int n2,
-                                                   int qs, const double* __restrict__ params,
-                                                   const double* __restrict__ diag, T* __restrict__ out,
-                                                   int64_t osb, int64_t osl, int64_t ldo) {
+__device__ __attribute__((always_inline)) inline void gram_block(const DevSpec& s, const lvae_xview& x1,
+                                                                 const lvae_xview& x2, int L, int n1, int n2, int qs,
+                                                                 const double* __restrict__ params,
+                                                                 const double* __restrict__ diag, T* __restrict__ out,
+                                                                 int64_t osb, int64_t osl, int64_t ldo, int bx, int by,
+                                                                 int bz) {
   __shared__ double sx1[kGT * kMaxQ];
   __shared__ double sx2[kGT * kMaxQ];
   __shared__ T sp[64];
   __shared__ T tab[MC * MF * kGTab];
-  const int bl = blockIdx.z, b = bl / L, l = bl % L;
-  const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * kGT;
+  const int bl = bz, b = bl / L, l = bl % L;
+  const int i0 = by * kGT, j0 = bx * kGT;
   const int tid = threadIdx.x;
   if (tid < s.n_params) sp[tid] = T(params[(int64_t)l * s.n_params + tid]);
   __syncthreads();
@@ -99,6 +102,35 @@ __global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lva
     if (i == j) v += dg;
     o[(int64_t)i * ldo + j] = v;
   }
+}
+
+template <int MC, int MF, typename T>
+__global__ __launch_bounds__(256) void gram_kernel(DevSpec s, lvae_xview x1, lvae_xview x2, int L, int n1, int n2,
+                                                   int qs, const double* __restrict__ params,
+                                                   const double* __restrict__ diag, T* __restrict__ out,
+                                                   int64_t osb, int64_t osl, int64_t ldo) {
+  gram_block<MC, MF, T>(s, x1, x2, L, n1, n2, qs, params, diag, out, osb, osl, ldo, blockIdx.x, blockIdx.y,
+                        blockIdx.z);
+}
+
+// several fp64 Grams in one launch (the Hensman forward's four: K0xz, K0zz, K0_p with spec0, B_p with
+// spec1): a 1-D grid over every job's blocks, block r of job q at (r % gx, r / gx % gy, r / (gx gy))
+constexpr int kGFMaxJobs = 4;
+struct GramFwdJobs {
+  DevSpec s[2];
+  int qs[2];
+  GramFwdJob j[kGFMaxJobs];
+  int njobs;
+};
+
+template <int MC, int MF>
+__global__ __launch_bounds__(256) void gram_multi_kernel(GramFwdJobs J, int L) {
+  int q = 0;
+  while (q + 1 < J.njobs && (int)blockIdx.x >= J.j[q + 1].blk0) ++q;  // (uniform)
+  const GramFwdJob& jb = J.j[q];
+  const int r = blockIdx.x - jb.blk0;
+  gram_block<MC, MF, double>(J.s[jb.spec], jb.x1, jb.x2, L, jb.n1, jb.n2, J.qs[jb.spec], jb.params, jb.diag, jb.out,
+                             jb.osb, jb.osl, jb.ldo, r % jb.gx, (r / jb.gx) % jb.gy, r / (jb.gx * jb.gy));
 }
 
 // Adjoint, generic strided G (fp64), several Grams in one launch (the Hensman backward contracts
@@ -1449,6 +1481,38 @@ static int gram_launch(const lvae_kernel_spec* spec, lvae_xview x1, lvae_xview x
     gram_kernel<8, 2, T><<<grid, block, 0, st>>>(ds, x1, x2, L, n1, n2, qs, params, diag, out, osb, osl, ldo);
   else
     gram_kernel<16, 4, T><<<grid, block, 0, st>>>(ds, x1, x2, L, n1, n2, qs, params, diag, out, osb, osl, ldo);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// host: up to kGFMaxJobs fp64 Grams (descriptors as lvae_gram_f64's arguments; spec index into specs[0..1])
+int gram_multi_f64(const lvae_kernel_spec* const* specs, const GramFwdJob* jobs, int njobs, int L, hipStream_t st) {
+  if (njobs < 1 || njobs > kGFMaxJobs || L < 1) return -4;
+  GramFwdJobs J{};
+  int bucket = 0, blocks = 0;
+  for (int k = 0; k < 2; ++k) {
+    if (!specs[k]) continue;
+    const int bk = spec_bucket(specs[k]);
+    if (!bk || spec_qs(specs[k]) > kMaxQ) return -1;
+    bucket = bk > bucket ? bk : bucket;
+    J.s[k] = to_dev(specs[k]);
+    J.qs[k] = spec_qs(specs[k]);
+  }
+  J.njobs = 0;
+  for (int q = 0; q < njobs; ++q) {
+    GramFwdJob jb = jobs[q];
+    if (jb.spec < 0 || jb.spec > 1 || !specs[jb.spec]) return -1;
+    if (jb.nb < 1 || jb.n1 < 0 || jb.n2 < 0) return -4;
+    if (jb.n1 == 0 || jb.n2 == 0) continue;
+    jb.gx = cdiv(jb.n2, kGT), jb.gy = cdiv(jb.n1, kGT), jb.blk0 = blocks;
+    blocks += jb.gx * jb.gy * jb.nb * L;
+    J.j[J.njobs++] = jb;
+  }
+  if (J.njobs == 0) return 0;
+  if (bucket == 1)
+    gram_multi_kernel<8, 2><<<blocks, 256, 0, st>>>(J, L);
+  else
+    gram_multi_kernel<16, 4><<<blocks, 256, 0, st>>>(J, L);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -353,10 +353,14 @@ int lvae_hensman_fwd_part_f64(int part, const lvae_kernel_spec* spec0, const lva
     // Grams (elbo_functions.py:171-176)
     fill_kernel<<<blocks(L), 256, 0, st>>>(w.epsv, L, d.eps);
     const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
-    LVAE_TRY(lvae_gram_f64(spec0, xv, zv, 1, L, B, M, params0, nullptr, w.K0xz, 0, BM, M, stream));
-    LVAE_TRY(lvae_gram_f64(spec0, zv, zv, 1, L, M, M, params0, w.epsv, w.K0zz, 0, MM, M, stream));
-    LVAE_TRY(lvae_gram_f64(spec0, xs, xs, P_b, L, T, T, params0, nullptr, w.K0st, TT, P_b * TT, T, stream));
-    LVAE_TRY(lvae_gram_f64(spec1, xs, xs, P_b, L, T, T, params1, noise, w.Bst, TT, P_b * TT, T, stream));
+    // (the four in one launch: gram_multi_f64)
+    const lvae_kernel_spec* specs[2] = {spec0, spec1};
+    const GramFwdJob jobs[4] = {
+        {0, 1, B, M, 0, 0, 0, xv, zv, params0, nullptr, w.K0xz, 0, BM, M},
+        {0, 1, M, M, 0, 0, 0, zv, zv, params0, w.epsv, w.K0zz, 0, MM, M},
+        {0, P_b, T, T, 0, 0, 0, xs, xs, params0, nullptr, w.K0st, TT, P_b * TT, T},
+        {1, P_b, T, T, 0, 0, 0, xs, xs, params1, noise, w.Bst, TT, P_b * TT, T}};
+    LVAE_TRY(gram_multi_f64(specs, jobs, 4, L, st));
     if (d.seg_len)
       hn_seg_mask_kernel<<<blocks((int64_t)L * B * M + (int64_t)L * P_b * TT), 256, 0, st>>>(
           L, P_b, T, M, d.seg_len, w.K0xz, w.K0st, w.Bst);
