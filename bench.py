@@ -230,10 +230,10 @@ def max_over_ranks(x, world, dev):
 # ------------------------------------------------------------------------------------------
 # CPU baselines (the oracle, fp64 torch-CPU, the reference's op sequence) -- rank 0, N = 1 only
 # ------------------------------------------------------------------------------------------
-def cpu_baseline_closed(P, T, L, threads8_dims=1, reps=3):
-    """The C3 step on the CPU port (fp64), by BASELINE.md's method bounded to ~25 s: one warm-up, then
-    the median of `reps` timings of the ConvVAE fwd/bwd on all N images and of one latent dim's
-    KL_closed fwd/bwd (every dim costs the same: same N, same kernel), the step = ConvVAE + L x dim;
+def cpu_baseline_closed(P, T, L, threads8_dims=1, warmups=3):
+    """The C3 step on the CPU port (fp64), by BASELINE.md's / SURVEY.md 8(d)'s method within one lease:
+    `warmups` warm-up steps (ConvVAE fwd/bwd on all N images + one latent dim's KL_closed fwd/bwd each),
+    then ONE whole timed step: the ConvVAE fwd/bwd and all L latent dims' KL_closed fwd/bwd (~60 s at C3);
     plus an 8-thread figure (ConvVAE + one dim, x L dims) for comparison with the survey container's
     numbers."""
     from oracle import lvae_oracle as O
@@ -262,15 +262,14 @@ def cpu_baseline_closed(P, T, L, threads8_dims=1, reps=3):
         return t_vae, time.perf_counter() - t0
 
     nthreads = torch.get_num_threads()
-    step(1)  # warm-up (allocator, thread pool, first touch)
-    runs = [step(1, l0=1 + k) for k in range(reps)]
-    t_vae = sorted(r[0] for r in runs)[reps // 2]
-    t_dim = sorted(r[1] for r in runs)[reps // 2]
-    t_step = t_vae + L * t_dim
+    for k in range(warmups):  # warm-ups (allocator, thread pool, first touch)
+        step(1, l0=k)
+    t_vae, t_kl = step(L)
+    t_step = t_vae + t_kl
     res = dict(value=1.0 / t_step, unit="ELBO-steps/s", cores=nthreads, kind="port",
-               sample=(f"oracle fp64 torch-CPU, {nthreads} threads, median of {reps} after 1 warm-up: ConvVAE "
-                       f"fwd/bwd on all {N} images ({t_vae:.2f} s) + KL_closed fwd/bwd of one latent dim "
-                       f"({t_dim:.2f} s) x {L} dims = {t_step:.1f} s per step"))
+               sample=(f"oracle fp64 torch-CPU, {nthreads} threads, one whole step after {warmups} warm-ups: "
+                       f"ConvVAE fwd/bwd on all {N} images ({t_vae:.2f} s) + KL_closed fwd/bwd of all {L} latent "
+                       f"dims ({t_kl:.2f} s) = {t_step:.1f} s per step"))
     try:
         torch.set_num_threads(8)
         v8, k8 = step(threads8_dims)
@@ -593,7 +592,9 @@ def run_c2(dev, reps=20):
     A = torch.empty(L, np_, np_, dtype=torch.float32, device=dev)
     Kinv = torch.empty_like(A)
     scr = torch.empty(int(lib.lvae_spd_inv_chol_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
-    sscr = torch.empty(int(lib.lvae_spd_sweep_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
+    with_sweep = os.environ.get("LVAE_BENCH_SWEEP") == "1"  # the retired sweep: opt-in extra
+    sscr = (torch.empty(int(lib.lvae_spd_sweep_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
+            if with_sweep else None)
     logdet = torch.empty(L, dtype=torch.float64, device=dev)
     info = torch.empty(L, dtype=torch.int32, device=dev)
     noise = torch.ones(L, dtype=torch.float64, device=dev)
@@ -654,7 +655,18 @@ def run_c2(dev, reps=20):
     t_gram_torch = timed(lambda: torch_gram_f32(params, X))
     t_potrf_torch = timed(lambda: torch_potrf_only(Kt))
     t_chol, t_inv = timed(torch_chol), timed(torch_chol_inv)
-    t_sweep = timed(hip_sweep)
+    t_sweep = timed(hip_sweep) if with_sweep else None
+    # the exported N x N factor (lvae_potrf_f32 / _f64 through lvae_amd.linalg) on the same prebuilt Gram,
+    # against torch.linalg.cholesky on it: the same input, the same output (L)
+    import lvae_amd.linalg as LA
+    t_potrf_export = timed(lambda: LA.cholesky_ex(Kt))
+    Kt64 = Kt.double()
+    t_potrf64_export = timed(lambda: LA.cholesky_ex(Kt64))
+    t_potrf64_torch = timed(lambda: torch_potrf_only(Kt64))
+    L32 = LA.cholesky_ex(Kt)[0]
+    Lref64 = torch.linalg.cholesky(Kt64)
+    err_l32 = float((L32.double() - Lref64).abs().max() / Lref64.abs().max())
+    err_l64 = float((LA.cholesky_ex(Kt64)[0] - Lref64).abs().max() / Lref64.abs().max())
     ref_inv, ref_ld = torch_chol_inv()
     err = float((inv_chol - ref_inv).abs().max() / ref_inv.abs().max())
     flop = L * N ** 3 / 3
@@ -671,9 +683,19 @@ def run_c2(dev, reps=20):
                                         "torch: torch.linalg.cholesky on the prebuilt fp32 Gram)",
             "hip_vs_torch_inverse_max_rel_diff": err, "hip_info_ok": info_ok,
             "logdet_max_rel_diff": float(((ld_chol.float() - ref_ld).abs() / ref_ld.abs()).max()),
-            "extra_retired_sweep": {"hip_gram_sweep_inverse_ms": t_sweep,
-                                    "note": "lvae_spd_sweep_f32, the rounds 1-2 block Gauss-Jordan inverse; the KL "
-                                            "no longer uses it"},
+            "potrf_export": {"lvae_potrf_f32_ms": t_potrf_export, "torch_cholesky_f32_ms": t_potrf_torch,
+                             "speedup_f32": t_potrf_torch / t_potrf_export,
+                             "gflops_f32": flop / (t_potrf_export * 1e-3) / 1e9,
+                             "lvae_potrf_f64_ms": t_potrf64_export, "torch_cholesky_f64_ms": t_potrf64_torch,
+                             "speedup_f64": t_potrf64_torch / t_potrf64_export,
+                             "gflops_f64": flop / (t_potrf64_export * 1e-3) / 1e9,
+                             "L_max_rel_diff_vs_torch_f64": {"f32": err_l32, "f64": err_l64},
+                             "note": "the C-ABI N x N factor (potrf.hip) on the prebuilt Gram, returning L, vs "
+                                     "torch.linalg.cholesky (rocSOLVER) on the same matrix; f32 includes the copy "
+                                     "into the padded workspace and out of it"},
+            **({"extra_retired_sweep": {"hip_gram_sweep_inverse_ms": t_sweep,
+                                        "note": "lvae_spd_sweep_f32, the rounds 1-2 block Gauss-Jordan inverse; the "
+                                                "KL no longer uses it (LVAE_BENCH_SWEEP=1)"}} if with_sweep else {}),
             "note": "HIP: Gram + Cholesky route (K^-1 and log|K|); torch: PyTorch fp32 Gram + torch.linalg.cholesky "
                     "(rocSOLVER) [+ cholesky_inverse + log-det for the same outputs]"}
 

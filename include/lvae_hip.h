@@ -19,6 +19,8 @@
  *   covar_module(x1, x2).evaluate()       -> lvae_gram_*            (GP_model.py:31-144,
  *                                             kernel_gen.py:9-310, call sites elbo_functions.py:22,56,171-174)
  *   autograd of that Gram wrt (scale, lengthscale) -> lvae_gram_bwd_*
+ *   torch.cholesky(K1) on N x N           -> lvae_potrf_f64 / _f32 (elbo_functions.py:26)
+ *   torch.cholesky_solve(B, LK1)          -> lvae_potrs_f64 / _f32, lvae_trsm_* (elbo_functions.py:27-28)
  *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_spd_inv_chol_f32 (also
  *                                             lvae_spd_sweep_f32; elbo_functions.py:26-29)
  *   KL_closed forward + autograd backward -> lvae_kl_closed_fwd_f32 / _bwd_f32 (elbo_functions.py:8-34)
@@ -126,7 +128,8 @@ int lvae_kl_closed_fwd_f32(const lvae_kernel_spec* spec, const double* x, int ld
  * evaluated from the covariates in fp64, hence spec / x / params / noise again, the same as the
  * factor's -- the trace and quadratic terms, kl, and with need_bwd the S-GEMM operand).  factor then
  * reduce on one stream (or with the reduce stream waiting on the factor's) equals
- * lvae_kl_closed_fwd_f32.                                                                        */
+ * lvae_kl_closed_fwd_f32.  One reduce per factor: the reduce (diag K^-1 refinement) and the backward
+ * reuse the factor's triangular-inverse planes in the workspace.                                 */
 int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
                               const double* params, const double* noise, int32_t* info, void* workspace,
                               void* stream);
@@ -187,6 +190,43 @@ int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Ainv, dou
 size_t lvae_spd_inv_chol_scratch_size(int np_, int L);
 int lvae_spd_inv_chol_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
                           void* stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* N x N factor / solve (potrf.hip): the reference's own LAPACK calls on K1,                   */
+/*   LK1 = torch.cholesky(K1);  torch.cholesky_solve(B, LK1);  logdet = 2 sum log diag(LK1)    */
+/* (elbo_functions.py:26-29), batched over L matrices: element (l, i, j) of a matrix argument   */
+/* at ptr[l*stride + i*ld + j].  Factors are lower triangular with a zero strict upper part    */
+/* (torch.cholesky's output); only the lower triangle of A is read.  info[l] LAPACK-style.     */
+/* ---------------------------------------------------------------------------------------- */
+/* Lout <- chol(A) in fp64, log|A| into logdet[l]: 64-wide blocked right-looking potrf, the panel
+ * by substitution (as LAPACK's trsm), the trailing update on the fp64 matrix cores.  Lout may be
+ * A itself (in place; then ldo == lda and stride_o == stride_a).  No workspace.              */
+int lvae_potrf_f64(int n, int L, const double* A, int64_t lda, int64_t stride_a, double* Lout, int64_t ldo,
+                   int64_t stride_o, double* logdet, int32_t* info, void* stream);
+/* The same in fp32 through the exact KL's own factorisation (chol_inv.hip: 256-wide blocks, the
+ * pivot blocks on fp32 MFMA in LDS, panels and trailing updates on the f16 cores with the 3-product
+ * split, ~2^-22 of each 256-block's max per product).  A is copied into the workspace (padded to a
+ * multiple of 256 with the identity), so Lout may alias A.  workspace:
+ * lvae_potrf_f32_workspace_size(n, L) bytes, 256-B aligned.  n <= 16384.                       */
+size_t lvae_potrf_f32_workspace_size(int n, int L);
+int lvae_potrf_f32(int n, int L, const float* A, int64_t lda, int64_t stride_a, float* Lout, int64_t ldo,
+                   int64_t stride_o, double* logdet, int32_t* info, void* workspace, void* stream);
+/* B [n, nrhs] <- op(Lf)^-1 B in place, op = Lf (trans = 0) or Lf^T (trans = 1), Lf lower
+ * triangular (e.g. lvae_potrf_*'s output).  Blocked over 64 rows: the 64 x 64 diagonal blocks are
+ * inverted first into the workspace (lvae_trsm_workspace_size(n, L) bytes, 256-B aligned), then one
+ * workgroup per 64 columns of B sweeps the block rows in dependency order on the fp64 matrix cores.
+ * The f32 variant reads / writes fp32 and computes in fp64.                                      */
+size_t lvae_trsm_workspace_size(int n, int L);
+int lvae_trsm_f64(int trans, int n, int nrhs, int L, const double* Lf, int64_t ldl, int64_t stride_l, double* B,
+                  int64_t ldb, int64_t stride_b, void* workspace, void* stream);
+int lvae_trsm_f32(int trans, int n, int nrhs, int L, const float* Lf, int64_t ldl, int64_t stride_l, float* B,
+                  int64_t ldb, int64_t stride_b, void* workspace, void* stream);
+/* B <- A^-1 B given Lf = chol(A): torch.cholesky_solve(B, Lf) (elbo_functions.py:27-28; also
+ * cholesky_solve(eye, LK1) = K1^-1).  Workspace as lvae_trsm_*.                                */
+int lvae_potrs_f64(int n, int nrhs, int L, const double* Lf, int64_t ldl, int64_t stride_l, double* B, int64_t ldb,
+                   int64_t stride_b, void* workspace, void* stream);
+int lvae_potrs_f32(int n, int nrhs, int L, const float* Lf, int64_t ldl, int64_t stride_l, float* B, int64_t ldb,
+                   int64_t stride_b, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Regime A: Hensman SVI, fp64 (elbo_functions.py:144-216; training.py:129-135)             */
@@ -256,6 +296,8 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
  *   iH' = H^-1 + lr (gH + gH^T);  H <- iH'^-1;  m <- H (H^-1 m - lr (gm - 2 gH m)).
  * iH: H^-1 if the caller already has it (e.g. workspace + lvae_hensman_iH_offset after the
  * forward on the same H), else NULL (H is inverted here, as training.py:130-131 does).
+ * info[l] (may be NULL): the first failed factorisation of dim l (H's, then iH''s), LAPACK-style;
+ * a dim whose factorisation fails keeps its (m, H) unchanged.
  * workspace: lvae_natgrad_workspace_size(L, M) bytes.                                        */
 size_t lvae_natgrad_workspace_size(int L, int M);
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m,

@@ -101,6 +101,8 @@ struct CiScratch {
   float* xsc;               // [L][nt][nt] (l, i, j): tile (i, j) of the trtri intermediate X
   _Float16 *XRh[2], *XRl[2];  // pipelined trtri: the X^T tiles (j, m) of row block m, [L][nt][256 x 256] (one
                               // chunk-major tile each), by row parity; nullptr unless ci_pipe_alloc
+  float* lout = nullptr;      // potrf-only export (ci_potrf_f32): the pivots write L_kk, the panels L_ik, in fp32
+                              // into the lower tiles of this [L][np][np] matrix (not part of `bytes`)
   int* cnt;                   // [L][nt] split pivots: arrival tickets per (dim, pass), zeroed per call (own block)
   float* xs;                  // [L][kCiPvG] split pivots: the split scale of each helper's X slab
   int nt;
@@ -456,6 +458,13 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
     __syncthreads();
   }
   CI_STAMP(2);
+  if (S.lout) {  // (potrf-only) L_kk, zero strict upper part, into tile (kb, kb) of lout
+    float* O = S.lout + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
+    for (int e = tid; e < kSwBB; e += 1024) {
+      const int r = e >> 8, c = e & 255;
+      O[(int64_t)r * np_ + c] = c <= r ? pv_blk(lf, r >> 5, c >> 5)[(r & 31) * kPvL + (c & 31)] : 0.f;
+    }
+  }
   if (w < 8) pv_trinv(pv_blk(lf, w, w), lane);
   __syncthreads();
   CI_STAMP(3);
@@ -701,6 +710,15 @@ __global__ __launch_bounds__(512) void ci_panel_kernel(CiScratch S, int np_, int
   const int64_t ot = (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_ + k * kSwB;
   ci_planes_out(acc, inv, sl, S.Lh + ot, S.Ll + ot, np_);
   if (threadIdx.x == 0) S.lsc[((int64_t)l * S.nt + i) * S.nt + k] = sl;
+  if (S.lout) {  // (potrf-only) L_ik in fp32 into tile (i, k) of lout
+    float* O = S.lout + ot;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) O[(int64_t)sx_row(a, e) * np_ + sx_col(b)] = acc[a][b][e] * inv;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1408,14 +1426,18 @@ __global__ __launch_bounds__(512) void ci_pair_kernel(CiGemmArgs g1, CiGemmArgs 
 // instance on the caller's stream between the passes -- measured 15.1 vs 14.2 ms per closed step at
 // L = 16: the small launches slowed the passes more than the overlap saved.)
 size_t ci_scratch_bytes(int np_, int L) { return CiScratch(nullptr, np_, L).bytes; }
+int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
+                  int32_t* info, hipStream_t st, float* lout = nullptr);
 
 // potrf + trtri: Y = L^-1 as the Y^T planes YT (+ the per-tile scales in the scratch); A and Kinv are
 // overwritten (Kinv holds the X^T planes)
+// (lout: potrf only -- no trtri, no pipelined schedule -- with L written in fp32 into lout's lower tiles)
 int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
-                  int32_t* info, hipStream_t st) {
+                  int32_t* info, hipStream_t st, float* lout) {
   if (np_ <= 0 || np_ % kSwB || np_ / kSwB > 64) return -1;
   if (L <= 0) return -2;
   CiScratch S((char*)scratch, np_, L);
+  S.lout = lout;
   const int nt = S.nt;
   const int64_t full = (int64_t)L * np_ * np_;
   _Float16* YTh = YT;
@@ -1436,7 +1458,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     (void)hipMemsetAsync(S.cnt, 0, CiScratch::cnt_bytes(L, nt), st);  // the split pivots' tickets
     if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
     const bool fuse = L <= kCiFuseMaxL;
-    const int pmode = ci_pipe_mode(np_, L);  // (implies fuse and the XR planes)
+    const int pmode = lout ? 0 : ci_pipe_mode(np_, L);  // (implies fuse and the XR planes)
     // the split pivot (kCiPvG workgroups per pending pivot); LVAE_PIVOT_SPLIT=0: one workgroup per dim
     static const bool split_env = !getenv("LVAE_PIVOT_SPLIT") || atoi(getenv("LVAE_PIVOT_SPLIT")) != 0;
     const bool split = split_env;
@@ -1544,6 +1566,7 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     }
   }
   LVAE_CHECK_LAUNCH();
+  if (lout) return 0;
   if (!pipe) {
     // trtri (recursive doubling, 2 launches per level): with lauum (ci_lauum_f32) the rest of potri
     ProfScope ps(LVAE_PH_POTRI, st);
@@ -1614,6 +1637,12 @@ int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv,
   }
   LVAE_CHECK_LAUNCH();
   return 0;
+}
+
+// potrf alone (lvae_potrf_f32): A [L, np, np] -> L in A's lower tiles (fp32; zero strict upper part of the
+// diagonal tiles; the other upper tiles untouched), log|A|, info
+int ci_potrf_f32(int np_, int L, float* A, void* scratch, double* logdet, int32_t* info, hipStream_t st) {
+  return ci_factor_f32(np_, L, A, scratch, nullptr, nullptr, logdet, info, st, A);
 }
 
 int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,

@@ -512,6 +512,24 @@ __global__ void natgrad_y_kernel(int64_t n, double lr, const double* __restrict_
   if (e < n) y[e] = v[e] - lr * gm[e] + 2.0 * lr * gw[e];
 }
 
+// commit: per dim l, (m, H) <- (mn, Hn) only if both factorisations (H^-1 when it was computed here, iH'^-1)
+// succeeded; info[l] = the first failure's LAPACK code (H's, else iH''s), 0 = ok.  A failed dim keeps its
+// (m, H) (the reference raises from torch.cholesky before assigning them, training.py:130-134).
+__global__ void natgrad_commit_kernel(int L, int M, const int32_t* __restrict__ inf, const double* __restrict__ Hn,
+                                      const double* __restrict__ mn, double* __restrict__ H, double* __restrict__ m,
+                                      int32_t* __restrict__ info) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, MM = (int64_t)M * M;
+  if (e < L * MM) {
+    const int l = (int)(e / MM);
+    if (inf[l] == 0 && inf[L + l] == 0) H[e] = Hn[e];
+  } else if (e < L * MM + (int64_t)L * M) {
+    const int64_t q = e - L * MM;
+    const int l = (int)(q / M);
+    if (inf[l] == 0 && inf[L + l] == 0) m[q] = mn[q];
+    if (q % M == 0 && info) info[l] = inf[l] != 0 ? inf[l] : inf[L + l];
+  }
+}
+
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m, const double* grad_H, double lr,
                             const double* iH_in, int32_t* info, void* workspace, void* stream) {
   if (L < 1) return -1;
@@ -538,15 +556,14 @@ int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* gr
   }
   // iH' = iH + lr (gH + gH^T)
   natgrad_ih_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, iHc, grad_H, iHn);
-  // v = iH m ; gw = gH m (before m and H are overwritten: iHc is the old H's inverse, H itself is not read
-  // again); H = iH'^-1 in place; y = v - lr gm + 2 lr gw ; m = H y
+  // v = iH m ; gw = gH m; Hn = iH'^-1; y = v - lr gm + 2 lr gw ; mn = Hn y (into gw, dead after y); then the
+  // commit writes (mn, Hn) over (m, H) for the dims whose factorisations succeeded
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, iHc, M, MM, 0, m, 1, M, 0, 0.0, v, 1, M, 0, L, 1, st));
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, grad_H, M, MM, 0, m, 1, M, 0, 0.0, gw, 1, M, 0, L, 1, st));
-  LVAE_TRY(spd_inv_small_f64(M, L, iHn, MM, H, MM, ld, inf + L, st));
+  LVAE_TRY(spd_inv_small_f64(M, L, iHn, MM, Hn, MM, ld, inf + L, st));
   natgrad_y_kernel<<<blocks((int64_t)L * M), 256, 0, st>>>((int64_t)L * M, lr, v, grad_m, gw, y);
-  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, H, M, MM, 0, y, 1, M, 0, 0.0, m, 1, M, 0, L, 1, st));
-  (void)Hn;
-  if (info) (void)hipMemcpyAsync(info, inf, sizeof(int32_t) * L, hipMemcpyDeviceToDevice, st);
+  LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, Hn, M, MM, 0, y, 1, M, 0, 0.0, gw, 1, M, 0, L, 1, st));
+  natgrad_commit_kernel<<<blocks(L * MM + (int64_t)L * M), 256, 0, st>>>(L, M, inf, Hn, gw, H, m, info);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -45,7 +45,7 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
 int syrk_x3_splits(int np_, int L);
 int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
 int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
-                  int32_t* info, hipStream_t st);
+                  int32_t* info, hipStream_t st, float* lout = nullptr);
 int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const double* mu, const float* sv,
                  float* apart, _Float16* Bh, float* bsc, hipStream_t st);
 size_t ci_scratch_bytes(int np_, int L);
@@ -74,7 +74,8 @@ struct KLWorkspace {
   double *mu, *alpha, *res, *kdiag, *logdet, *part, *rpart;
   int* covflag;      // 1: integer covariates (the Gram kernels' fp32 covariate path; set by the factor)
   char* rb;          // the binned residual's plan / bin sums (kl_resid_bins.hip)
-  double* K64;       // [L, np, np] fp64 K of the dims whose diag K^-1 is refined (kl_refine.hip)
+  double* K64;       // [ceil(L / 2), np, np] fp64 K of the dims whose diag K^-1 is refined (kl_refine.hip), two
+                     // rounds: = the Y^T planes (dead between lauum and the backward's S) + np^2 floats for odd L
   double* rest;      // [L] the refinement gate's estimate (sum_r s_r + noise) max (K^-1)_ii
   int* rflag;        // [L] 1: diag K^-1 refined
   size_t bytes;
@@ -88,8 +89,10 @@ struct KLWorkspace {
     const size_t mat = (size_t)L * np_ * np_ * sizeof(float);
     A = (float*)take(mat);
     Bp = reinterpret_cast<_Float16*>(A);
-    planes = (_Float16*)take(mat);
     Kinv = (float*)take(mat);
+    planes = (_Float16*)take(mat);
+    K64 = reinterpret_cast<double*>(planes);
+    take(kl_refine_bytes(np_, L) - mat);  // (odd L: the second half of the last K64 slot, right after the planes)
     v = (float*)take((size_t)L * np_ * sizeof(float));
     sv = (float*)take((size_t)L * np_ * sizeof(float));
     bsc = (float*)take((size_t)L * sizeof(float));
@@ -105,7 +108,6 @@ struct KLWorkspace {
     covflag = (int*)take(sizeof(int));
     rb = take(kl_resid_bins_bytes(np_, L, LVAE_MAX_COMP));
     Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
-    K64 = (double*)take(kl_refine_bytes(np_, L));
     rest = (double*)take((size_t)L * sizeof(double));
     rflag = (int*)take((size_t)L * sizeof(int));
     bytes = off;

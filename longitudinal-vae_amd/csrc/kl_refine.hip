@@ -43,7 +43,22 @@ constexpr int kRfFillWG = 2048, kRgGemmWG = 512;  // grid sizes (the gemm: 2 res
 // est_l and flag_l; grid L, 256 threads.  max_i K_ii is bounded by sum_r s_r + noise_l (every factor is
 // <= 1 at zero distance and every gate passes or zeroes the component): exact for kernels without Bin
 // gates, conservative (a larger est) otherwise, and no kernel evaluations on the caller's stream
-__global__ __launch_bounds__(256) void kl_refine_gate_kernel(DevSpec s, const double* __restrict__ params,
+// A linear factor x_i[d] x_j[d] (the C5 extension) is not <= 1: its component's scale is multiplied by
+// max_i x_i[d]^2, the factor's largest diagonal value (taken here from the covariates, per LIN factor).
+__device__ inline double gate_block_max(double v, double* mred) {
+  const int tid = threadIdx.x;
+  __syncthreads();  // the previous reduction's readers are done
+  mred[tid] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) mred[tid] = fmax(mred[tid], mred[tid + o]);
+    __syncthreads();
+  }
+  return mred[0];
+}
+
+__global__ __launch_bounds__(256) void kl_refine_gate_kernel(DevSpec s, const double* __restrict__ x, int ldx,
+                                                             const double* __restrict__ params,
                                                              const double* __restrict__ noise,
                                                              const double* __restrict__ kdiag, int n, int np_,
                                                              int mode, double tau, double* __restrict__ est,
@@ -53,16 +68,24 @@ __global__ __launch_bounds__(256) void kl_refine_gate_kernel(DevSpec s, const do
   const double* d = kdiag + (int64_t)l * np_;
   double mx = 0.0;
   for (int i = tid; i < n; i += 256) mx = fmax(mx, d[i]);
-  mred[tid] = mx;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) mred[tid] = fmax(mred[tid], mred[tid + o]);
-    __syncthreads();
+  const double dmax = gate_block_max(mx, mred);
+  double ks = noise[l];
+  for (int r = 0; r < s.n_comp; ++r) {  // (uniform loops)
+    double sc = params[(int64_t)l * s.n_params + s.scale_idx[r]];
+    for (int f = 0; f < s.n_fac[r]; ++f) {
+      if (s.kind[r][f] != LVAE_LIN) continue;
+      const int dd = s.dim[r][f];
+      double m2 = 0.0;
+      for (int i = tid; i < n; i += 256) {
+        const double xv = x[(int64_t)i * ldx + dd];
+        m2 = fmax(m2, xv * xv);
+      }
+      sc *= gate_block_max(m2, mred);
+    }
+    ks += sc;
   }
   if (tid == 0) {
-    double ks = noise[l];
-    for (int r = 0; r < s.n_comp; ++r) ks += params[(int64_t)l * s.n_params + s.scale_idx[r]];
-    const double e = ks * mred[0];
+    const double e = ks * dmax;
     est[l] = e;
     flag[l] = mode == 1 ? 1 : (mode == 2 && e > tau ? 1 : 0);
   }
@@ -88,15 +111,16 @@ __global__ __launch_bounds__(256) void kl_refine_fill_kernel(DevSpec s, const do
                                                              int n, int np_, int L, int qs,
                                                              const double* __restrict__ params,
                                                              const double* __restrict__ noise,
-                                                             const int* __restrict__ flag, double* __restrict__ K) {
+                                                             const int* __restrict__ flag, double* __restrict__ K,
+                                                             int r0, int cap) {
   __shared__ int list[kRfMaxL];
   __shared__ double sx1[kRfT * kRfQ];
   __shared__ double sx2[kRfT * kRfQ];
   __shared__ double sp[64];
-  const int cnt = refine_list(flag, L, list);
+  const int cnt = min(max(refine_list(flag, L, list) - r0, 0), cap);  // this round's flagged dims
   const int tid = threadIdx.x, ntf = (n + kRfT - 1) / kRfT, per = ntf * ntf;
   for (int it = blockIdx.x; it < cnt * per; it += gridDim.x) {
-    const int l = list[it / per], t = it % per, i0 = (t / ntf) * kRfT, j0 = (t % ntf) * kRfT;
+    const int slot = it / per, l = list[r0 + slot], t = it % per, i0 = (t / ntf) * kRfT, j0 = (t % ntf) * kRfT;
     __syncthreads();  // the previous item's LDS readers are done
     if (tid < s.n_params) sp[tid] = params[(int64_t)l * s.n_params + tid];
     for (int e = tid; e < kRfT * qs; e += 256) {
@@ -107,7 +131,7 @@ __global__ __launch_bounds__(256) void kl_refine_fill_kernel(DevSpec s, const do
     __syncthreads();
     const int jj = tid & 63, j = j0 + jj;
     const double nz = noise[l];
-    double* o = K + (int64_t)l * np_ * np_;
+    double* o = K + (int64_t)slot * np_ * np_;
 #pragma unroll 4
     for (int k = 0; k < kRfT / 4; ++k) {
       const int ii = (tid >> 6) + 4 * k, i = i0 + ii;
@@ -129,20 +153,20 @@ __device__ inline double refine_x(const float* __restrict__ X, int np_, int k, i
 __global__ __launch_bounds__(256) void kl_refine_gemm_kernel(const double* __restrict__ K,
                                                              const float* __restrict__ Kinv, int n, int np_,
                                                              int L, const int* __restrict__ flag,
-                                                             double* __restrict__ part) {
+                                                             double* __restrict__ part, int r0, int cap) {
   __shared__ int list[kRfMaxL];
   __shared__ double As[kRgT * kRgAs];
   __shared__ double Bs[kRgK * kRgBs];
   __shared__ double red[kRgT];
-  const int cnt = refine_list(flag, L, list);
+  const int cnt = min(max(refine_list(flag, L, list) - r0, 0), cap);
   const int nt = np_ / kRgT, ntn = (n + kRgT - 1) / kRgT, per = ntn * ntn;
   for (int it = blockIdx.x; it < cnt * per; it += gridDim.x) {
-    const int l = list[it / per], t = it % per;
+    const int slot = it / per, l = list[r0 + slot], t = it % per;
     const int I = t / ntn, J = t % ntn;
     const int i0 = I * kRgT, j0 = J * kRgT;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = (w >> 1) * 64, wc = (w & 1) * 64, li = lane & 15, lk = lane >> 4;
-    const double* Kl = K + (int64_t)l * np_ * np_;
+    const double* Kl = K + (int64_t)slot * np_ * np_;
     const float* Xl = Kinv + (int64_t)l * np_ * np_;
     bi_f64x4 acc[4][4];
 #pragma unroll
@@ -263,7 +287,11 @@ static double refine_tau() {
   return v ? atof(v) : 16.0;
 }
 
-size_t kl_refine_bytes(int np_, int L) { return (size_t)L * np_ * np_ * sizeof(double); }
+// K64 holds kl_refine_cap(L) = ceil(L / 2) dims: the flagged dims go in (at most) two rounds through the caller's
+// buffer -- the KL workspace lends the factor's Y^T planes (L np^2 fp16 pairs, dead after lauum until the backward
+// writes S there) plus np^2 floats for odd L, instead of a dedicated L np^2 fp64 buffer
+int kl_refine_cap(int L) { return (L + 1) / 2; }
+size_t kl_refine_bytes(int np_, int L) { return (size_t)kl_refine_cap(L) * np_ * np_ * sizeof(double); }
 
 size_t kl_refine_part_bytes(int np_, int L) { return (size_t)L * (np_ / kRgT) * np_ * sizeof(double); }
 
@@ -283,12 +311,17 @@ int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n
     for (int f = 0; f < spec->n_fac[r]; ++f) qs = spec->dim[r][f] + 1 > qs ? spec->dim[r][f] + 1 : qs;
   if (!bucket || qs > kRfQ || qs > ldx || np_ % kRgT || L > kRfMaxL) return -1;
   const DevSpec ds = to_dev(spec);
-  kl_refine_gate_kernel<<<L, 256, 0, st>>>(ds, params, noise, kdiag, n, np_, mode, refine_tau(), est, flag);
-  if (bucket == 1)
-    kl_refine_fill_kernel<8, 2><<<kRfFillWG, 256, 0, st>>>(ds, x, ldx, n, np_, L, qs, params, noise, flag, K64);
-  else
-    kl_refine_fill_kernel<16, 4><<<kRfFillWG, 256, 0, st>>>(ds, x, ldx, n, np_, L, qs, params, noise, flag, K64);
-  kl_refine_gemm_kernel<<<kRgGemmWG, 256, 0, st>>>(K64, Kinv, n, np_, L, flag, part);
+  kl_refine_gate_kernel<<<L, 256, 0, st>>>(ds, x, ldx, params, noise, kdiag, n, np_, mode, refine_tau(), est, flag);
+  const int cap = kl_refine_cap(L);
+  for (int r0 = 0; r0 < L; r0 += cap) {  // (rounds with no flagged dims: launches that read the flags and exit)
+    if (bucket == 1)
+      kl_refine_fill_kernel<8, 2><<<kRfFillWG, 256, 0, st>>>(ds, x, ldx, n, np_, L, qs, params, noise, flag, K64,
+                                                             r0, cap);
+    else
+      kl_refine_fill_kernel<16, 4><<<kRfFillWG, 256, 0, st>>>(ds, x, ldx, n, np_, L, qs, params, noise, flag, K64,
+                                                              r0, cap);
+    kl_refine_gemm_kernel<<<kRgGemmWG, 256, 0, st>>>(K64, Kinv, n, np_, L, flag, part, r0, cap);
+  }
   kl_refine_diag_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(part, n, np_, flag, kdiag);
   LVAE_CHECK_LAUNCH();
   return 0;

@@ -130,6 +130,14 @@ SIGNATURES = {
     "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_spd_inv_chol_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_inv_chol_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "lvae_potrf_f64": (_I32, [_I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP]),
+    "lvae_potrf_f32_workspace_size": (_SZ, [_I32, _I32]),
+    "lvae_potrf_f32": (_I32, [_I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _VP]),
+    "lvae_trsm_workspace_size": (_SZ, [_I32, _I32]),
+    "lvae_trsm_f64": (_I32, [_I32, _I32, _I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP]),
+    "lvae_trsm_f32": (_I32, [_I32, _I32, _I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP]),
+    "lvae_potrs_f64": (_I32, [_I32, _I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP]),
+    "lvae_potrs_f32": (_I32, [_I32, _I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP]),
     "lvae_predict_workspace_size": (_SZ, [_I32, _I32, _I32, _I32, _I32]),
     "lvae_predict_f64": (_I32, [_SPEC, _SPEC, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _I32, _VP, _VP,
                                 _VP, _VP, _D, _VP, _VP, _VP, _VP]),

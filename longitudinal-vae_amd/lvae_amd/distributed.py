@@ -164,7 +164,7 @@ class LatentShardedClosedStep:
         return self._step_plain(img, mask, X, eps)
 
     def _step_overlapped(self, img, mask, X, eps):
-        from .elbo import KL_closed_batched, KLFactor, _noise_vector
+        from .elbo import KLFactor, _noise_vector
         from .kernels import kernel_spec_and_params
         W, r = self.world, self.rank
         self.opt.zero_grad(set_to_none=True)
@@ -174,6 +174,9 @@ class LatentShardedClosedStep:
         vst.wait_stream(main)  # the previous step's updates
         L = self.vae.latent_dim
         N = X.shape[0]
+        n_loc = img.shape[0]
+        if n_loc * W != N:  # (checked before the factor's enqueue is handed to its worker thread)
+            raise ValueError(f"rank rows {n_loc} x world {W} != N = {N} (equal image shards required)")
         d0, d1 = shard_bounds(L, W, r)
         own = d1 > d0
         factor = None
@@ -181,13 +184,20 @@ class LatentShardedClosedStep:
             spec, params = kernel_spec_and_params(self.kernel)
             noise = _noise_vector(self.lik, L).to(params.device)
             factor = KLFactor(spec, params[d0:d1], noise[d0:d1], X, main)
+        try:
+            return self._step_overlapped_rest(img, mask, X, eps, main, vst, capturing, L, N, n_loc, d0, d1, own,
+                                              factor)
+        finally:
+            if factor is not None:
+                factor.wait_enqueued()  # (a no-op once waited: never leave the worker enqueueing into freed buffers)
+
+    def _step_overlapped_rest(self, img, mask, X, eps, main, vst, capturing, L, N, n_loc, d0, d1, own, factor):
+        from .elbo import KL_closed_batched
+        r = self.rank
         gathered = torch.cuda.Event()
         with torch.cuda.stream(vst):
             gv = None if capturing else self.gvae
             mu, log_var = gv.encode(img, mask) if gv is not None else self.vae.encode(img)
-            n_loc = mu.shape[0]
-            if n_loc * W != N:
-                raise ValueError(f"rank rows {n_loc} x world {W} != N = {N} (equal image shards required)")
             z = self.vae.sample_latent(mu, log_var, eps)
             full = self._all_gather(torch.cat([mu.detach(), log_var.detach()], 1).contiguous(), N)
             gathered.record(vst)

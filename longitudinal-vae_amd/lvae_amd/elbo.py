@@ -540,7 +540,12 @@ def natural_gradient_update_(m, H, grad_m, grad_H, natural_gradient_lr):
                                          float(natural_gradient_lr), _lib.ptr(iH), _lib.ptr(info), _lib.ptr(ws),
                                          _lib.stream_ptr())
     _lib.check(rc, "natgrad_update")
-    _check_info(info, "natural-gradient update cholesky")
+    # the raw-pointer write is invisible to autograd's version counters: bump them, so that saved-tensor checks
+    # and the iH cache (keyed on H._version) see the new (m, H)
+    from torch.autograd.graph import increment_version
+    increment_version(m)
+    increment_version(H)
+    _check_info(info, "natural-gradient update cholesky")  # (a failed dim kept its m, H: natgrad_commit_kernel)
     return True
 
 

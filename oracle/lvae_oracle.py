@@ -140,6 +140,18 @@ def gram(spec, params, x1, x2):
 # Regime B: exact KL (elbo_functions.py:8-34)
 #   KL = 1/2 ( tr(K^-1 V) + mu^T K^-1 mu - N + log|K| - sum log v ),  K = Gram + noise I
 # ------------------------------------------------------------------------------------------
+def potrf(A):
+    """LK1 = torch.cholesky(K1) (elbo_functions.py:26): LAPACK potrf in fp64 (batched over leading dims);
+    returns (L, log|A| = 2 sum log diag L (elbo_functions.py:29))."""
+    L = torch.linalg.cholesky(A)
+    return L, 2 * torch.log(torch.diagonal(L, dim1=-2, dim2=-1)).sum(-1)
+
+
+def potrs(B, L):
+    """torch.cholesky_solve(B, LK1) (elbo_functions.py:27-28): A^-1 B from the factor."""
+    return torch.cholesky_solve(B, L)
+
+
 def kl_closed(spec, params, x, noise, mu, logv):
     """Device-agnostic: on CPU tensors it is the CPU oracle; the large-N parity tests also evaluate
     this same fp64 formula with the tensors on the GPU (PyTorch's fp64 Cholesky) as the checker."""

@@ -185,7 +185,8 @@ def test_closed_step_backward_order_agrees(hip):
     the two loss terms as separate roots, the KL backward split into its (mu, logvar) and hyper-parameter
     nodes) against one plain backward from the summed loss on the same models and data: every parameter
     after two Adam steps within 1e-5 (the same fp32 terms summed on different streams; Adam's normalised
-    steps carry that rounding into the parameters at ~1e-6)."""
+    steps carry that rounding into the parameters at ~1e-6: observed 1.53e-6 on one r4 box, hence 1e-5
+    rather than 1e-6; a self-consistency check, the oracle tests pin the values)."""
     import lvae_amd as la
     from lvae_amd.data import health_mnist_batch
     from lvae_amd.steps import ClosedStep
@@ -221,3 +222,68 @@ def test_closed_step_backward_order_agrees(hip):
     for (n, p), (_, q) in zip(list(vae_s.named_parameters()) + list(k_s.named_parameters()),
                               list(vae_r.named_parameters()) + list(k_r.named_parameters())):
         assert rel(p, q) < 1e-5, n
+
+
+def _overlap_worker(rank, world, port, L, q):
+    """One rank of a gloo process group over CUDA tensors on the one GPU: LatentShardedClosedStep's
+    overlapped path (_step_overlapped: factor first, ConvVAE stream, split backward) against its plain
+    path (_step_plain) on identical fresh models and this rank's rows."""
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lvae_amd as la
+        from lvae_amd.data import health_mnist_batch
+        from lvae_amd.distributed import LatentShardedClosedStep, shard_bounds
+        from lvae_amd.vae import ConvVAE
+        P, T = 32, 16
+        N = P * T
+        img, mask, X = health_mnist_batch(P, T, seed=29, device=DEV)
+        eps = torch.randn(N, L, generator=torch.Generator().manual_seed(3)).to(DEV)
+        lo, hi = shard_bounds(N, world, rank)
+        out = {}
+        for mode in ("overlapped", "plain"):
+            torch.manual_seed(17)
+            vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+            k = la.generate_kernel(**CFG, latent_dim=L)
+            set_raw(k, _random_hypers(k, L, np.random.default_rng(29)))
+            k = k.to(DEV)
+            lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
+            opt = torch.optim.SGD(list(vae.parameters()) + list(k.parameters()), lr=0.0)
+            step = LatentShardedClosedStep(vae, k, lik, opt, weight=0.15, loss_function="mse")
+            fn = step._step_overlapped if mode == "overlapped" else step._step_plain
+            net, rl, _, gp = fn(img[lo:hi], mask[lo:hi], X, eps[lo:hi])
+            torch.cuda.synchronize()
+            out[mode] = ([float(net), float(rl), float(gp)],
+                         [p.grad.detach().cpu().double().clone() for p in list(k.parameters()) + list(vae.parameters())])
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("L", [4, 1])  # L = 1: world 2 > L, rank 1 owns no latent dim
+def test_gloo_world2_cuda_overlapped_matches_plain(hip, L):
+    """The sharded exact-KL step's overlapped GPU path at world 2 (gloo over CUDA tensors, both ranks on the
+    one GPU) equals its plain path on every rank: loss terms and every gradient within 1e-5 of their max
+    (fp32 ConvVAE sums in other stream orders), including a rank that owns no latent dim."""
+    import multiprocessing as mp
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, L, qq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(qq.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(world):
+        (to, go), (tp, gp) = res[rank]["overlapped"], res[rank]["plain"]
+        assert np.allclose(to, tp, rtol=1e-5), (rank, to, tp)
+        for a, b in zip(go, gp):
+            assert rel(a, b) < 1e-5, rank
+    # the replicas agree across ranks (the flat SUM all-reduce)
+    for a, b in zip(res[0]["overlapped"][1], res[1]["overlapped"][1]):
+        assert torch.equal(a, b)

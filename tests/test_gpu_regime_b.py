@@ -68,7 +68,7 @@ def test_kl_closed_single_dim_api(hip):
     assert abs(kl.item() - g["kl"][0]) < 1e-4 * abs(g["kl"][0])
 
 
-@pytest.mark.parametrize("P,L", [(64, 2), (13, 3), (9, 1)])  # N = 1024, 208 (padded), 144 (padded)
+@pytest.mark.parametrize("P,L", [(64, 2), (64, 8), (13, 3), (9, 1)])  # N = 1024 (64-8: C2), 208 / 144 (padded)
 def test_kl_closed_vs_oracle(hip, P, L):
     import lvae_amd as la
     from lvae_amd.data import health_mnist_covariates
@@ -176,6 +176,11 @@ def test_gram_batched_semantics(hip):
     assert rel(got, raw.grad) < 1e-12
 
 
+# the retired block sweep (spd_sweep.hip, rounds 1-2) is an opt-in extra: LVAE_TEST_SWEEP=1 adds it back
+import os as _os  # noqa: E402
+INV_KINDS = ["chol", "sweep"] if _os.environ.get("LVAE_TEST_SWEEP") == "1" else ["chol"]
+
+
 def _spd_inverse(hip, kind, n, L, Ad):
     """A^-1 (both triangles), log|A|, info of the [L, n, n] fp32 lower triangles Ad through the C ABI:
     kind 'chol' (blocked Cholesky + trtri + lauum, chol_inv.hip, the KL's inverse) or 'sweep'."""
@@ -192,7 +197,7 @@ def _spd_inverse(hip, kind, n, L, Ad):
     return Ai, logdet, info
 
 
-@pytest.mark.parametrize("kind", ["chol", "sweep"])
+@pytest.mark.parametrize("kind", INV_KINDS)
 @pytest.mark.parametrize("n,L", [(256, 3), (512, 2), (768, 2), (1280, 2), (4096, 1), (256, 9), (512, 9), (768, 10),
                                  (1280, 9)])
 def test_spd_inverse(hip, kind, n, L):
@@ -218,7 +223,7 @@ def test_spd_inverse(hip, kind, n, L):
     assert rel(logdet.cpu(), torch.logdet(A)) < 1e-6
 
 
-@pytest.mark.parametrize("kind", ["chol", "sweep"])
+@pytest.mark.parametrize("kind", INV_KINDS)
 def test_spd_inverse_not_pd(hip, kind):
     """A non-SPD pivot is reported LAPACK-style with the global column (block 1, local column 10)."""
     n, L = 512, 2
@@ -246,7 +251,7 @@ def test_spd_inverse_ill_conditioned(hip):
         K = torch.stack([O.gram(spec, O.constrain(torch.tensor(raw[l])), X, X) for l in range(L)])
         K = K + noise * torch.eye(P * T, dtype=torch.float64)
         res = {}
-        for kind in ("chol", "sweep"):
+        for kind in INV_KINDS:
             Ai, logdet, info = _spd_inverse(hip, kind, P * T, L, K.float().to(DEV).contiguous())
             assert int(info.abs().sum()) == 0
             Xi = Ai.cpu().double()
@@ -257,7 +262,8 @@ def test_spd_inverse_ill_conditioned(hip):
         conds = [float(torch.linalg.cond(K[l])) for l in range(L)]
         for l in range(L):
             assert res["chol"][l] < max(1e-3, 2 * conds[l] * 2.0 ** -22), (noise, l, conds[l])
-            assert res["chol"][l] < 0.2 * res["sweep"][l] or res["sweep"][l] < 1e-2
+            if "sweep" in res:
+                assert res["chol"][l] < 0.2 * res["sweep"][l] or res["sweep"][l] < 1e-2
 
 
 def test_kl_closed_vs_oracle_full_size(hip):
