@@ -1203,6 +1203,214 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
     part[((int64_t)l * kBwdSlots + sl) * G + g0] = wred[0][sl] + wred[1][sl] + wred[2][sl] + wred[3][sl];
 }
 
+// ------------------------------------------------------------------------------------------
+// The table path's adjoint as a HISTOGRAM (r5): every raw adjoint sum is  sum_ij g_ij D_p[bits_ij][d_ij,g]
+// with D_p a function of (the pair's gate bits, its distance in the dim of p's group) only, so
+//     raw_p = sum_{b, d} H_g[b][d] D_p[b][d],      H_g[b][d] = sum of g_ij over the pairs in bin (b, d) of group g
+// -- per element ONE histogram add per group instead of one table read + FMA per parameter.  The bins are
+// int64 fixed point (LDS atomics, ds_add_u64): g_ij is converted to q = round(g 2^(SHIFT - E)) straight from
+// its float bits, with E a per-dim bound on |g| (2^E > 2 (max diag K^-1 + max v max diag K^-1 tr K^-1 +
+// max alpha^2): |K^-1_ij|, |S_ij| <= their diagonals' max, S_ii <= max v (K^-2)_ii <= max v tr K^-1 (K^-1)_ii)
+// and SHIFT = 62 - the bits a bin's count can take over the workgroup's tiles: integer adds are exact and
+// associative, so the sums are DETERMINISTIC (no order dependence) and every element keeps 2^-SHIFT of the
+// bound (~2^-44).  After the tiles: raw_p = 2^(E - SHIFT) sum_bins (double) H D_p in a fixed order, into the
+// same per-workgroup slots kl_gram_bwd_reduce reads.  The diagonal's sum (d/d noise) stays an fp32 / fp64 sum.
+// ------------------------------------------------------------------------------------------
+__device__ inline long long fx_q(float g, int sbias) {
+  const unsigned u = __float_as_uint(g);
+  const int e = (int)((u >> 23) & 0xffu);
+  const long long m = (long long)((u & 0x7fffffu) | 0x800000u);
+  const int sh = e + sbias;
+  long long q;
+  if (sh >= 0) {
+    q = m << (sh < 39 ? sh : 39);  // (sh <= SHIFT - 24 <= 38 when |g| < 2^E: the clamp never binds)
+  } else {
+    const int r = -sh;
+    q = r < 25 ? ((m + (1ll << (r - 1))) >> r) : 0ll;  // round to nearest (ties up); below 2^-25 of the grid: 0
+  }
+  q = e == 0 ? 0ll : q;  // zero / subnormal (|g| < 2^-126: below any grid)
+  return (u >> 31) ? -q : q;
+}
+
+#ifndef LVAE_HIST_WPE
+#define LVAE_HIST_WPE 2  // the histogram adjoint's waves per SIMD (register cap)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_HIST_WPE))) void kl_gram_bwd_hist_kernel(
+    GramTab tb, const double* __restrict__ x, int ldx, int n, int np_, int qs, const double* __restrict__ params,
+    const float* __restrict__ Kinv, const float* __restrict__ S, const float* __restrict__ Sx, int nsplit,
+    const double* __restrict__ alpha, const double* __restrict__ kdiag, const float* __restrict__ vv, int shift,
+    double* __restrict__ part, int ntiles, const int* __restrict__ covflag) {
+  if (*covflag != 2) return;  // (uniform, before any barrier)
+  __shared__ float sx1[2][kGT * kMaxQB];  // (two buffers: this tile's and the next one's)
+  __shared__ float sx2[2][kGT * kMaxQB];
+  __shared__ float sp[64];
+  __shared__ float sa1[2][kGT], sa2[2][kGT];
+  __shared__ double wred[4][kBwdSlots];
+  __shared__ double bred[4][4];
+  extern __shared__ double hdyn[];  // [ng 2^B kTabR] int64 bins, then the fp32 derivative tables
+  const int G = gridDim.x, g0 = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+  const int lane = tid & 63, wv = tid >> 6, np_s = tb.n_params;
+  const int tstride = (1 << tb.nbits) * kTabR, nbins = tb.ng * tstride;
+  unsigned long long* H = reinterpret_cast<unsigned long long*>(hdyn);
+  float* tab = reinterpret_cast<float*>(hdyn + nbins);
+  if (tid < np_s) sp[tid] = float(params[(int64_t)l * np_s + tid]);
+  for (int e = tid; e < 4 * kBwdSlots; e += 256) (&wred[0][0])[e] = 0.0;
+  for (int e = tid; e < nbins; e += 256) H[e] = 0ull;
+  // the bound on |g| of this dim (every workgroup of the dim computes the same value: no extra launch)
+  int sbias;
+  {
+    const double* kd = kdiag + (int64_t)l * np_;
+    const float* vl = vv + (int64_t)l * np_;
+    const double* al = alpha + (int64_t)l * np_;
+    double kmx = 0.0, ksum = 0.0, vmx = 0.0, amx = 0.0;
+    for (int i = tid; i < n; i += 256) {
+      const double k = kd[i], a = al[i];
+      kmx = fmax(kmx, fabs(k));
+      ksum += fabs(k);
+      vmx = fmax(vmx, (double)vl[i]);
+      amx = fmax(amx, a * a);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      kmx = fmax(kmx, __shfl_xor(kmx, o, 64));
+      ksum += __shfl_xor(ksum, o, 64);
+      vmx = fmax(vmx, __shfl_xor(vmx, o, 64));
+      amx = fmax(amx, __shfl_xor(amx, o, 64));
+    }
+    if (lane == 0) {
+      bred[wv][0] = kmx;
+      bred[wv][1] = ksum;
+      bred[wv][2] = vmx;
+      bred[wv][3] = amx;
+    }
+    __syncthreads();
+    kmx = fmax(fmax(bred[0][0], bred[1][0]), fmax(bred[2][0], bred[3][0]));
+    ksum = (bred[0][1] + bred[1][1]) + (bred[2][1] + bred[3][1]);
+    vmx = fmax(fmax(bred[0][2], bred[1][2]), fmax(bred[2][2], bred[3][2]));
+    amx = fmax(fmax(bred[0][3], bred[1][3]), fmax(bred[2][3], bred[3][3]));
+    const double gb = 2.0 * (kmx + vmx * kmx * ksum + amx);
+    int E = 0;
+    if (gb > 0.0 && gb < 1e300) (void)frexp(gb, &E);  // gb < 2^E
+    sbias = shift - E - 150;
+  }
+  tab_build_bwd(tb, sp, tab);
+  const float* ki = Kinv + (int64_t)l * np_ * np_;
+  const float* si = S + (int64_t)l * np_ * np_;
+  const double* al = alpha + (int64_t)l * np_;
+  auto load_ks = [&](int i0, int j0, g_f32x4 (&kv4)[4], g_f32x4 (&sv4)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int64_t o = (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc;
+      kv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(ki + o));
+      sv4[a] = __builtin_nontemporal_load(reinterpret_cast<const g_f32x4*>(si + o));
+    }
+    for (int q = 1; q < nsplit; ++q) {  // K-split partials of S (syrk_x3_splits)
+      const float* sq = Sx + (int64_t)(q - 1) * gridDim.y * np_ * np_ + (int64_t)l * np_ * np_;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        sv4[a] += __builtin_nontemporal_load(
+            reinterpret_cast<const g_f32x4*>(sq + (int64_t)(i0 + 4 * tr + a) * np_ + j0 + 4 * tc));
+    }
+  };
+  float dd = 0.f;
+  double dsum = 0.0;
+  int since_flush = 0;
+  int t = g0, I = 0, J = 0, In = 0, Jn = 0;
+  g_f32x4 kv4[4], sv4[4];
+  CovPrefetchF pf;
+  double an = 0.0;
+  // software pipeline as kl_gram_bwd_tab_kernel: K^-1 / S one tile ahead in registers, the covariates and
+  // alpha entries two tiles ahead (the other LDS buffer), one barrier per tile
+  if (t < ntiles) {
+    tri_index(t, I, J);
+    load_ks(I * kGT, J * kGT, kv4, sv4);
+    pf.load(x, ldx, n, qs, I * kGT, J * kGT);
+    if (tid < 2 * kGT) an = al[(tid < kGT ? I : J) * kGT + (tid & (kGT - 1))];
+    pf.store(qs, sx1[0], sx2[0]);
+    if (tid < kGT) sa1[0][tid] = float(an);
+    else if (tid < 2 * kGT) sa2[0][tid - kGT] = float(an);
+    if (t + G < ntiles) {
+      tri_index(t + G, In, Jn);
+      pf.load(x, ldx, n, qs, In * kGT, Jn * kGT);
+      if (tid < 2 * kGT) an = al[(tid < kGT ? In : Jn) * kGT + (tid & (kGT - 1))];
+    }
+  }
+  __syncthreads();  // the bins, the tables and the first tile's LDS
+  for (int b = 0; t < ntiles; t += G, b ^= 1) {
+    const int i0 = I * kGT, j0 = J * kGT;
+    const bool more = t + G < ntiles;
+    const float* __restrict__ cx1 = sx1[b];
+    const float* __restrict__ cx2 = sx2[b];
+    long long q[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int i = i0 + 4 * tr + a;
+      const g_f32x4 kv = kv4[a], sv = sv4[a];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = j0 + 4 * tc + c;
+        const float gv = 0.5f * (kv[c] - sv[c] - sa1[b][4 * tr + a] * sa2[b][4 * tc + c]);
+        const bool in = i < n && j < n && j <= i;
+        if (in && i == j) dd += gv;
+        q[a][c] = fx_q(in ? ((i == j) ? gv : 2.f * gv) : 0.f, sbias);
+      }
+    }
+    if (more) load_ks(In * kGT, Jn * kGT, kv4, sv4);  // (in flight under this tile's bins)
+    int bits[4][4];
+    tab_bits(tb, cx1, cx2, tr, tc, bits);
+#pragma unroll 1
+    for (int gi = 0; gi < tb.ng; ++gi) {
+      int idx[4][4];
+      tab_index(tb, gi, cx1, cx2, tr, tc, bits, idx);
+      unsigned long long* hg = H + gi * tstride;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (q[a][c] != 0) atomicAdd(hg + idx[a][c], (unsigned long long)q[a][c]);
+    }
+    if (++since_flush == 8 || t + G >= ntiles) {  // the diagonal's fp32 sums into fp64
+      since_flush = 0;
+      dsum += (double)dd;
+      dd = 0.f;
+    }
+    if (more) {
+      pf.store(qs, sx1[b ^ 1], sx2[b ^ 1]);
+      if (tid < kGT) sa1[b ^ 1][tid] = float(an);
+      else if (tid < 2 * kGT) sa2[b ^ 1][tid - kGT] = float(an);
+      int I2 = 0, J2 = 0;
+      if (t + 2 * G < ntiles) {
+        tri_index(t + 2 * G, I2, J2);
+        pf.load(x, ldx, n, qs, I2 * kGT, J2 * kGT);
+        if (tid < 2 * kGT) an = al[(tid < kGT ? I2 : J2) * kGT + (tid & (kGT - 1))];
+      }
+      __syncthreads();  // buffer b ^ 1 written; every reader of buffer b done
+      I = In, J = Jn, In = I2, Jn = J2;
+    }
+  }
+  __syncthreads();  // every bin add done
+  // raw_p = 2^(E - SHIFT) sum_bins H D_p: thread t takes bins t, t + 256, ... of p's group, then the waves'
+  // sums in a fixed order
+  const double unscale = ldexp(1.0, -(sbias + 150));  // 2^(E - SHIFT)
+  for (int gi = 0; gi < tb.ng; ++gi) {
+    const long long* hg = reinterpret_cast<const long long*>(H + gi * tstride);
+    for (int k = tb.pbeg[gi]; k < tb.pbeg[gi + 1]; ++k) {
+      const float* tk = tab + k * tstride;
+      double acc = 0.0;
+      for (int e = tid; e < tstride; e += 256) acc += (double)hg[e] * (double)tk[e];
+      acc = wave_sum(acc);
+      if (lane == 0) wred[wv][tb.porder[k]] = acc * unscale;
+    }
+  }
+  {
+    const double w = wave_sum(dsum);
+    if (lane == 0) wred[wv][kNoiseSlot] = w;
+  }
+  __syncthreads();
+  for (int sl = tid; sl < kBwdSlots; sl += 256)
+    part[((int64_t)l * kBwdSlots + sl) * G + g0] = ((wred[0][sl] + wred[1][sl]) + wred[2][sl]) + wred[3][sl];
+}
+
 // fp64 residual of the exact-KL solve, r = mu - K alpha0 (K = Gram + noise I, alpha0 = K^-1 mu from the
 // fp32 inverse), the matrix never materialised: every lower 64-tile's kernel values are evaluated in
 // fp64 (fp64 exp / sin, covariate tests and differences exact, as the reference's double arithmetic)
@@ -1593,8 +1801,8 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L) {
 
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
-                const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
-                const int* covflag, hipStream_t st) {
+                const double* alpha, const double* kdiag, const float* v, const double* gkl, double* part,
+                double* dparams, double* dnoise, const int* covflag, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
   if (!bucket || qs > kMaxQB || spec->n_params > 64) return -1;
@@ -1614,9 +1822,19 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
   const size_t dyn = (size_t)(spec->n_params + 1) * 256 * sizeof(float);
   GramTab tb;
   if (gram_tab_build(spec, tb) && !getenv_off("LVAE_GRAM_TAB")) {  // (the same decision as kl_gram_fill's)
-    const size_t tdyn = dyn + (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
-    kl_gram_bwd_tab_kernel<<<dim3(G, L), 256, tdyn, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
-                                                          alpha, part, ntiles, covflag);
+    const size_t tabb = (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
+    if (!getenv_off("LVAE_GRAM_HIST")) {
+      // the histogram adjoint: SHIFT = 62 - (bits of a bin's largest possible count, + 1)
+      const int per = (ntiles + G - 1) / G;
+      int hb = 1;
+      while ((1ll << hb) < (long long)per * kGT * kGT) ++hb;
+      const size_t hdyn = (size_t)tb.ng * (1 << tb.nbits) * kTabR * sizeof(double) + tabb;
+      kl_gram_bwd_hist_kernel<<<dim3(G, L), 256, hdyn, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
+                                                             alpha, kdiag, v, 62 - (hb + 1), part, ntiles, covflag);
+    } else {
+      kl_gram_bwd_tab_kernel<<<dim3(G, L), 256, dyn + tabb, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx,
+                                                                  nsplit, alpha, part, ntiles, covflag);
+    }
   }
   if (bucket == 1) {
     kl_gram_bwd_tiles<8, 2, float><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,

@@ -40,8 +40,8 @@ int kl_gram_fill(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
 size_t kl_gram_bwd_partials_bytes(int np_, int L);
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
-                const double* alpha, const double* gkl, double* part, double* dparams, double* dnoise,
-                const int* covflag, hipStream_t st);
+                const double* alpha, const double* kdiag, const float* v, const double* gkl, double* part,
+                double* dparams, double* dnoise, const int* covflag, hipStream_t st);
 int syrk_x3_splits(int np_, int L);
 int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
 int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
@@ -411,7 +411,7 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);
     LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, S, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
-                         gkl, ws.part, dparams, dnoise, ws.covflag, st));
+                         ws.kdiag, ws.v, gkl, ws.part, dparams, dnoise, ws.covflag, st));
   }
   LVAE_CHECK_LAUNCH();
   return 0;
