@@ -163,6 +163,13 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
  * refined) to device buffers, on `stream`.  No reference counterpart (diagnostic).                  */
 int lvae_kl_closed_refine_state(int n, int L, const void* workspace, double* est, int32_t* flag, void* stream);
 
+/* The backward's hyper-parameter half takes one of two routes, decided on the device from the covariates by the
+ * factor (kl_hyper.hip): the S = K^-1 V K^-1 GEMM + the Gram adjoint, or -- for the table family of kernels on
+ * integer-coded covariates with the "big" (id) covariate in contiguous runs -- the binned route (bin sums of
+ * K^-1 and the id runs' blocks, no S; env LVAE_KL_HYPER=0 forces the GEMM route).  This copies the last
+ * factor's choice (int32: 1 = binned) to a device buffer, on `stream`.  No reference counterpart (diagnostic). */
+int lvae_kl_closed_hyper_state(int n, int L, const void* workspace, int32_t* on, void* stream);
+
 /* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
  * 256-wide pivot blocks (the r1-r2 Regime B inverse; lvae_kl_closed_* now use lvae_spd_inv_chol_f32's
  * blocked Cholesky, which is ~100x more accurate at cond 1e5; kept as a C-ABI entry): per pivot block k,

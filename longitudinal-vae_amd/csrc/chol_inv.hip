@@ -924,6 +924,8 @@ struct CiGemmArgs {
   _Float16 *bh_out, *bl_out;
   float* bsc;
   int pre = 0;  // kCiLauum(KL): K^-1's lower tiles are in Kinv already (pipelined lauum): epilogue only
+  const int* hbon = nullptr;  // kCiLauumKL: *hbon != 0 -> the binned hyper-gradient (kl_hyper.hip) runs: the full
+                              // symmetric K^-1 (the mirror) instead of the S GEMM's B planes
 };
 
 // one halving butterfly step over lane bit D (D <= 16): the lane keeps the half of its N partial sums
@@ -1331,16 +1333,20 @@ __device__ inline void ci_gemm_body(const CiGemmArgs& g, const CiScratch& S, con
       ci_kl_partials(acc, 1.f, g, l, i, j, kl_mu, kl_part);
       const int64_t tb = l * np2 + (int64_t)i * kSwB * np_ + (int64_t)j * kSwB;   // B tile (i, j)
       const int64_t tbt = l * np2 + (int64_t)j * kSwB * np_ + (int64_t)i * kSwB;  // B tile (j, i)
-      const float sb = g.bh_out ? g.bsc[l] : 0.f;  // the dim's split scale of B (ci_bscale_kernel)
-      if (g.bh_out && kCiBC16) {
+      // (uniform) the binned hyper-gradient's plan is on: the mirror of K^-1, no B planes
+      const bool hbm = g.bh_out && g.hbon && *g.hbon;
+      _Float16* const bho = hbm ? nullptr : g.bh_out;
+      _Float16* const blo = hbm ? nullptr : g.bl_out;
+      const float sb = bho ? g.bsc[l] : 0.f;  // the dim's split scale of B (ci_bscale_kernel)
+      if (bho && kCiBC16) {
         // B(i, j) = T diag(sqrt v_j), column-scaled, straight from the registers into the chunk-major
         // planes (x3_c16.hpp): tile (i, j) is the 128 KB run of chunks 16 j .. 16 j + 15 of row block i
         const int64_t tc = c16_off(l, np_, i * kSwB, j * kSwB);
-        c16_tile_planes_out(acc, [&](int b) { return sb * kl_sv[kSwB + sx_col(b)]; }, g.bh_out + tc, g.bl_out + tc);
-      } else if (g.bh_out) {
+        c16_tile_planes_out(acc, [&](int b) { return sb * kl_sv[kSwB + sx_col(b)]; }, bho + tc, blo + tc);
+      } else if (bho) {
         // B(i, j) = T diag(sqrt v_j): column-scaled, straight from the registers
-        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(g.bh_out + tb, (short)0, 0x7fffffff, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(g.bl_out + tb, (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(bho + tb, (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(blo + tb, (short)0, 0x7fffffff, 0x00020000);
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const int vb = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 2;
 #pragma unroll
@@ -1361,14 +1367,14 @@ __device__ inline void ci_gemm_body(const CiGemmArgs& g, const CiScratch& S, con
       }
       // (no mirror of K^-1 here: the exact KL's readers -- kl_alpha_sym_kernel, the Gram adjoint, the
       // diagonal -- read its lower tiles only; the B planes need both halves)
-      if (i != j && (g.bh_out || LVAE_KL_MIRROR))
+      if (i != j && (bho || hbm || LVAE_KL_MIRROR))
         ci_transposed_out(acc, 1.f, lds, [&](int c, int r0, f32x4 v) {
-          if (LVAE_KL_MIRROR) *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
-          if (g.bh_out) {
+          if (hbm || LVAE_KL_MIRROR) *reinterpret_cast<f32x4*>(Ot + (int64_t)c * np_ + r0) = v;
+          if (bho) {
             const f32x4 s4 = *reinterpret_cast<const f32x4*>(&kl_sv[r0]);
             // B(j, i) row c, columns r0 .. r0 + 3 (one 4-half run of a chunk either way)
             const int64_t o = kCiBC16 ? c16_off(l, np_, j * kSwB + c, i * kSwB + r0) : tbt + (int64_t)c * np_ + r0;
-            ci_split4(v * s4, sb, g.bh_out + o, g.bl_out + o);
+            ci_split4(v * s4, sb, bho + o, blo + o);
           }
         });
     } else if (i != j) {
@@ -1615,7 +1621,7 @@ __global__ __launch_bounds__(64) void ci_bscale_kernel(CiScratch S, const float*
 // lauum, K^-1 = Y^T Y from ci_factor_f32's Y^T planes.  With mu (the exact KL's reduce): also the
 // partials of K^-1 mu (apart) and, if Bh, the planes of B = K^-1 diag(sqrt v) with their scale bsc[L].
 int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const double* mu, const float* sv,
-                 float* apart, _Float16* Bh, float* bsc, hipStream_t st) {
+                 float* apart, _Float16* Bh, float* bsc, hipStream_t st, const int* hbon) {
   if (np_ <= 0 || np_ % kSwB || np_ / kSwB > 64) return -1;
   CiScratch S((char*)scratch, np_, L);
   const int nt = S.nt, per = nt * (nt + 1) / 2, nwg = per * L;
@@ -1630,6 +1636,7 @@ int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv,
     gl.bh_out = Bh;
     gl.bl_out = Bh ? Bh + full : nullptr;
     gl.bsc = bsc;
+    gl.hbon = hbon;
     if (Bh) ci_bscale_kernel<<<L, 64, 0, st>>>(S, sv, np_, bsc);
     ci_gemm_kernel<kCiLauumKL><<<nwg, 512, 0, st>>>(gl, S);
   } else {
@@ -1648,7 +1655,7 @@ int ci_potrf_f32(int np_, int L, float* A, void* scratch, double* logdet, int32_
 int ci_inverse_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
                    int32_t* info, hipStream_t st) {
   LVAE_TRY(ci_factor_f32(np_, L, A, scratch, YT, Kinv, logdet, info, st));
-  return ci_lauum_f32(np_, L, scratch, YT, Kinv, nullptr, nullptr, nullptr, nullptr, nullptr, st);
+  return ci_lauum_f32(np_, L, scratch, YT, Kinv, nullptr, nullptr, nullptr, nullptr, nullptr, st, nullptr);
 }
 
 }  // namespace lvae

@@ -5,6 +5,7 @@
 // thread produces 16 elements of one column (consecutive lanes -> consecutive columns, so the
 // stores are coalesced).  The Gram is HBM-write-bound: per element 4 B (f32) / 8 B (f64) out.
 #include "gram_bwd.hpp"
+#include "gram_tab.hpp"
 
 namespace lvae {
 
@@ -326,7 +327,6 @@ __global__ __launch_bounds__(256) void gram_bwd_sum_kernel(GramBwdJobs J, const 
 // fp64 (exact 0/1 and exact differences, as the reference's double arithmetic); factor values,
 // products and sums are fp32 (the covariance is fp32); RBF / periodic use the native exp2.
 // ------------------------------------------------------------------------------------------
-constexpr float kLog2e = 1.4426950408889634f;
 typedef float g_f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ inline void tri_index(int t, int& I, int& J) {
@@ -359,7 +359,6 @@ __device__ inline void stage_cov(const double* __restrict__ x, int ldx, int n, i
 // fp64 path rounds the exact fp64 difference to fp32 as well).  One workgroup, written by the factor for
 // its kernels: flag 0 = not integer-coded (fp64 covariates), 1 = integer-coded, 2 = integer-coded and
 // every dim of tabmask spans < kTabD values (the table path, gram_tab_*; tab_ok: the spec allows it).
-constexpr int kTabD = 64;
 __global__ __launch_bounds__(1024) void cov_int_check_kernel(const double* __restrict__ x, int ldx, int n, int qs,
                                                              int tab_ok, int tabmask, int* __restrict__ flag) {
   __shared__ int bad, wide;
@@ -402,11 +401,6 @@ __global__ __launch_bounds__(1024) void cov_int_check_kernel(const double* __res
   if (threadIdx.x == 0) *flag = bad ? 0 : (tab_ok && !wide ? 2 : 1);
 }
 
-// sin(pi t) for t = |d| / p >= 0: reduced to pi r, r = t - rint(t) in [-1/2, 1/2] in fp64 (the
-// period is exact), then the native sine (sin^2 has period pi, so the sign flip of the reduction
-// cancels in every use; per_sin2 gives sin(2 pi t) = sin(2 pi r) for the period derivative)
-__device__ inline float per_sin(double t) { return __sinf(float(M_PI) * float(t - rint(t))); }
-__device__ inline float per_sin2(double t) { return __sinf(2.f * float(M_PI) * float(t - rint(t))); }
 
 // factor (kind, dim d, params pf) on the thread's 4 x 4 micro-tile: v[a][c] *= phi(x_i, x_j)
 template <typename CT>
@@ -788,153 +782,6 @@ __global__ __launch_bounds__(256) void kl_gram_bwd_tiles(DevSpec s, const double
 #ifndef LVAE_TAB_WPE
 #define LVAE_TAB_WPE 3  // the table adjoint's waves per SIMD (register cap)
 #endif
-constexpr int kTabMaxG = 3, kTabMaxBits = 5;
-constexpr int kTabR = kTabD + 1;  // table row stride (odd: the rows of different gate bits on other banks)
-constexpr int kTabMaxFillLds = kTabMaxG * (1 << kTabMaxBits) * kTabR;  // floats
-constexpr int kTabMaxBwdLds = 256 * kTabR;                             // floats (n_params 2^B <= 256)
-struct GramTab {
-  int ng, nbits, n_params;
-  int gdim[kTabMaxG];                               // the group's continuous dim (-1: none at all)
-  int bkind[kTabMaxBits], bdim[kTabMaxBits];        // gate b: LVAE_CAT / LVAE_BIN on dim
-  int cgrp[LVAE_MAX_COMP], cmask[LVAE_MAX_COMP];    // component r: its group, the gate bits it needs
-  int ckind[LVAE_MAX_COMP], cpi[LVAE_MAX_COMP];     // its continuous factor (kind -1: none), param index
-  int csc[LVAE_MAX_COMP];                           // its scale's param index
-  int n_comp;
-  int porder[64];                                   // parameter slots ordered by group
-  int pbeg[kTabMaxG + 1];                           // porder[pbeg[g] .. pbeg[g + 1]) belong to group g
-  int pcomp[64], ptype[64];                         // slot p: its component, 0 scale / 1 RBF l / 2 PER l / 3 PER p
-};
-
-// host: the table description of spec, false if the spec does not fit it
-static bool gram_tab_build(const lvae_kernel_spec* s, GramTab& t) {
-  t = GramTab{};
-  t.n_comp = s->n_comp;
-  t.n_params = s->n_params;
-  if (s->n_params > 64 || s->n_comp < 1) return false;
-  for (int r = 0; r < s->n_comp; ++r) {
-    int nc = 0, mask = 0;
-    t.ckind[r] = -1;
-    t.cpi[r] = 0;
-    t.cgrp[r] = -1;
-    t.csc[r] = s->scale_idx[r];
-    for (int f = 0; f < s->n_fac[r]; ++f) {
-      const int k = s->kind[r][f], d = s->dim[r][f];
-      if (k == LVAE_CAT || k == LVAE_BIN) {
-        int b = 0;
-        while (b < t.nbits && !(t.bkind[b] == k && t.bdim[b] == d)) ++b;
-        if (b == t.nbits) {
-          if (t.nbits == kTabMaxBits) return false;
-          t.bkind[b] = k;
-          t.bdim[b] = d;
-          ++t.nbits;
-        }
-        mask |= 1 << b;
-      } else if (k == LVAE_RBF || k == LVAE_PER) {
-        if (++nc > 1) return false;
-        int g = 0;
-        while (g < t.ng && t.gdim[g] != d) ++g;
-        if (g == t.ng) {
-          if (t.ng == kTabMaxG) return false;
-          t.gdim[g] = d;
-          ++t.ng;
-        }
-        t.cgrp[r] = g;
-        t.ckind[r] = k;
-        t.cpi[r] = s->param_idx[r][f];
-      } else {
-        return false;  // linear factors: not a function of the distance
-      }
-    }
-    t.cmask[r] = mask;
-  }
-  if (t.ng == 0) {
-    t.ng = 1;
-    t.gdim[0] = -1;
-  }
-  for (int r = 0; r < s->n_comp; ++r)
-    if (t.cgrp[r] < 0) t.cgrp[r] = 0;
-  // parameter slots -> (component, type); ordered by group
-  for (int p = 0; p < 64; ++p) t.pcomp[p] = -1;
-  for (int r = 0; r < s->n_comp; ++r) {
-    t.pcomp[t.csc[r]] = r;
-    t.ptype[t.csc[r]] = 0;
-    if (t.ckind[r] == LVAE_RBF) {
-      t.pcomp[t.cpi[r]] = r;
-      t.ptype[t.cpi[r]] = 1;
-    } else if (t.ckind[r] == LVAE_PER) {
-      t.pcomp[t.cpi[r]] = r;
-      t.ptype[t.cpi[r]] = 2;
-      t.pcomp[t.cpi[r] + 1] = r;
-      t.ptype[t.cpi[r] + 1] = 3;
-    }
-  }
-  int k = 0;
-  for (int g = 0; g < t.ng; ++g) {
-    t.pbeg[g] = k;
-    for (int p = 0; p < s->n_params; ++p)
-      if (t.pcomp[p] >= 0 && t.cgrp[t.pcomp[p]] == g) t.porder[k++] = p;
-  }
-  t.pbeg[t.ng] = k;
-  if (t.ng * (1 << t.nbits) * kTabR > kTabMaxFillLds) return false;
-  if (k * (1 << t.nbits) * kTabR > kTabMaxBwdLds) return false;
-  return true;
-}
-
-// the continuous factor phi_r(m) of component r at integer distance m (1 without one), fp32 as the
-// direct path (apply_factor); and the parts of its parameter derivatives the raw sums carry
-__device__ inline float tab_phi(const GramTab& t, int r, const float* __restrict__ sp, int m) {
-  const int k = t.ckind[r];
-  if (k == LVAE_RBF) {
-    const float ell = sp[t.cpi[r]], cf = -0.5f * kLog2e / (ell * ell), df = float(m);
-    return __builtin_amdgcn_exp2f(cf * df * df);
-  }
-  if (k == LVAE_PER) {
-    const float ell = sp[t.cpi[r]], cf = -2.f * kLog2e / (ell * ell);
-    const float sn = per_sin((double)m / (double)sp[t.cpi[r] + 1]);
-    return __builtin_amdgcn_exp2f(cf * sn * sn);
-  }
-  return 1.f;
-}
-
-// fill tables: tab[(g * 2^B + b) * kTabR + m] = sum over the components r of group g whose gates are in b
-__device__ inline void tab_build_fill(const GramTab& t, const float* __restrict__ sp, float* __restrict__ tab) {
-  const int nb = 1 << t.nbits, ne = t.ng * nb * kTabR;
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-    const int m = e % kTabR, b = (e / kTabR) % nb, g = e / (kTabR * nb);
-    float v = 0.f;
-    for (int r = 0; r < t.n_comp; ++r)
-      if (t.cgrp[r] == g && (t.cmask[r] & ~b) == 0) v += sp[t.csc[r]] * tab_phi(t, r, sp, m);
-    tab[e] = v;
-  }
-}
-
-// adjoint tables: tab[(k * 2^B + b) * kTabR + m] for the k-th slot of porder: d k_r / d theta without
-// the constants kl_gram_bwd_reduce applies (scale: phi; RBF l: s phi m^2; PER l: s phi sin^2 u; PER p:
-// s phi m sin 2u), 0 when r's gates are not all in b
-__device__ inline void tab_build_bwd(const GramTab& t, const float* __restrict__ sp, float* __restrict__ tab) {
-  const int nb = 1 << t.nbits, np = t.pbeg[t.ng], ne = np * nb * kTabR;
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-    const int m = e % kTabR, b = (e / kTabR) % nb, k = e / (kTabR * nb);
-    const int p = t.porder[k], r = t.pcomp[p], ty = t.ptype[p];
-    float v = 0.f;
-    if ((t.cmask[r] & ~b) == 0) {
-      const float phi = tab_phi(t, r, sp, m), sc = sp[t.csc[r]];
-      if (ty == 0) v = phi;
-      else if (ty == 1) v = sc * phi * float(m) * float(m);
-      else {
-        const double u = (double)m / (double)sp[t.cpi[r] + 1];
-        if (ty == 2) {
-          const float sn = per_sin(u);
-          v = sc * phi * sn * sn;
-        } else {
-          v = sc * phi * float(m) * per_sin2(u);
-        }
-      }
-    }
-    tab[e] = v;
-  }
-}
-
 // the micro-tile's gate bits as table row offsets: bits[a][c] = (sum_b pass_b << b) * kTabR
 __device__ inline void tab_bits(const GramTab& t, const float* __restrict__ sx1, const float* __restrict__ sx2,
                                 int tr, int tc, int (&bits)[4][4]) {
@@ -1074,8 +921,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
                                                               const float* __restrict__ Sx, int nsplit,
                                                               const double* __restrict__ alpha,
                                                               double* __restrict__ part, int ntiles,
-                                                              const int* __restrict__ covflag) {
-  if (*covflag != 2) return;  // (uniform, before any barrier)
+                                                              const int* __restrict__ covflag,
+                                                              const int* __restrict__ hbon) {
+  if (*covflag != 2 || (hbon && *hbon)) return;  // (uniform, before any barrier; hbon: kl_hyper.hip's path)
   __shared__ float sx1[2][kGT * kMaxQB];  // (two buffers: this tile's and the next one's)
   __shared__ float sx2[2][kGT * kMaxQB];
   __shared__ float sp[64];
@@ -1215,6 +1063,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_TAB_WP
 // associative, so the sums are DETERMINISTIC (no order dependence) and every element keeps 2^-SHIFT of the
 // bound (~2^-44).  After the tiles: raw_p = 2^(E - SHIFT) sum_bins (double) H D_p in a fixed order, into the
 // same per-workgroup slots kl_gram_bwd_reduce reads.  The diagonal's sum (d/d noise) stays an fp32 / fp64 sum.
+// Measured (r5, scripts/gpu_r5b.sh, the exact-KL fwd + bwd alone at the headline, rocprofv3, same box): 813-845 us
+// against the table kernel's 519-524 us -- bit-reproducible and within 4e-6 of it, but the 64-bit LDS atomics
+// serialise on the bins the lanes of one instruction share (~16-30 distinct (bits, d) per 64 elements of a tile
+// row band), which costs more than the per-parameter table reads they replace.  Opt-in: LVAE_GRAM_HIST=1.
 // ------------------------------------------------------------------------------------------
 __device__ inline long long fx_q(float g, int sbias) {
   const unsigned u = __float_as_uint(g);
@@ -1239,8 +1091,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LVAE_HIST_W
     GramTab tb, const double* __restrict__ x, int ldx, int n, int np_, int qs, const double* __restrict__ params,
     const float* __restrict__ Kinv, const float* __restrict__ S, const float* __restrict__ Sx, int nsplit,
     const double* __restrict__ alpha, const double* __restrict__ kdiag, const float* __restrict__ vv, int shift,
-    double* __restrict__ part, int ntiles, const int* __restrict__ covflag) {
-  if (*covflag != 2) return;  // (uniform, before any barrier)
+    double* __restrict__ part, int ntiles, const int* __restrict__ covflag, const int* __restrict__ hbon) {
+  if (*covflag != 2 || (hbon && *hbon)) return;  // (uniform, before any barrier)
   __shared__ float sx1[2][kGT * kMaxQB];  // (two buffers: this tile's and the next one's)
   __shared__ float sx2[2][kGT * kMaxQB];
   __shared__ float sp[64];
@@ -1799,10 +1651,14 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L) {
   return (size_t)L * kl_gram_bwd_groups(np_, L) * kBwdSlots * sizeof(double);
 }
 
+int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, const double* params,
+                 const float* Kinv, const float* v, const double* alpha, const double* kdiag, void* wsbase, double* part,
+                 int G, hipStream_t st);
+
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
                 const double* alpha, const double* kdiag, const float* v, const double* gkl, double* part,
-                double* dparams, double* dnoise, const int* covflag, hipStream_t st) {
+                double* dparams, double* dnoise, const int* covflag, void* hbws, const int* hbon, hipStream_t st) {
   const int bucket = spec_bucket(spec);
   const int qs = spec_qs(spec);
   if (!bucket || qs > kMaxQB || spec->n_params > 64) return -1;
@@ -1823,17 +1679,18 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
   GramTab tb;
   if (gram_tab_build(spec, tb) && !getenv_off("LVAE_GRAM_TAB")) {  // (the same decision as kl_gram_fill's)
     const size_t tabb = (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
-    if (!getenv_off("LVAE_GRAM_HIST")) {
+    const char* hv = getenv("LVAE_GRAM_HIST");
+    if (hv && atoi(hv) == 1) {  // opt-in: measured slower (r5: 813-845 vs 519-524 us alone, gpurun_out/r5b)
       // the histogram adjoint: SHIFT = 62 - (bits of a bin's largest possible count, + 1)
       const int per = (ntiles + G - 1) / G;
       int hb = 1;
       while ((1ll << hb) < (long long)per * kGT * kGT) ++hb;
       const size_t hdyn = (size_t)tb.ng * (1 << tb.nbits) * kTabR * sizeof(double) + tabb;
       kl_gram_bwd_hist_kernel<<<dim3(G, L), 256, hdyn, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx, nsplit,
-                                                             alpha, kdiag, v, 62 - (hb + 1), part, ntiles, covflag);
+                                                             alpha, kdiag, v, 62 - (hb + 1), part, ntiles, covflag, hbon);
     } else {
       kl_gram_bwd_tab_kernel<<<dim3(G, L), 256, dyn + tabb, st>>>(tb, x, ldx, n, np_, qs, params, Kinv, S, Sx,
-                                                                  nsplit, alpha, part, ntiles, covflag);
+                                                                  nsplit, alpha, part, ntiles, covflag, hbon);
     }
   }
   if (bucket == 1) {
@@ -1847,6 +1704,8 @@ int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, i
     kl_gram_bwd_tiles<16, 4, double><<<dim3(G, L), 256, dyn, st>>>(ds, x, ldx, n, np_, qs, params, Kinv, S, Sx,
                                                                     nsplit, alpha, part, ntiles, covflag);
   }
+  // the binned hyper-gradient (kl_hyper.hip; its kernels exit when the plan is off, the table kernel when it is on)
+  if (hbws) LVAE_TRY(kl_hyper_bwd(spec, x, ldx, n, np_, L, params, Kinv, v, alpha, kdiag, hbws, part, G, st));
   kl_gram_bwd_reduce<<<dim3(spec->n_params + 1, L), 256, 0, st>>>(pinfo, spec->n_params, part, G, params, gkl,
                                                                   dparams, dnoise);
   LVAE_CHECK_LAUNCH();

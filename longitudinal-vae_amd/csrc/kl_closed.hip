@@ -41,13 +41,19 @@ size_t kl_gram_bwd_partials_bytes(int np_, int L);
 int kl_gram_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                 const double* params, const float* Kinv, const float* S, const float* Sx, int nsplit,
                 const double* alpha, const double* kdiag, const float* v, const double* gkl, double* part,
-                double* dparams, double* dnoise, const int* covflag, hipStream_t st);
+                double* dparams, double* dnoise, const int* covflag, void* hbws, const int* hbon, hipStream_t st);
 int syrk_x3_splits(int np_, int L);
-int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st);
+int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st,
+                   const int* skip);
+size_t kl_hyper_bytes(int np_, int L);
+struct HbDev;
+HbDev* kl_hyper_dev(void* base, int np_, int L);
+int kl_hyper_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, void* wsbase,
+                  const int* covflag, hipStream_t st);
 int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* Kinv, double* logdet,
                   int32_t* info, hipStream_t st, float* lout = nullptr);
 int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const double* mu, const float* sv,
-                 float* apart, _Float16* Bh, float* bsc, hipStream_t st);
+                 float* apart, _Float16* Bh, float* bsc, hipStream_t st, const int* hbon);
 size_t ci_scratch_bytes(int np_, int L);
 size_t kl_resid_partials_bytes(int np_, int L);
 int kl_gram_resid(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
@@ -76,6 +82,8 @@ struct KLWorkspace {
   char* rb;          // the binned residual's plan / bin sums (kl_resid_bins.hip)
   double* K64;       // [ceil(L / 2), np, np] fp64 K of the dims whose diag K^-1 is refined (kl_refine.hip), two
                      // rounds: = the Y^T planes (dead between lauum and the backward's S) + np^2 floats for odd L
+  char* hb;          // the binned hyper-gradient's plan, point bins / runs and slab partials (kl_hyper.hip)
+  const int* hbon;   // its device flag: on -> the lauum writes K^-1's mirror, the S GEMM and the table adjoint exit
   double* rest;      // [L] the refinement gate's estimate (sum_r s_r + noise) max (K^-1)_ii
   int* rflag;        // [L] 1: diag K^-1 refined
   size_t bytes;
@@ -108,6 +116,8 @@ struct KLWorkspace {
     covflag = (int*)take(sizeof(int));
     rb = take(kl_resid_bins_bytes(np_, L, LVAE_MAX_COMP));
     Sx = (float*)take(mat * (size_t)(syrk_x3_splits(np_, L) - 1));
+    hb = take(kl_hyper_bytes(np_, L));
+    hbon = base ? reinterpret_cast<const int*>(kl_hyper_dev(hb, np_, L)) : nullptr;  // (HbDev::on: its first member)
     rest = (double*)take((size_t)L * sizeof(double));
     rflag = (int*)take((size_t)L * sizeof(int));
     bytes = off;
@@ -286,6 +296,12 @@ extern "C" {
 
 int lvae_kl_closed_padded_n(int n) { return ((n + 255) / 256) * 256; }
 
+// (kl_hyper.hip's state query: where the workspace keeps the binned hyper-gradient's region)
+size_t kl_hyper_offset_in_kl_ws(int np_, int L) {
+  KLWorkspace ws(nullptr, np_, L);
+  return (size_t)(uintptr_t)ws.hb;
+}
+
 size_t lvae_kl_closed_workspace_size(int n, int L) {
   const int np_ = lvae_kl_closed_padded_n(n);
   return KLWorkspace(nullptr, np_, L).bytes;
@@ -319,6 +335,8 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
     ProfScope ps(LVAE_PH_GRAM, st);
     LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, ws.covflag, st));
   }
+  // the binned hyper-gradient's plan (covariates only; the reduce's lauum and the backward read its flag)
+  LVAE_TRY(kl_hyper_plan(spec, x, ldx, n, np_, L, ws.hb, ws.covflag, st));
   // Y = L^-1 and log|K|: blocked Cholesky + trtri (chol_inv.hip; phases POTRF / POTRI inside); lauum
   // runs in the reduce
   LVAE_TRY(ci_factor_f32(np_, L, ws.A, ws.chol, ws.planes, ws.Kinv, ws.logdet, info, st));
@@ -355,7 +373,7 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
   // K^-1 (+ the partials of a0 = K^-1 mu, + the B planes); a0, d; r = mu - K a0 in fp64 from the
   // covariates; a = a0 + K^-1 r
   LVAE_TRY(ci_lauum_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.mu, ws.sv, ws.apart, need_bwd ? ws.Bp : nullptr,
-                        ws.bsc, st));
+                        ws.bsc, st, ws.hbon));
   kl_alpha0_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.apart, ws.Kinv, np_, ws.alpha, ws.kdiag);
   const bool rb_on = kl_resid_bins_enabled(spec, n);  // (the plan: the factor call's, joined on `st`)
   LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res,
@@ -406,12 +424,12 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
   float* S = reinterpret_cast<float*>(ws.planes);
   {
     ProfScope ps(LVAE_PH_SYRK, st);
-    LVAE_TRY(syrk_tiles_f32(np_, L, ws.bsc, ws.Bp, S, ws.Sx, st));
+    LVAE_TRY(syrk_tiles_f32(np_, L, ws.bsc, ws.Bp, S, ws.Sx, st, ws.hbon));
   }
   {
     ProfScope ps(LVAE_PH_GRAM_BWD, st);
     LVAE_TRY(kl_gram_bwd(spec, x, ldx, n, np_, L, params, ws.Kinv, S, ws.Sx, syrk_x3_splits(np_, L), ws.alpha,
-                         ws.kdiag, ws.v, gkl, ws.part, dparams, dnoise, ws.covflag, st));
+                         ws.kdiag, ws.v, gkl, ws.part, dparams, dnoise, ws.covflag, ws.hb, ws.hbon, st));
   }
   LVAE_CHECK_LAUNCH();
   return 0;

@@ -295,8 +295,10 @@ __global__ __launch_bounds__(512) void syrk_tiles_kernel(const _Float16* __restr
 template <int NS>
 __global__ __launch_bounds__(512) void syrk_c16_kernel(const _Float16* __restrict__ Bh, const _Float16* __restrict__ Bl,
                                                        const float* __restrict__ bsc, float* __restrict__ S,
-                                                       float* __restrict__ Sx, int np_, int ntl, int nwg, int L, int ns) {
+                                                       float* __restrict__ Sx, int np_, int ntl, int nwg, int L, int ns,
+                                                       const int* __restrict__ skip) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[NS * kC16Stage];
+  if (skip && *skip) return;  // (uniform) the binned hyper-gradient needs no S (kl_hyper.hip)
   // tiles v = blockIdx.x, + gridDim.x, ...: one each with the full grid (nwg workgroups); a grid of fewer
   // (a multiple of 8: v keeps its blockIdx's XCD) leaves CUs to the ConvVAE stream (syrk_tiles_f32)
   for (int v = blockIdx.x; v < nwg; v += gridDim.x) {
@@ -351,7 +353,8 @@ static int syrk_grid(int nwg) {
   return g >= 8 ? g : nwg;
 }
 
-int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st) {
+int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, float* S, float* Sx, hipStream_t st,
+                   const int* skip) {
   if (np_ % kSxT) return -1;
   const int64_t per = (int64_t)np_ * np_;
   const int ns = syrk_x3_splits(np_, L);
@@ -359,7 +362,7 @@ int syrk_tiles_f32(int np_, int L, const float* bsc, const _Float16* planes, flo
   const int nt = np_ / kSxT, ntl = nt * (nt + 1) / 2, nwg = ntl * L * ns;
   if (kCiBC16)
     syrk_c16_kernel<kC16NS><<<syrk_grid(nwg), 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl,
-                                                            nwg, L, ns);
+                                                            nwg, L, ns, skip);
   else
     syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, bsc, S, Sx, np_, ntl, nwg, L, ns);
   LVAE_CHECK_LAUNCH();
@@ -379,9 +382,11 @@ int syrk_dev_variant(int variant, int np_, int L, const float* rsc, const _Float
   else if (variant == 4)  // the product kernel (rsc[l * np] read as the dims' scales: ones)
     syrk_tiles_kernel<<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
   else if (variant == 5)  // chunk-major planes (x3_c16.hpp), 4-stage ring
-    syrk_c16_kernel<4><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
+    syrk_c16_kernel<4><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1,
+                                            nullptr);
   else if (variant == 6)  // chunk-major planes, 5-stage ring (all 160 KB of LDS)
-    syrk_c16_kernel<5><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1);
+    syrk_c16_kernel<5><<<nwg, 512, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, nullptr, np_, ntl, nwg, L, 1,
+                                            nullptr);
   else if (variant == 3)
     syrk_h2_kernel<<<2 * nwg, 256, 0, st>>>(planes, planes + (int64_t)L * per, rsc, S, np_, 2 * ntl, 2 * nwg, L);
   else

@@ -93,6 +93,7 @@ SIGNATURES = {
     "lvae_kl_closed_bwd_latent_f32": (_I32, [_I32, _I32, _VP, _I32, _VP, _VP, _VP, _VP, _VP]),
     "lvae_kl_closed_bwd_hyper_f32": (_I32, [_SPEC, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_kl_closed_refine_state": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP]),
+    "lvae_kl_closed_hyper_state": (_I32, [_I32, _I32, _VP, _VP, _VP]),
     "lvae_vae_loss_fwd_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_vae_loss_bwd_partials": (_SZ, [_I32]),
     "lvae_vae_loss_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _VP]),

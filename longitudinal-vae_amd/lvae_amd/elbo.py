@@ -157,6 +157,22 @@ def kl_closed_refine_log():
         _refine_log = prev
 
 
+_hyper_log = None  # a list while kl_closed_hyper_log() is active
+
+
+@contextlib.contextmanager
+def kl_closed_hyper_log():
+    """Yields a list that gets, per KL_closed forward inside the block, the device int32 [1]: 1 when the
+    backward's hyper-parameter half takes the binned route (kl_hyper.hip: no S GEMM), 0 for the S GEMM +
+    Gram adjoint (lvae_kl_closed_hyper_state)."""
+    global _hyper_log
+    prev, _hyper_log = _hyper_log, []
+    try:
+        yield _hyper_log
+    finally:
+        _hyper_log = prev
+
+
 def _log_refine(lib, ws, n, L, dev):
     est = torch.zeros(L, dtype=torch.float64, device=dev)
     flag = torch.zeros(L, dtype=torch.int32, device=dev)
@@ -233,6 +249,11 @@ class _KLClosedFn(torch.autograd.Function):
         _check_info(info, "KL_closed cholesky")
         if _refine_log is not None:
             _log_refine(lib, ws, n, L, dev)
+        if _hyper_log is not None:
+            on = torch.zeros(1, dtype=torch.int32, device=dev)
+            _lib.check(lib.lvae_kl_closed_hyper_state(n, L, _lib.ptr(ws), _lib.ptr(on), _lib.stream_ptr()),
+                       "kl_closed_hyper_state")
+            _hyper_log.append(on)
         state.ws, state.p, state.x64, state.spec, state.n, state.L = ws, p, x64, spec, n, L
         ctx.save_for_backward(lv64, ws)
         ctx.in_dtypes = (mu.dtype, logv.dtype)

@@ -1,0 +1,102 @@
+"""The exact KL backward's two hyper-parameter routes (kl_hyper.hip): the binned route (no S = K^-1 V K^-1 GEMM:
+bin sums of K^-1 for the components without an id gate, the id runs' blocks for the others) against the fp64
+oracle's autograd of KL_closed (elbo_functions.py:8-34) and against the S-GEMM route (LVAE_KL_HYPER=0) on the
+same inputs.  Tolerance: the north star's 1e-4 relative (of the max-norm) on every raw-parameter gradient; the two
+routes agree to 2e-5 (both fp32-equivalent inverses, different summation)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import lvae_oracle as O
+from test_gpu_regime_b import CFG, DEV, _random_hypers, rel, set_raw
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(P, L, seed, perm=None, hyper=None):
+    import lvae_amd as la
+    from lvae_amd.data import health_mnist_covariates
+    from lvae_amd.elbo import kl_closed_hyper_log
+    T = 16
+    X = torch.tensor(health_mnist_covariates(P, T, seed=seed))
+    gen = torch.Generator().manual_seed(seed)
+    mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
+    if perm is not None:
+        X, mu, lv = X[perm], mu[perm], lv[perm]
+    k = la.generate_kernel(**CFG, latent_dim=L).double()
+    raw = _random_hypers(k, L, np.random.default_rng(seed))
+    set_raw(k, raw)
+    kd = k.to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+    mu_d, lv_d = mu.to(DEV).requires_grad_(), lv.to(DEV).requires_grad_()
+    old = os.environ.get("LVAE_KL_HYPER")
+    if hyper is not None:
+        os.environ["LVAE_KL_HYPER"] = str(hyper)
+    try:
+        with kl_closed_hyper_log() as hlog:
+            kl = la.KL_closed_batched(kd, X.to(DEV), lik, mu_d, lv_d)
+        (kl * torch.arange(1, L + 1, device=DEV)).sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("LVAE_KL_HYPER", None)
+        else:
+            os.environ["LVAE_KL_HYPER"] = old
+    draw = torch.stack([p.grad for _, p in kd.named_parameters()], 1).cpu()
+    dnoise = lik._log_noise.grad.cpu()
+    return dict(X=X, mu=mu, lv=lv, raw=raw, kl=kl.detach().cpu(), draw=draw, dmu=mu_d.grad.cpu(), dlv=lv_d.grad.cpu(),
+                on=int(hlog[0].item()), dnoise=dnoise)
+
+
+def _oracle_grads(r, l):
+    spec = O.spec_full(**CFG)
+    raw = torch.tensor(r["raw"][l], requires_grad=True)
+    ref = O.kl_closed(spec, O.constrain(raw), r["X"], 1.0, r["mu"][:, l], r["lv"][:, l])
+    ((l + 1) * ref).backward()
+    return ref.detach(), raw.grad
+
+
+@pytest.mark.parametrize("P,L", [(64, 3), (13, 2), (256, 2)])  # N = 1024, 208 (ragged: padded to 256), 4096
+def test_binned_hyper_route_vs_oracle(hip, P, L):
+    r = _run(P, L, seed=P)
+    assert r["on"] == 1, "the binned route should run on subject-contiguous integer covariates"
+    for l in range(L):
+        ref, g = _oracle_grads(r, l)
+        assert rel(r["kl"][l], ref) < 1e-4
+        e = rel(r["draw"][l], g)
+        print(f"P={P} dim {l}: binned-route raw-parameter gradients rel err {e:.2e}")
+        assert e < 1e-4
+
+
+@pytest.mark.parametrize("P,L", [(64, 3), (256, 2)])
+def test_binned_and_gemm_routes_agree(hip, P, L):
+    a = _run(P, L, seed=P + 1)
+    b = _run(P, L, seed=P + 1, hyper=0)
+    assert a["on"] == 1 and b["on"] == 0
+    assert torch.equal(a["kl"], b["kl"])  # (the forward is the same either way)
+    assert torch.equal(a["dmu"], b["dmu"]) and torch.equal(a["dlv"], b["dlv"])
+    e = rel(a["draw"], b["draw"])
+    en = rel(a["dnoise"], b["dnoise"])
+    print(f"P={P}: binned vs S-GEMM route raw gradients {e:.2e}, noise {en:.2e}")
+    assert e < 2e-5 and en < 2e-5
+
+
+def test_binned_route_off_for_unsorted_ids(hip):
+    """Subjects interleaved (the id runs are not contiguous): the plan turns the binned route off and the S-GEMM
+    route runs; gradients still match the oracle."""
+    P, L, T = 16, 2, 16
+    perm = torch.randperm(P * T, generator=torch.Generator().manual_seed(3))
+    r = _run(P, L, seed=7, perm=perm)
+    assert r["on"] == 0
+    for l in range(L):
+        _, g = _oracle_grads(r, l)
+        assert rel(r["draw"][l], g) < 1e-4
+
+
+def test_binned_route_deterministic(hip):
+    a = _run(64, 2, seed=9)
+    b = _run(64, 2, seed=9)
+    assert torch.equal(a["draw"], b["draw"])
