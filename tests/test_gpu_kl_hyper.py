@@ -30,7 +30,7 @@ def _run(P, L, seed, perm=None, hyper=None):
     raw = _random_hypers(k, L, np.random.default_rng(seed))
     set_raw(k, raw)
     kd = k.to(DEV)
-    lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+    lik = la.GaussianLikelihood(L, noise=1.0).to(DEV)
     mu_d, lv_d = mu.to(DEV).requires_grad_(), lv.to(DEV).requires_grad_()
     old = os.environ.get("LVAE_KL_HYPER")
     if hyper is not None:
