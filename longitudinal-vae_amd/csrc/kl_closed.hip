@@ -298,8 +298,9 @@ int lvae_kl_closed_padded_n(int n) { return ((n + 255) / 256) * 256; }
 
 // (kl_hyper.hip's state query: where the workspace keeps the binned hyper-gradient's region)
 size_t kl_hyper_offset_in_kl_ws(int np_, int L) {
-  KLWorkspace ws(nullptr, np_, L);
-  return (size_t)(uintptr_t)ws.hb;
+  char* const fake = reinterpret_cast<char*>(uintptr_t(1) << 20);  // (offsets only: any aligned base)
+  KLWorkspace ws(fake, np_, L);
+  return (size_t)(ws.hb - fake);
 }
 
 size_t lvae_kl_closed_workspace_size(int n, int L) {
