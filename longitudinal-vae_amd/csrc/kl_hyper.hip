@@ -24,8 +24,9 @@
 // applies the same parameter constants.
 //
 // Conditions (hb_plan_kernel, on the device; otherwise `on` = 0 and the S GEMM + table adjoint run as before):
-// the table path's (covariate flag 2); a Cat gate covariate spanning > 16 values is "big", at most one; its values
-// non-decreasing over the points (runs contiguous) with runs of <= 64 points; far binnings <= 4, with <= 128 bins
+// the table path's (covariate flag 2); the Cat gate covariate of the widest range (> 4 values) is "big" (the id),
+// the other Cat gates span <= 16 values; its values non-decreasing over the points (runs contiguous) with runs of
+// <= 64 points; far binnings <= 4, with <= 128 bins
 // in all and sum nbins^2 <= 4096; <= 8 parameter slots on near components.
 #include "blkinv.hpp"
 #include "gram_tab.hpp"
@@ -36,7 +37,8 @@ constexpr int kHbMaxBin = 4;    // far binnings
 constexpr int kHbBins = 128;    // far bins in all
 constexpr int kHbBins2 = 4096;  // sum over binnings of nbins^2
 constexpr int kHbRun = 64;      // longest run of the big covariate
-constexpr int kHbSmall = 16;    // a Cat gate covariate spanning more values is big
+constexpr int kHbSmall = 16;    // Cat gate covariates other than the big one span at most this many values
+constexpr int kHbSmallest = 4;  // the big covariate spans more than this many values
 constexpr int kHbNear = 8;      // parameter slots of the near components
 constexpr int kHbT = 64;        // row tile = column slab
 constexpr int kHbTP = 65;       // LDS pitch of a tile row (floats)
@@ -120,14 +122,13 @@ __global__ __launch_bounds__(1024) void hb_plan_kernel(GramTab tb, const double*
     HbDev p{};
     int f = 0;
     p.big = -1;
-    for (int b = 0; b < tb.nbits; ++b) {
+    for (int b = 0; b < tb.nbits; ++b) {  // big: the Cat gate covariate of the widest range (> kHbSmallest values)
       p.gmin[b] = lo[b];
       p.grng[b] = hi[b] - lo[b] + 1;
-      if (tb.bkind[b] == LVAE_CAT && p.grng[b] > kHbSmall) {
-        if (p.big >= 0) f = 1;  // two big covariates
-        p.big = b;
-      }
+      if (tb.bkind[b] == LVAE_CAT && p.grng[b] > kHbSmallest && (p.big < 0 || p.grng[b] > p.grng[p.big])) p.big = b;
     }
+    for (int b = 0; b < tb.nbits; ++b)  // a second wide Cat covariate would need bins of its own: not this route
+      if (b != p.big && tb.bkind[b] == LVAE_CAT && p.grng[b] > kHbSmall) f = 1;
     for (int g = 0; g < tb.ng; ++g) {
       p.wmin[g] = tb.gdim[g] >= 0 ? lo[tb.nbits + g] : 0;
       p.wrng[g] = tb.gdim[g] >= 0 ? hi[tb.nbits + g] - lo[tb.nbits + g] + 1 : 1;
