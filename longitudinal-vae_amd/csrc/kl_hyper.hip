@@ -217,6 +217,14 @@ __global__ __launch_bounds__(1024) void hb_plan_kernel(GramTab tb, const double*
 // ------------------------------------------------------------------------------------------
 __device__ inline int hb_row_slot(int row) { return (row >> 6) & 1; }
 
+// an LDS fp64 add whose return value is not used (ds_add_f64): a wave's adds to one address apply in program order
+__device__ inline void hb_lds_add(double* p, double v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+constexpr int kHbPre = (kHbQ * kHbT + 255) / 256;  // covariate values a thread prefetches per tile
+typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
+
 __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const double* __restrict__ x, int ldx,
                                                       int n, int np_, int qs, const double* __restrict__ params,
                                                       const float* __restrict__ Kinv, const float* __restrict__ vv,
@@ -225,10 +233,12 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
   __shared__ __attribute__((aligned(16))) float T[2][kHbT * kHbTP];  // the row tiles of the window (slot = (row / 64) & 1)
   __shared__ float cov[2][kHbQ][kHbT];          // their covariates
   __shared__ double alr[2][kHbT];               // their alpha
-  __shared__ uint8_t pb[kHbMaxBin][2][kHbT];    // their bins
   __shared__ float vs[kHbT];                    // v of the slab's columns
   __shared__ float sp[64];
   __shared__ int runs[kHbT], runl[kHbT], nrun;
+  __shared__ int sbdim[kTabMaxBits], sbkind[kTabMaxBits];  // the gates (LDS copies: no kernarg loads in loops)
+  __shared__ int snoff[kHbNear], sngd[kHbNear];            // near slot: its table offset, its distance dim
+  __shared__ uint8_t cbin[kHbMaxBin][kHbT];     // bins of the slab's columns
   __shared__ double red[4][kHbNear + 1];
   extern __shared__ double hdyn[];              // H [kHbBins][64] (fp64), then the derivative tables (fp32)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, J = blockIdx.x, l = blockIdx.y, J0 = J * kHbT;
@@ -237,58 +247,100 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
   if (!d.on) return;  // (uniform)
   double* H = hdyn;
   float* tab = reinterpret_cast<float*>(hdyn + kHbBins * kHbT);
-  const int tstride = (1 << tb.nbits) * kTabR;
+  const int tstride = (1 << tb.nbits) * kTabR, nbits = tb.nbits;
   if (tid < tb.n_params) sp[tid] = float(params[(int64_t)l * tb.n_params + tid]);
   for (int e = tid; e < d.nbins * kHbT; e += 256) H[e] = 0.0;
   if (tid < kHbT) vs[tid] = vv[(int64_t)l * np_ + J0 + tid];
+  if (tid < kTabMaxBits) {
+    sbdim[tid] = tid < nbits ? tb.bdim[tid] : 0;
+    sbkind[tid] = tid < nbits ? tb.bkind[tid] : 0;
+  }
+  if (tid < d.nnear) {
+    const int kk = d.nslot[tid];
+    snoff[tid] = kk * tstride;
+    sngd[tid] = tb.gdim[tb.cgrp[tb.pcomp[tb.porder[kk]]]];
+  }
+  for (int e = tid; e < d.nbin * kHbT; e += 256) cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
   __syncthreads();
   tab_build_bwd(tb, sp, tab);
   const float* K = Kinv + (int64_t)l * np_ * np_;
   const double* al = alpha + (int64_t)l * np_;
+  const int nbin = d.nbin, nnear = d.nnear, bigon = d.big >= 0;
+  const int myoff = w < nbin ? d.boff[w] : 0;
   double nacc[kHbNear];
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) nacc[k] = 0.0;
   double tS = 0.0;
   const int nt = np_ / kHbT;
-  for (int I = 0; I < nt; ++I) {
-    const int I0 = I * kHbT, sl = I & 1;
-    // load: the tile (float4 runs of the rows), the rows' covariates / alpha / bins; the runs ending in it
+  // software pipeline: tile I + 1's K^-1 rows, covariates, alpha, bins and run ends in registers during tile I
+  hb_f32x4 pk[4];
+  float pc[kHbPre];
+  double pa = 0.0;
+  int pbn = 255, pre_ = -1, prs = -1;
+  auto fetch = [&](int I) {
+    const int I0 = I * kHbT;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = tid + 256 * u, r = e >> 4, c4 = (e & 15) * 4;
-      const float4 v4 = *reinterpret_cast<const float4*>(K + (int64_t)(I0 + r) * np_ + J0 + c4);
+      pk[u] = __builtin_nontemporal_load(reinterpret_cast<const hb_f32x4*>(K + (int64_t)(I0 + r) * np_ + J0 + c4));
+    }
+#pragma unroll
+    for (int u = 0; u < kHbPre; ++u) {
+      const int e = tid + 256 * u, q = e / kHbT, r = e % kHbT;
+      pc[u] = (q < qs && I0 + r < n) ? float(x[(int64_t)(I0 + r) * ldx + q]) : 0.f;
+    }
+    if (tid < kHbT) pa = al[I0 + tid];
+    pbn = w < nbin ? (int)ws.pbin[(size_t)w * np_ + I0 + lane] : 255;
+    if (w == 0 && bigon) {
+      pre_ = ws.re[I0 + lane];
+      prs = ws.rs[I0 + lane];
+    }
+  };
+  fetch(0);
+  for (int I = 0; I < nt; ++I) {
+    const int I0 = I * kHbT, sl = I & 1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, r = e >> 4, c4 = (e & 15) * 4;
       float* t = &T[sl][r * kHbTP + c4];
-      t[0] = v4.x;
-      t[1] = v4.y;
-      t[2] = v4.z;
-      t[3] = v4.w;
+      t[0] = pk[u][0];
+      t[1] = pk[u][1];
+      t[2] = pk[u][2];
+      t[3] = pk[u][3];
     }
-    for (int e = tid; e < qs * kHbT; e += 256) {
-      const int q = e / kHbT, r = e % kHbT;
-      cov[sl][q][r] = I0 + r < n ? float(x[(int64_t)(I0 + r) * ldx + q]) : 0.f;
+#pragma unroll
+    for (int u = 0; u < kHbPre; ++u) {
+      const int e = tid + 256 * u, q = e / kHbT, r = e % kHbT;
+      if (q < kHbQ) cov[sl][q][r] = pc[u];
     }
-    if (tid < kHbT) alr[sl][tid] = al[I0 + tid];
-    for (int e = tid; e < d.nbin * kHbT; e += 256) pb[e / kHbT][sl][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + I0 + e % kHbT];
-    if (w == 0) {
+    if (tid < kHbT) alr[sl][tid] = pa;
+    const int bn = pbn;  // (wave w < nbin: the bin of row lane in binning w)
+    if (w == 0) {        // the runs of the big covariate ending in this tile
       const int i = I0 + lane;
-      const bool last = d.big >= 0 && i < n && ws.re[i] == i + 1;
+      const bool last = bigon && i < n && pre_ == i + 1;
       const unsigned long long m = __ballot(last);
       if (last) {
         const int k = __popcll(m & ((1ull << lane) - 1));
-        runs[k] = ws.rs[i];
-        runl[k] = i + 1 - ws.rs[i];
+        runs[k] = prs;
+        runl[k] = i + 1 - prs;
       }
       if (lane == 0) nrun = __popcll(m);
     }
     __syncthreads();
-    // H_g[bin(i)][m] += K^-1_im: wave w owns the bins = w (mod 4) (each H entry one owner: a fixed order)
-    for (int r = 0; r < kHbT; ++r)
-      for (int g = 0; g < d.nbin; ++g) {
-        const int b = pb[g][sl][r];
-        if (b != 255 && ((d.boff[g] + b) & 3) == w) H[(d.boff[g] + b) * kHbT + lane] += (double)T[sl][r * kHbTP + lane];
+    if (I + 1 < nt) fetch(I + 1);  // (in flight under this tile's work)
+    // H_w[bin(i)][m] += K^-1_im: wave w owns binning w, lane m column m; the rows in order (ds_add_f64 without
+    // return: no dependent latency, program order per address -> a fixed summation order)
+    if (w < nbin) {
+      const float* tr = &T[sl][lane];
+#pragma unroll 16
+      for (int r = 0; r < kHbT; ++r) {
+        const int b = __builtin_amdgcn_readlane(bn, r);
+        if (b != 255) hb_lds_add(&H[(myoff + b) * kHbT + lane], (double)tr[r * kHbTP]);
       }
+    }
     {  // the slab's part of tr S = sum_m v_m sum_i (K^-1_im)^2: wave w, rows = w (mod 4)
       float ts = 0.f;
+#pragma unroll
       for (int r = w; r < kHbT; r += 4) {
         const float t = T[sl][r * kHbTP + lane];
         ts += t * t;
@@ -299,7 +351,8 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
     // to the waves; each lane's 4 pairs contracted at once with the near slots' tables
     {
       int item = w;
-      for (int k = 0; k < nrun; ++k) {
+      const int nr = nrun;
+      for (int k = 0; k < nr; ++k) {
         const int s0 = runs[k], len = runl[k], nb16 = (len + 15) >> 4;
         for (; item < nb16 * nb16; item += 4) {
           const int bi = item / nb16, bj = item % nb16;
@@ -317,28 +370,31 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
           }
           // lane: C[4 lk + q][li] -> pair (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li)
-          const int j = s0 + 16 * bj + li;
+          const int j = s0 + 16 * bj + li, sj = hb_row_slot(j), rj = j & 63;
+          const bool jin = j >= J0 && j < J0 + kHbT;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int ioff = 16 * bi + 4 * lk + q, i = s0 + ioff;
-            if (ioff >= len || 16 * bj + li >= len) continue;
-            const int si = hb_row_slot(i), sj = hb_row_slot(j), ri = i & 63, rj = j & 63;
-            // the pair's gate bits and distances (tab_bits / tab_index on single elements)
+            if (ioff >= len || !vb) continue;
+            const int si = hb_row_slot(i), ri = i & 63;
+            // the pair's gate bits (tab_bits on one element)
             int bits = 0;
-            for (int b = 0; b < tb.nbits; ++b) {
-              const float xi = cov[si][tb.bdim[b]][ri], xj = cov[sj][tb.bdim[b]][rj];
-              const bool pass = tb.bkind[b] == LVAE_CAT ? xi == xj : xi + xj == 2.f;
+#pragma unroll
+            for (int b = 0; b < kTabMaxBits; ++b) {
+              if (b >= nbits) break;
+              const float xi = cov[si][sbdim[b]][ri], xj = cov[sj][sbdim[b]][rj];
+              const bool pass = sbkind[b] == LVAE_CAT ? xi == xj : xi + xj == 2.f;
               bits += pass ? (kTabR << b) : 0;
             }
             double val = -0.5 * (double)acc[q];  // the S part (this slab's columns)
-            if (j >= J0 && j < J0 + kHbT)        // the K^-1 and alpha alpha^T parts: once, by the slab holding column j
+            if (jin)                             // the K^-1 and alpha alpha^T parts: once, by the slab holding column j
               val += 0.5 * ((double)T[si][ri * kHbTP + (j - J0)] - alr[si][ri] * alr[sj][rj]);
 #pragma unroll
-            for (int k = 0; k < kHbNear; ++k) {
-              if (k >= d.nnear) break;
-              const int kk = d.nslot[k], g = tb.cgrp[tb.pcomp[tb.porder[kk]]], gd = tb.gdim[g];
+            for (int k2 = 0; k2 < kHbNear; ++k2) {
+              if (k2 >= nnear) break;
+              const int gd = sngd[k2];
               const int dist = gd >= 0 ? (int)fabsf(cov[si][gd][ri] - cov[sj][gd][rj]) : 0;
-              nacc[k] += val * (double)tab[kk * tstride + bits + dist];
+              nacc[k2] += val * (double)tab[snoff[k2] + bits + dist];
             }
           }
         }
@@ -353,18 +409,19 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
   __syncthreads();
   if (tid < d.nbins) {
     int g = 0;
-    while (g + 1 < d.nbin && tid >= d.boff[g + 1]) ++g;
+    while (g + 1 < nbin && tid >= d.boff[g + 1]) ++g;
     const int b = tid - d.boff[g], nb = d.bn[g];
+    double* qrow = Qs + d.b2off[g] + b * nb;
     for (int m = 0; m < kHbT; ++m) {
-      const int bc = ws.pbin[(size_t)g * np_ + J0 + m];
-      if (bc != 255) Qs[d.b2off[g] + b * nb + bc] += H[tid * kHbT + m];
+      const int bc = cbin[g][m];
+      if (bc != 255) qrow[bc] += H[tid * kHbT + m];
     }
   }
   __syncthreads();
   double* out = ws.part + ((int64_t)l * nt + J) * kHbPart;
   for (int e = tid; e < d.nb2; e += 256) out[kHbBins2 + e] = Qs[e];
   // M_g = H_g V H_g^T on v_mfma_f64_16x16x4f64: 16 x 16 blocks dealt to the waves
-  for (int g = 0; g < d.nbin; ++g) {
+  for (int g = 0; g < nbin; ++g) {
     const int nb = d.bn[g], nb16 = (nb + 15) >> 4;
     for (int item = w; item < nb16 * nb16; item += 4) {
       const int bi = item / nb16, bj = item % nb16, li = lane & 15, lk = lane >> 4;
@@ -425,14 +482,23 @@ __global__ __launch_bounds__(256) void hb_final_kernel(GramTab tb, HbWs ws, int 
   if (tid < tb.n_params) sp[tid] = float(params[(int64_t)l * tb.n_params + tid]);
   if (tid < kBwdSlotsHb) raw[tid] = 0.0;
   const double* al = alpha + (int64_t)l * np_;
-  if (tid < d.nbins) {  // a[b]: thread b scans the points in order
+  {  // a[b]: thread b scans the points in order, 256 at a time through LDS (fixed order)
+    __shared__ double ach[256];
+    __shared__ uint8_t bch[kHbMaxBin][256];
     int g = 0;
-    while (g + 1 < d.nbin && tid >= d.boff[g + 1]) ++g;
+    while (tid < d.nbins && g + 1 < d.nbin && tid >= d.boff[g + 1]) ++g;
     const int b = tid - d.boff[g];
     double s = 0.0;
-    for (int i = 0; i < n; ++i)
-      if (ws.pbin[(size_t)g * np_ + i] == b) s += al[i];
-    av[tid] = s;
+    for (int i0 = 0; i0 < n; i0 += 256) {
+      __syncthreads();
+      ach[tid] = i0 + tid < n ? al[i0 + tid] : 0.0;
+      for (int q = 0; q < d.nbin; ++q) bch[q][tid] = i0 + tid < n ? ws.pbin[(size_t)q * np_ + i0 + tid] : 255;
+      __syncthreads();
+      if (tid < d.nbins)
+        for (int k = 0; k < 256; ++k)
+          if (bch[g][k] == b) s += ach[k];
+    }
+    if (tid < d.nbins) av[tid] = s;
   }
   __syncthreads();
   tab_build_bwd(tb, sp, ftab);
