@@ -141,9 +141,10 @@ __device__ inline void tab_build_fill(const GramTab& t, const float* __restrict_
 // adjoint tables: tab[(k * 2^B + b) * kTabR + m] for the k-th slot of porder: d k_r / d theta without
 // the constants kl_gram_bwd_reduce applies (scale: phi; RBF l: s phi m^2; PER l: s phi sin^2 u; PER p:
 // s phi m sin 2u), 0 when r's gates are not all in b
-__device__ inline void tab_build_bwd(const GramTab& t, const float* __restrict__ sp, float* __restrict__ tab) {
-  const int nb = 1 << t.nbits, np = t.pbeg[t.ng], ne = np * nb * kTabR;
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+// entry e of the derivative tables (slot k = e / (kTabR 2^nbits), gate bits b, distance m)
+__device__ inline float tab_bwd_entry(const GramTab& t, const float* __restrict__ sp, int e) {
+  const int nb = 1 << t.nbits;
+  {
     const int m = e % kTabR, b = (e / kTabR) % nb, k = e / (kTabR * nb);
     const int p = t.porder[k], r = t.pcomp[p], ty = t.ptype[p];
     float v = 0.f;
@@ -161,8 +162,13 @@ __device__ inline void tab_build_bwd(const GramTab& t, const float* __restrict__
         }
       }
     }
-    tab[e] = v;
+    return v;
   }
+}
+
+__device__ inline void tab_build_bwd(const GramTab& t, const float* __restrict__ sp, float* __restrict__ tab) {
+  const int ne = t.pbeg[t.ng] * (1 << t.nbits) * kTabR;
+  for (int e = threadIdx.x; e < ne; e += blockDim.x) tab[e] = tab_bwd_entry(t, sp, e);
 }
 
 }  // namespace lvae

@@ -26,8 +26,9 @@
 // Conditions (hb_plan_kernel, on the device; otherwise `on` = 0 and the S GEMM + table adjoint run as before):
 // the table path's (covariate flag 2); the Cat gate covariate of the widest range (> 4 values) is "big" (the id),
 // the other Cat gates span <= 16 values; its values non-decreasing over the points (runs contiguous) with runs of
-// <= 64 points; far binnings <= 4, with <= 128 bins
-// in all and sum nbins^2 <= 4096; <= 8 parameter slots on near components.
+// <= 64 points; far binnings <= 4, with <= 128 bins in all and sum nbins^2 <= 4096; <= 8 parameter slots on near
+// components; Bin gate values within 64 of their minimum, distance values within 65535 of theirs (the row keys);
+// on the host: the slab kernel's LDS fits (hb_slab_lds).
 #include "blkinv.hpp"
 #include "gram_tab.hpp"
 
@@ -41,9 +42,14 @@ constexpr int kHbSmall = 16;    // Cat gate covariates other than the big one sp
 constexpr int kHbSmallest = 4;  // the big covariate spans more than this many values
 constexpr int kHbNear = 8;      // parameter slots of the near components
 constexpr int kHbT = 64;        // row tile = column slab
-constexpr int kHbTP = 65;       // LDS pitch of a tile row (floats)
-constexpr int kHbQ = 16;        // covariate columns staged
-constexpr int kHbPart = 2 * kHbBins2 + kHbNear + 1;  // doubles per (dim, slab) partial record
+constexpr int kHbTP = 68;       // LDS pitch of a tile row (floats: 16-B aligned rows, 16 rows on distinct banks)
+// the per-(dim, slab) partial record (doubles): M [nb2], Q [nb2] (at kHbBins2), then the tail: the near slots' S
+// parts, tr S, the near slots' K^-1 - alpha alpha^T parts (hb_near_kernel, record of row tile I), a = Phi^T alpha
+constexpr int kHbNearS = 2 * kHbBins2;
+constexpr int kHbNearK = kHbNearS + kHbNear + 1;
+constexpr int kHbA = kHbNearK + kHbNear;
+constexpr int kHbTail = 2 * kHbNear + 1 + kHbBins;
+constexpr int kHbPart = 2 * kHbBins2 + kHbTail;
 
 struct HbDev {
   int on, nbin, big, nbins, nb2, nnear;
@@ -54,12 +60,16 @@ struct HbDev {
   int nslot[kHbNear];                                        // near parameter slots (GramTab porder index)
 };
 
+typedef unsigned hb_u32x4 __attribute__((ext_vector_type(4)));
+
 struct HbWs {
   HbDev* dev;
   uint8_t* pbin;  // [kHbMaxBin][np] local bin of every point (255: padding)
   int* rs;        // [np] start of the point's run of the big covariate
   int* re;        // [np] its end (exclusive)
   double* part;   // [L][np / 64][kHbPart] per-slab partials
+  float* tab;     // [L][kTabMaxBwdLds] the derivative tables per dim (hb_tab_kernel)
+  hb_u32x4* rkey;    // [np] per point: gate values (6 bits each, the big gate's 0), distance values (16 bits each)
   size_t bytes;
   HbWs(char* base, int np_, int L) {
     size_t off = 0;
@@ -73,6 +83,8 @@ struct HbWs {
     rs = (int*)take((size_t)np_ * sizeof(int));
     re = (int*)take((size_t)np_ * sizeof(int));
     part = (double*)take((size_t)L * (np_ / kHbT) * kHbPart * sizeof(double));
+    tab = (float*)take((size_t)L * kTabMaxBwdLds * sizeof(float));
+    rkey = (hb_u32x4*)take((size_t)np_ * sizeof(hb_u32x4));
     bytes = off;
   }
 };
@@ -189,6 +201,25 @@ __global__ __launch_bounds__(1024) void hb_plan_kernel(GramTab tb, const double*
     }
     ws.rs[i] = s;
     ws.re[i] = e;
+    hb_u32x4 key = {0u, 0u, 0u, 0u};  // the near pairs' key: gate values (not the big one) and distance values
+    if (i < n) {
+      for (int b = 0; b < tb.nbits; ++b) {
+        const int v = (int)x[(int64_t)i * ldx + tb.bdim[b]] - d.gmin[b];
+        if (b == d.big) continue;
+        if (v < 0 || v > 63) bad = 1;
+        key.x |= (unsigned)(v & 63) << (6 * b);
+      }
+      for (int g = 0; g < tb.ng; ++g) {
+        if (tb.gdim[g] < 0) continue;
+        const int v = (int)x[(int64_t)i * ldx + tb.gdim[g]] - d.wmin[g];
+        if (v < 0 || v > 65535) bad = 1;
+        const unsigned u = (unsigned)(v & 0xffff);
+        if (g == 0) key.y |= u;
+        else if (g == 1) key.y |= u << 16;
+        else key.z |= u;
+      }
+    }
+    ws.rkey[i] = key;
     for (int g = 0; g < kHbMaxBin; ++g) {
       int idx = 255;
       if (g < d.nbin && i < n) {
@@ -210,151 +241,296 @@ __global__ __launch_bounds__(1024) void hb_plan_kernel(GramTab tb, const double*
 }
 
 
+// the derivative tables of dim l once (entry per thread), for the slab and final kernels to copy
+__global__ __launch_bounds__(256) void hb_tab_kernel(GramTab tb, HbWs ws, const double* __restrict__ params) {
+  __shared__ float sp[64];
+  const int tid = threadIdx.x, l = blockIdx.y, e = blockIdx.x * 256 + tid;
+  if (!ws.dev->on) return;  // (uniform)
+  if (tid < tb.n_params) sp[tid] = float(params[(int64_t)l * tb.n_params + tid]);
+  __syncthreads();
+  if (e < tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR) ws.tab[(int64_t)l * kTabMaxBwdLds + e] = tab_bwd_entry(tb, sp, e);
+}
+
+// a pair's code inside one run of the big covariate, from the two points' keys (hb_plan_kernel): the gate bits
+// and the distance per distance group, [bits | d_0 << 8 | d_1 << 16 | d_2 << 24]
+__device__ inline unsigned hb_pair_code(const GramTab& tb, const int* gmin, hb_u32x4 ki, hb_u32x4 kj) {
+  unsigned c = 0;
+#pragma unroll
+  for (int b = 0; b < kTabMaxBits; ++b) {
+    if (b >= tb.nbits) break;
+    const int vi = (int)((ki.x >> (6 * b)) & 63u), vj = (int)((kj.x >> (6 * b)) & 63u);
+    const bool pass = tb.bkind[b] == LVAE_CAT ? vi == vj : vi + vj + 2 * gmin[b] == 2;
+    c |= pass ? (1u << b) : 0u;
+  }
+  const unsigned di[3] = {ki.y & 0xffffu, ki.y >> 16, ki.z & 0xffffu}, dj[3] = {kj.y & 0xffffu, kj.y >> 16, kj.z & 0xffffu};
+#pragma unroll
+  for (int g = 0; g < kTabMaxG; ++g) {
+    if (g >= tb.ng) break;
+    const unsigned dist = di[g] > dj[g] ? di[g] - dj[g] : dj[g] - di[g];  // (0 without a distance dim)
+    c |= (dist < (unsigned)kTabD ? dist : (unsigned)kTabD) << (8 * (g + 1));
+  }
+  return c;
+}
+
+// the near slots' tables of dim l into LDS (slot after slot; hb_tab_kernel's) and each slot's distance group
+__device__ inline void hb_near_tables(const GramTab& tb, const HbDev& d, const float* __restrict__ gt, int tstride,
+                                      float* __restrict__ tab, int* __restrict__ sgrp) {
+  const int tid = threadIdx.x;
+  if (tid < d.nnear) sgrp[tid] = tb.cgrp[tb.pcomp[tb.porder[d.nslot[tid]]]];
+  for (int e = tid; e < d.nnear * tstride; e += blockDim.x) tab[e] = gt[d.nslot[e / tstride] * tstride + e % tstride];
+}
+
+// a pair's table entry in near slot k (table base tk = k * tstride)
+__device__ inline float hb_near_d(const float* tab, int tk, unsigned code, int grp) {
+  return tab[tk + (int)(code & 0xffu) * kTabR + (int)((code >> (8 * (grp + 1))) & 0xffu)];
+}
+
+// ------------------------------------------------------------------------------------------
+// the near runs' K^-1 and alpha alpha^T parts (no S): workgroup (I, l) takes the pairs of row tile I,
+// record (l, I) gets sum over them of (K^-1_ij - alpha_i alpha_j) / 2 * D_k(i, j) per near slot k
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n, int np_,
+                                                      const float* __restrict__ Kinv, const double* __restrict__ alpha) {
+  __shared__ HbDev d;
+  __shared__ int sgrp[kHbNear];
+  __shared__ double red[4][kHbNear];
+  extern __shared__ float ntab[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, I = blockIdx.x, l = blockIdx.y, I0 = I * kHbT;
+  if (tid == 0) d = *ws.dev;
+  __syncthreads();
+  if (!d.on) return;  // (uniform)
+  const int tstride = (1 << tb.nbits) * kTabR, nnear = d.nnear;
+  hb_near_tables(tb, d, ws.tab + (int64_t)l * kTabMaxBwdLds, tstride, ntab, sgrp);
+  __syncthreads();
+  const float* K = Kinv + (int64_t)l * np_ * np_;
+  const double* al = alpha + (int64_t)l * np_;
+  double acc[kHbNear];
+#pragma unroll
+  for (int k = 0; k < kHbNear; ++k) acc[k] = 0.0;
+  if (d.big >= 0) {
+    for (int e = tid; e < kHbT * kHbRun; e += 256) {
+      const int i = I0 + e / kHbRun, jj = e % kHbRun;
+      if (i >= n) continue;
+      const int s = ws.rs[i], len = ws.re[i] - s;
+      if (jj >= len) continue;
+      const int j = s + jj;
+      const unsigned c = hb_pair_code(tb, d.gmin, ws.rkey[i], ws.rkey[j]);
+      const double val = 0.5 * ((double)K[(int64_t)i * np_ + j] - al[i] * al[j]);
+#pragma unroll
+      for (int k = 0; k < kHbNear; ++k)
+        if (k < nnear) acc[k] += val * (double)hb_near_d(ntab, k * tstride, c, sgrp[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kHbNear; ++k) {
+    const double sk = wave_sum(acc[k]);
+    if (lane == 0) red[w][k] = sk;
+  }
+  __syncthreads();
+  if (tid < kHbNear)
+    ws.part[((int64_t)l * (np_ / kHbT) + I) * kHbPart + kHbNearK + tid] =
+        ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+}
+
 // ------------------------------------------------------------------------------------------
 // the slab pass: workgroup (J, l) streams column slab J (64 columns) of the full symmetric K^-1 of dim l, 64-row
 // tile by tile, and writes its partial record: M_g = H_g V H_g^T, Q_g = H_g Phi_g (the slab's columns), the near
-// runs' parts per near slot and the slab's part of tr S.
+// runs' S parts per near slot, the slab's part of tr S and of a = Phi^T alpha.
+//
+//   H_g += Phi_g(tile)^T K^-1(tile, slab): a one-hot GEMM per 32-bin block and 32-column block on
+//     v_mfma_f32_32x32x16_bf16, K^-1 split exactly into three bf16 pieces (hi + mid + lo = the fp32 value), the
+//     one-hot operand exact: fp32 sums of the tile's 64 rows, then fp64 adds into H (each entry owned by one lane)
+//   near runs ending in the tile: 16 x 16 blocks of X V X^T on v_mfma_f32_16x16x4f32, contracted with the near
+//     slots' tables through the pair codes (hb_pair_code, from the rows' keys)
+//   tr S part: from the registers the tile arrives in
+// Tiles arrive two ahead in registers (two prefetch sets, the loop unrolled by two).
 // ------------------------------------------------------------------------------------------
 __device__ inline int hb_row_slot(int row) { return (row >> 6) & 1; }
 
-// an LDS fp64 add whose return value is not used (ds_add_f64): a wave's adds to one address apply in program order
-__device__ inline void hb_lds_add(double* p, double v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
+typedef float hb_f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 hb_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kHbBlk = 7;  // 32-bin blocks over the binnings (sum ceil(nb_g / 32) with sum nb_g <= 128, <= 4 binnings)
+
+constexpr int kHbSlabThreads = 512, kHbSlabWaves = kHbSlabThreads / 64;  // (2 waves per SIMD: latency hiding)
+constexpr int kHbPk = kHbT * kHbT / 4 / kHbSlabThreads;                    // float4 per thread per tile
+
+struct HbPre {        // one tile's prefetch
+  hb_f32x4 pk[kHbPk]; // K^-1 rows (e >> 4), columns 4 (e & 15) .. + 3, e = tid + kHbSlabThreads u
+  int pbn;            // wave w < nbin: bin of row lane in binning w
+  int pre_, prs;      // wave 0: run end / start of row lane
+  hb_u32x4 key;       // wave 0: key of row lane
+};
+
+// the three bf16 pieces of 8 fp32 values (truncation: t = hi + mid + lo exactly)
+__device__ inline void hb_split8(const float* t, hb_bf16x8& hi, hb_bf16x8& mid, hb_bf16x8& lo) {
+  hb_u32x4 h, m, o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = t[2 * k], b = t[2 * k + 1];
+    const float ah = __uint_as_float(__float_as_uint(a) & 0xffff0000u), bh = __uint_as_float(__float_as_uint(b) & 0xffff0000u);
+    const float a1 = a - ah, b1 = b - bh;
+    const float am = __uint_as_float(__float_as_uint(a1) & 0xffff0000u), bm = __uint_as_float(__float_as_uint(b1) & 0xffff0000u);
+    const float a2 = a1 - am, b2 = b1 - bm;
+    h[k] = __builtin_amdgcn_perm(__float_as_uint(bh), __float_as_uint(ah), 0x07060302u);
+    m[k] = __builtin_amdgcn_perm(__float_as_uint(bm), __float_as_uint(am), 0x07060302u);
+    o[k] = __builtin_amdgcn_perm(__float_as_uint(b2), __float_as_uint(a2), 0x07060302u);
+  }
+  hi = __builtin_bit_cast(hb_bf16x8, h);
+  mid = __builtin_bit_cast(hb_bf16x8, m);
+  lo = __builtin_bit_cast(hb_bf16x8, o);
 }
 
-constexpr int kHbPre = (kHbQ * kHbT + 255) / 256;  // covariate values a thread prefetches per tile
-typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const double* __restrict__ x, int ldx,
-                                                      int n, int np_, int qs, const double* __restrict__ params,
+__global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbWs ws, int n, int np_,
                                                       const float* __restrict__ Kinv, const float* __restrict__ vv,
-                                                      const double* __restrict__ alpha) {
+                                                      const double* __restrict__ alpha, int dbg) {
   __shared__ HbDev d;
   __shared__ __attribute__((aligned(16))) float T[2][kHbT * kHbTP];  // the row tiles of the window (slot = (row / 64) & 1)
-  __shared__ float cov[2][kHbQ][kHbT];          // their covariates
-  __shared__ double alr[2][kHbT];               // their alpha
-  __shared__ float vs[kHbT];                    // v of the slab's columns
-  __shared__ float sp[64];
-  __shared__ int runs[kHbT], runl[kHbT], nrun;
-  __shared__ int sbdim[kTabMaxBits], sbkind[kTabMaxBits];  // the gates (LDS copies: no kernarg loads in loops)
-  __shared__ int snoff[kHbNear], sngd[kHbNear];            // near slot: its table offset, its distance dim
+  __shared__ __attribute__((aligned(8))) uint8_t rbin[kHbMaxBin][kHbT];  // bins of the current tile's rows
   __shared__ uint8_t cbin[kHbMaxBin][kHbT];     // bins of the slab's columns
-  __shared__ double red[4][kHbNear + 1];
-  extern __shared__ double hdyn[];              // H [kHbBins][64] (fp64), then the derivative tables (fp32)
+  __shared__ float vs[kHbT];                    // v of the slab's columns
+  __shared__ double acol[kHbT];                 // alpha of the slab's columns
+  __shared__ int runs[kHbT], runl[kHbT], nrun;
+  __shared__ hb_u32x4 rk[2][kHbT];                 // the window's row keys
+  __shared__ int sgrp[kHbNear];
+  __shared__ int sbg[kHbBlk], sbb[kHbBlk], nbk;  // 32-bin blocks: binning, block index
+  __shared__ double red[kHbSlabWaves][kHbNear + 1];
+  extern __shared__ double hdyn[];              // H [kHbBins][64] (fp64), then the near slots' tables (fp32)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, J = blockIdx.x, l = blockIdx.y, J0 = J * kHbT;
   if (tid == 0) d = *ws.dev;
   __syncthreads();
   if (!d.on) return;  // (uniform)
   double* H = hdyn;
   float* tab = reinterpret_cast<float*>(hdyn + kHbBins * kHbT);
-  const int tstride = (1 << tb.nbits) * kTabR, nbits = tb.nbits;
-  if (tid < tb.n_params) sp[tid] = float(params[(int64_t)l * tb.n_params + tid]);
-  for (int e = tid; e < d.nbins * kHbT; e += 256) H[e] = 0.0;
-  if (tid < kHbT) vs[tid] = vv[(int64_t)l * np_ + J0 + tid];
-  if (tid < kTabMaxBits) {
-    sbdim[tid] = tid < nbits ? tb.bdim[tid] : 0;
-    sbkind[tid] = tid < nbits ? tb.bkind[tid] : 0;
+  const int tstride = (1 << tb.nbits) * kTabR;
+  for (int e = tid; e < d.nbins * kHbT; e += kHbSlabThreads) H[e] = 0.0;
+  if (tid < kHbT) {
+    vs[tid] = vv[(int64_t)l * np_ + J0 + tid];
+    acol[tid] = alpha[(int64_t)l * np_ + J0 + tid];
   }
-  if (tid < d.nnear) {
-    const int kk = d.nslot[tid];
-    snoff[tid] = kk * tstride;
-    sngd[tid] = tb.gdim[tb.cgrp[tb.pcomp[tb.porder[kk]]]];
+  for (int e = tid; e < d.nbin * kHbT; e += kHbSlabThreads) cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
+  hb_near_tables(tb, d, ws.tab + (int64_t)l * kTabMaxBwdLds, tstride, tab, sgrp);
+  if (tid == 0) {  // the 32-bin blocks of the binnings in order
+    int t = 0;
+    for (int g = 0; g < d.nbin; ++g)
+      for (int bb = 0; bb * 32 < d.bn[g] && t < kHbBlk; ++bb, ++t) {
+        sbg[t] = g;
+        sbb[t] = bb;
+      }
+    nbk = t;
   }
-  for (int e = tid; e < d.nbin * kHbT; e += 256) cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
   __syncthreads();
-  tab_build_bwd(tb, sp, tab);
   const float* K = Kinv + (int64_t)l * np_ * np_;
-  const double* al = alpha + (int64_t)l * np_;
   const int nbin = d.nbin, nnear = d.nnear, bigon = d.big >= 0;
-  const int myoff = w < nbin ? d.boff[w] : 0;
+  // this wave's H work: column block cb = w & 1, the 32-bin blocks t = w >> 1 (mod kHbSlabWaves / 2)
+  const int cb = w & 1, nblk = nbk;
+  int ngrp[kHbNear];
+#pragma unroll
+  for (int k = 0; k < kHbNear; ++k) ngrp[k] = k < nnear ? sgrp[k] : 0;
   double nacc[kHbNear];
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) nacc[k] = 0.0;
   double tS = 0.0;
+  float vreg[4];  // v of this thread's 4 columns (the same in every tile)
+#pragma unroll
+  for (int c = 0; c < 4; ++c) vreg[c] = vs[(tid & 15) * 4 + c];
   const int nt = np_ / kHbT;
-  // software pipeline: tile I + 1's K^-1 rows, covariates, alpha, bins and run ends in registers during tile I
-  hb_f32x4 pk[4];
-  float pc[kHbPre];
-  double pa = 0.0;
-  int pbn = 255, pre_ = -1, prs = -1;
-  auto fetch = [&](int I) {
+
+  auto fetch = [&](int I, HbPre& p) {
     const int I0 = I * kHbT;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + 256 * u, r = e >> 4, c4 = (e & 15) * 4;
-      pk[u] = __builtin_nontemporal_load(reinterpret_cast<const hb_f32x4*>(K + (int64_t)(I0 + r) * np_ + J0 + c4));
+    for (int u = 0; u < kHbPk; ++u) {
+      const int e = tid + kHbSlabThreads * u, r = e >> 4, c4 = (e & 15) * 4;
+      p.pk[u] = __builtin_nontemporal_load(reinterpret_cast<const hb_f32x4*>(K + (int64_t)(I0 + r) * np_ + J0 + c4));
     }
-#pragma unroll
-    for (int u = 0; u < kHbPre; ++u) {
-      const int e = tid + 256 * u, q = e / kHbT, r = e % kHbT;
-      pc[u] = (q < qs && I0 + r < n) ? float(x[(int64_t)(I0 + r) * ldx + q]) : 0.f;
-    }
-    if (tid < kHbT) pa = al[I0 + tid];
-    pbn = w < nbin ? (int)ws.pbin[(size_t)w * np_ + I0 + lane] : 255;
-    if (w == 0 && bigon) {
-      pre_ = ws.re[I0 + lane];
-      prs = ws.rs[I0 + lane];
-    }
+    // (every load unconditional: no branch around loads, so the waits before a tile's use count exactly the
+    // newer tile's loads and leave them in flight)
+    p.pbn = (int)ws.pbin[(size_t)(w < nbin ? w : 0) * np_ + I0 + lane];  // (used by waves w < nbin only)
+    p.pre_ = ws.re[I0 + lane];
+    p.prs = ws.rs[I0 + lane];
+    p.key = ws.rkey[I0 + lane];
   };
-  fetch(0);
-  for (int I = 0; I < nt; ++I) {
-    const int I0 = I * kHbT, sl = I & 1;
+
+  auto body = [&](int I, const int sl, HbPre& p) {
+    const int I0 = I * kHbT;
+    float ts = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + 256 * u, r = e >> 4, c4 = (e & 15) * 4;
-      float* t = &T[sl][r * kHbTP + c4];
-      t[0] = pk[u][0];
-      t[1] = pk[u][1];
-      t[2] = pk[u][2];
-      t[3] = pk[u][3];
-    }
+    for (int u = 0; u < kHbPk; ++u) {
+      const int e = tid + kHbSlabThreads * u, r = e >> 4, c4 = (e & 15) * 4;
+      *reinterpret_cast<hb_f32x4*>(&T[sl][r * kHbTP + c4]) = p.pk[u];
 #pragma unroll
-    for (int u = 0; u < kHbPre; ++u) {
-      const int e = tid + 256 * u, q = e / kHbT, r = e % kHbT;
-      if (q < kHbQ) cov[sl][q][r] = pc[u];
+      for (int c = 0; c < 4; ++c) ts += p.pk[u][c] * p.pk[u][c] * vreg[c];  // tr S part: sum_m v_m (K^-1_im)^2
     }
-    if (tid < kHbT) alr[sl][tid] = pa;
-    const int bn = pbn;  // (wave w < nbin: the bin of row lane in binning w)
-    if (w == 0) {        // the runs of the big covariate ending in this tile
+    tS += (double)ts;
+    if (w < nbin) rbin[w][lane] = (uint8_t)p.pbn;
+    if (w == 0) {  // the runs of the big covariate ending in this tile, the rows' keys
       const int i = I0 + lane;
-      const bool last = bigon && i < n && pre_ == i + 1;
+      rk[sl][lane] = p.key;
+      const bool last = bigon && i < n && p.pre_ == i + 1;
       const unsigned long long m = __ballot(last);
       if (last) {
         const int k = __popcll(m & ((1ull << lane) - 1));
-        runs[k] = prs;
-        runl[k] = i + 1 - prs;
+        runs[k] = p.prs;
+        runl[k] = i + 1 - p.prs;
       }
       if (lane == 0) nrun = __popcll(m);
     }
     __syncthreads();
-    if (I + 1 < nt) fetch(I + 1);  // (in flight under this tile's work)
-    // H_w[bin(i)][m] += K^-1_im: wave w owns binning w, lane m column m; the rows in order (ds_add_f64 without
-    // return: no dependent latency, program order per address -> a fixed summation order)
-    if (w < nbin) {
-      const float* tr = &T[sl][lane];
-#pragma unroll 16
-      for (int r = 0; r < kHbT; ++r) {
-        const int b = __builtin_amdgcn_readlane(bn, r);
-        if (b != 255) hb_lds_add(&H[(myoff + b) * kHbT + lane], (double)tr[r * kHbTP]);
-      }
-    }
-    {  // the slab's part of tr S = sum_m v_m sum_i (K^-1_im)^2: wave w, rows = w (mod 4)
-      float ts = 0.f;
+    fetch(I + 2 < nt ? I + 2 : nt - 1, p);  // (in flight under the next two tiles' work; the last two: a dummy)
+    if (!(dbg & 1) && (w >> 1) < nblk) {  // (waves without a block skip the B operands too)
+      // B operands: rows 16 ks + 8 (lane >> 5) + 0..7 of column 32 cb + (lane & 31), three bf16 pieces
+      hb_bf16x8 bh[4], bm[4], bl[4];
+      const int col = 32 * cb + (lane & 31), hh = lane >> 5;
 #pragma unroll
-      for (int r = w; r < kHbT; r += 4) {
-        const float t = T[sl][r * kHbTP + lane];
-        ts += t * t;
+      for (int ks = 0; ks < 4; ++ks) {
+        float t8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t8[k] = T[sl][(16 * ks + 8 * hh + k) * kHbTP + col];
+        hb_split8(t8, bh[ks], bm[ks], bl[ks]);
       }
-      tS += (double)ts * (double)vs[lane];
+      for (int q = w >> 1; q < nblk; q += kHbSlabWaves / 2) {  // this wave's blocks
+        const int g = sbg[q], b0 = 32 * sbb[q], nb = d.bn[g];
+        const int mybin = b0 + (lane & 31);
+        hb_f32x16 acc = {};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          // A operand (one-hot): [bin b0 + (lane & 31)][rows 16 ks + 8 hh + 0..7]
+          const uint2 rb = *reinterpret_cast<const uint2*>(&rbin[g][16 * ks + 8 * hh]);
+          hb_u32x4 a;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const unsigned wd = k < 2 ? rb.x : rb.y, sh = 16 * (k & 1);
+            const unsigned lo_ = ((wd >> sh) & 0xffu) == (unsigned)mybin ? 0x3f80u : 0u;
+            const unsigned hi_ = ((wd >> (sh + 8)) & 0xffu) == (unsigned)mybin ? 0x3f800000u : 0u;
+            a[k] = lo_ | hi_;
+          }
+          const hb_bf16x8 av = __builtin_bit_cast(hb_bf16x8, a);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl[ks], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bm[ks], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh[ks], acc, 0, 0, 0);
+        }
+        // acc[e]: bin b0 + (e & 3) + 8 (e >> 2) + 4 hh, column col
+        double* hc = H + (int64_t)d.boff[g] * kHbT + col;
+        double hv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          hv[e] = b < nb ? hc[b * kHbT] : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (b < nb) hc[b * kHbT] = hv[e] + (double)acc[e];
+        }
+      }
     }
-    // near runs ending in this tile: 16 x 16 blocks (bi, bj) of X V X^T on v_mfma_f32_16x16x4f32, block items dealt
-    // to the waves; each lane's 4 pairs contracted at once with the near slots' tables
-    {
+    // near runs ending in this tile: 16 x 16 blocks (bi, bj) of X V X^T, block items dealt to the waves
+    if (!(dbg & 2)) {
       int item = w;
       const int nr = nrun;
       for (int k = 0; k < nr; ++k) {
         const int s0 = runs[k], len = runl[k], nb16 = (len + 15) >> 4;
-        for (; item < nb16 * nb16; item += 4) {
+        for (; item < nb16 * nb16; item += kHbSlabWaves) {
           const int bi = item / nb16, bj = item % nb16;
           const int li = lane & 15, lk = lane >> 4;
           const int ra = s0 + 16 * bi + li, rb = s0 + 16 * bj + li;  // the lane's A row, B column
@@ -362,68 +538,65 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
           const float* ta = &T[hb_row_slot(ra)][(ra & 63) * kHbTP];
           const float* tb2 = &T[hb_row_slot(rb)][(rb & 63) * kHbTP];
           bi_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+#pragma unroll
           for (int s4 = 0; s4 < kHbT; s4 += 4) {
             const int m = s4 + lk;
             const float a = va ? ta[m] * vs[m] : 0.f;
             const float b = vb ? tb2[m] : 0.f;
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
           }
-          // lane: C[4 lk + q][li] -> pair (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li)
-          const int j = s0 + 16 * bj + li, sj = hb_row_slot(j), rj = j & 63;
-          const bool jin = j >= J0 && j < J0 + kHbT;
+          // the lane's 4 pairs (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li)
+          const hb_u32x4 kj = rk[hb_row_slot(rb)][rb & 63];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int ioff = 16 * bi + 4 * lk + q, i = s0 + ioff;
             if (ioff >= len || !vb) continue;
-            const int si = hb_row_slot(i), ri = i & 63;
-            // the pair's gate bits (tab_bits on one element)
-            int bits = 0;
-#pragma unroll
-            for (int b = 0; b < kTabMaxBits; ++b) {
-              if (b >= nbits) break;
-              const float xi = cov[si][sbdim[b]][ri], xj = cov[sj][sbdim[b]][rj];
-              const bool pass = sbkind[b] == LVAE_CAT ? xi == xj : xi + xj == 2.f;
-              bits += pass ? (kTabR << b) : 0;
-            }
-            double val = -0.5 * (double)acc[q];  // the S part (this slab's columns)
-            if (jin)                             // the K^-1 and alpha alpha^T parts: once, by the slab holding column j
-              val += 0.5 * ((double)T[si][ri * kHbTP + (j - J0)] - alr[si][ri] * alr[sj][rj]);
+            const unsigned c = hb_pair_code(tb, d.gmin, rk[hb_row_slot(i)][i & 63], kj);
 #pragma unroll
             for (int k2 = 0; k2 < kHbNear; ++k2) {
               if (k2 >= nnear) break;
-              const int gd = sngd[k2];
-              const int dist = gd >= 0 ? (int)fabsf(cov[si][gd][ri] - cov[sj][gd][rj]) : 0;
-              nacc[k2] += val * (double)tab[snoff[k2] + bits + dist];
+              nacc[k2] += (double)acc[q] * (double)hb_near_d(tab, k2 * tstride, c, ngrp[k2]);
             }
           }
         }
         item -= nb16 * nb16;  // (this wave's next item index in the following run's block list)
       }
     }
-    __syncthreads();  // every reader of slot sl done before tile I + 2 overwrites it (and the run list)
+    __syncthreads();  // every reader of slot sl done before tile I + 2 overwrites it (and the run list, the bins)
+  };
+
+  HbPre pa, pb;
+  fetch(0, pa);
+  fetch(1, pb);  // (nt >= 4)
+  for (int I = 0; I < nt; I += 2) {  // (nt even: np % 256 == 0)
+    body(I, 0, pa);
+    body(I + 1, 1, pb);
   }
-  // Q_g[b][b'] = sum over the slab's columns m in bin b' of H_g[b][m]: thread (g, b) owns row b (LDS scratch = T)
+  // Q_g[b][b'] = sum over the slab's columns m in bin b' of H_g[b][m]: thread (g, b) owns row b (LDS scratch = T);
+  // a part: thread (g, b) sums alpha over the slab's columns in bin b
   double* Qs = reinterpret_cast<double*>(&T[0][0]);
-  for (int e = tid; e < d.nb2; e += 256) Qs[e] = 0.0;
+  for (int e = tid; e < d.nb2; e += kHbSlabThreads) Qs[e] = 0.0;
   __syncthreads();
+  double* out = ws.part + ((int64_t)l * nt + J) * kHbPart;
   if (tid < d.nbins) {
     int g = 0;
     while (g + 1 < nbin && tid >= d.boff[g + 1]) ++g;
     const int b = tid - d.boff[g], nb = d.bn[g];
     double* qrow = Qs + d.b2off[g] + b * nb;
+    double as = 0.0;
     for (int m = 0; m < kHbT; ++m) {
       const int bc = cbin[g][m];
       if (bc != 255) qrow[bc] += H[tid * kHbT + m];
+      if (bc == b) as += acol[m];
     }
+    out[kHbA + tid] = as;
   }
   __syncthreads();
-  double* out = ws.part + ((int64_t)l * nt + J) * kHbPart;
-  for (int e = tid; e < d.nb2; e += 256) out[kHbBins2 + e] = Qs[e];
+  for (int e = tid; e < d.nb2; e += kHbSlabThreads) out[kHbBins2 + e] = Qs[e];
   // M_g = H_g V H_g^T on v_mfma_f64_16x16x4f64: 16 x 16 blocks dealt to the waves
   for (int g = 0; g < nbin; ++g) {
     const int nb = d.bn[g], nb16 = (nb + 15) >> 4;
-    for (int item = w; item < nb16 * nb16; item += 4) {
+    for (int item = w; item < nb16 * nb16; item += kHbSlabWaves) {
       const int bi = item / nb16, bj = item % nb16, li = lane & 15, lk = lane >> 4;
       const int ba = 16 * bi + li, bb = 16 * bj + li;
       const double* ha = H + (int64_t)(d.boff[g] + (ba < nb ? ba : 0)) * kHbT;
@@ -443,7 +616,7 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
       }
     }
   }
-  // the near slots' and tr S's parts: the waves' sums in a fixed order
+  // the near slots' S parts and tr S's part: the waves' sums in a fixed order
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) {
     const double sk = wave_sum(nacc[k]);
@@ -454,7 +627,12 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
     if (lane == 0) red[w][kHbNear] = st;
   }
   __syncthreads();
-  if (tid <= kHbNear) out[2 * kHbBins2 + tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if (tid <= kHbNear) {
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < kHbSlabWaves; ++u) t += red[u][tid];
+    out[kHbNearS + tid] = t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -463,59 +641,47 @@ __global__ __launch_bounds__(256) void hb_slab_kernel(GramTab tb, HbWs ws, const
 // ------------------------------------------------------------------------------------------
 constexpr int kNoiseSlotHb = 64, kBwdSlotsHb = 65;  // (gram.hip's kNoiseSlot / kBwdSlots)
 
+// the slab records summed over J in a fixed order, in place into slab 0's record: thread (e, l) owns entry e
+__global__ __launch_bounds__(256) void hb_sum_kernel(HbWs ws, int np_) {
+  const int i = blockIdx.x * 256 + threadIdx.x, l = blockIdx.y, nt = np_ / kHbT, nb2 = ws.dev->nb2;
+  if (!ws.dev->on || i >= 2 * nb2 + kHbTail) return;  // (the written entries only: M, Q, the tail)
+  const int e = i < nb2 ? i : i < 2 * nb2 ? kHbBins2 + i - nb2 : 2 * kHbBins2 + i - 2 * nb2;
+  double* pl = ws.part + (int64_t)l * nt * kHbPart + e;
+  double s = 0.0;
+#pragma unroll 16
+  for (int J = 0; J < nt; ++J) s += pl[(int64_t)J * kHbPart];
+  pl[0] = s;
+}
+
 __global__ __launch_bounds__(256) void hb_final_kernel(GramTab tb, HbWs ws, int n, int np_,
-                                                       const double* __restrict__ params,
                                                        const double* __restrict__ alpha,
                                                        const double* __restrict__ kdiag, double* __restrict__ part,
-                                                       int G) {
+                                                       int G, int dbg) {
   __shared__ HbDev d;
-  __shared__ float sp[64];
   __shared__ double Gb[kHbBins2];   // (Q - M - a a^T) / 2 per far bin pair
-  __shared__ double av[kHbBins];    // a = Phi^T alpha
   __shared__ double raw[kBwdSlotsHb];
   __shared__ double red[4];
+  __shared__ double nz;
   extern __shared__ float ftab[];   // the derivative tables
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l = blockIdx.x, nt = np_ / kHbT;
   if (tid == 0) d = *ws.dev;
   __syncthreads();
   if (!d.on) return;  // (uniform)
-  if (tid < tb.n_params) sp[tid] = float(params[(int64_t)l * tb.n_params + tid]);
   if (tid < kBwdSlotsHb) raw[tid] = 0.0;
   const double* al = alpha + (int64_t)l * np_;
-  {  // a[b]: thread b scans the points in order, 256 at a time through LDS (fixed order)
-    __shared__ double ach[256];
-    __shared__ uint8_t bch[kHbMaxBin][256];
-    int g = 0;
-    while (tid < d.nbins && g + 1 < d.nbin && tid >= d.boff[g + 1]) ++g;
-    const int b = tid - d.boff[g];
-    double s = 0.0;
-    for (int i0 = 0; i0 < n; i0 += 256) {
-      __syncthreads();
-      ach[tid] = i0 + tid < n ? al[i0 + tid] : 0.0;
-      for (int q = 0; q < d.nbin; ++q) bch[q][tid] = i0 + tid < n ? ws.pbin[(size_t)q * np_ + i0 + tid] : 255;
-      __syncthreads();
-      if (tid < d.nbins)
-        for (int k = 0; k < 256; ++k)
-          if (bch[g][k] == b) s += ach[k];
-    }
-    if (tid < d.nbins) av[tid] = s;
+  const double* pl = ws.part + (int64_t)l * nt * kHbPart;  // (hb_sum_kernel's sums)
+  {
+    const float* gt = ws.tab + (int64_t)l * kTabMaxBwdLds;
+    for (int e = tid; e < tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR; e += 256) ftab[e] = gt[e];
   }
-  __syncthreads();
-  tab_build_bwd(tb, sp, ftab);
-  const double* pl = ws.part + (int64_t)l * nt * kHbPart;
   for (int e = tid; e < d.nb2; e += 256) {
     int g = 0;
     while (g + 1 < d.nbin && e >= d.b2off[g + 1]) ++g;
     const int nb = d.bn[g], b = (e - d.b2off[g]) / nb, bc = (e - d.b2off[g]) % nb;
-    double m = 0.0, q = 0.0;
-    for (int J = 0; J < nt; ++J) {
-      m += pl[(int64_t)J * kHbPart + e];
-      q += pl[(int64_t)J * kHbPart + kHbBins2 + e];
-    }
-    Gb[e] = 0.5 * (q - m - av[d.boff[g] + b] * av[d.boff[g] + bc]);
+    const double m = pl[e], q = pl[kHbBins2 + e];
+    Gb[e] = 0.5 * (q - m - pl[kHbA + d.boff[g] + b] * pl[kHbA + d.boff[g] + bc]);
   }
-  // tr G = (sum diag K^-1 - tr S - alpha^T alpha) / 2 (the noise slot): the first two sums here
-  __shared__ double nz;
+  // tr G = (sum diag K^-1 - tr S - alpha^T alpha) / 2 (the noise slot)
   {
     double s = 0.0;
     for (int i = tid; i < n; i += 256) s += kdiag[(int64_t)l * np_ + i] - al[i] * al[i];
@@ -524,19 +690,13 @@ __global__ __launch_bounds__(256) void hb_final_kernel(GramTab tb, HbWs ws, int 
   }
   __syncthreads();
   if (tid == 0) {
-    double ts = 0.0;
-    for (int J = 0; J < nt; ++J) ts += pl[(int64_t)J * kHbPart + 2 * kHbBins2 + kHbNear];
-    nz = 0.5 * ((((red[0] + red[1]) + red[2]) + red[3]) - ts);
-    // near slots: the slabs' parts in order
-    for (int k = 0; k < d.nnear; ++k) {
-      double sk = 0.0;
-      for (int J = 0; J < nt; ++J) sk += pl[(int64_t)J * kHbPart + 2 * kHbBins2 + k];
-      raw[tb.porder[d.nslot[k]]] = sk;
-    }
+    nz = 0.5 * ((((red[0] + red[1]) + red[2]) + red[3]) - pl[kHbNearS + kHbNear]);
+    for (int k = 0; k < d.nnear; ++k)  // near slots: -S part / 2 + the K^-1 - alpha alpha^T part
+      raw[tb.porder[d.nslot[k]]] = -0.5 * pl[kHbNearS + k] + pl[kHbNearK + k];
   }
   const int tstride = (1 << tb.nbits) * kTabR;
   // far slots: sum over the bin pairs of the slot's binning
-  for (int k = 0; k < tb.pbeg[tb.ng]; ++k) {
+  for (int k = 0; k < ((dbg & 16) ? 0 : tb.pbeg[tb.ng]); ++k) {
     const int p = tb.porder[k], r = tb.pcomp[p], g = d.cbin[r];
     if (g < 0) continue;  // (uniform) near
     const int nb = d.bn[g], grp = d.bgrp[g], W = grp >= 0 ? d.wrng[grp] : 1;
@@ -547,8 +707,9 @@ __global__ __launch_bounds__(256) void hb_final_kernel(GramTab tb, HbWs ws, int 
       b /= W;
       bc /= W;
       int bits = 0;
-      for (int q = tb.nbits - 1; q >= 0; --q) {  // the mask's gate values, the last bit fastest (hb_plan_kernel)
-        if (!((d.bmask[g] >> q) & 1)) continue;
+#pragma unroll
+      for (int q = kTabMaxBits - 1; q >= 0; --q) {  // the mask's gate values, the last bit fastest (hb_plan_kernel)
+        if (q >= tb.nbits || !((d.bmask[g] >> q) & 1)) continue;
         const int v1 = b % d.grng[q] + d.gmin[q], v2 = bc % d.grng[q] + d.gmin[q];
         b /= d.grng[q];
         bc /= d.grng[q];
@@ -575,21 +736,40 @@ __global__ __launch_bounds__(256) void hb_final_kernel(GramTab tb, HbWs ws, int 
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
+static int hb_dbg() {  // (timing only: LVAE_HB_DBG bits skip the slab pass's parts -- wrong results)
+  const char* v = getenv("LVAE_HB_DBG");
+  return v ? atoi(v) : 0;
+}
+
 static int hb_enabled() {  // (read per call: A/B runs and tests switch it inside one process)
   const char* v = getenv("LVAE_KL_HYPER");
   return !v || atoi(v) != 0;
 }
 
-// the plan (after kl_gram_fill's covariate check, on the same stream); tb valid only with tab_ok
+// the slab kernel's LDS: static + H + the near slots' tables (at most kHbNear of them); 0 = does not fit
+static size_t hb_slab_lds(const GramTab& tb) {
+  static size_t stat = 0;
+  if (!stat) {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_slab_kernel)) != hipSuccess) return 0;
+    stat = a.sharedSizeBytes;
+  }
+  const int ns = tb.pbeg[tb.ng] < kHbNear ? tb.pbeg[tb.ng] : kHbNear;
+  const size_t dyn = (size_t)kHbBins * kHbT * sizeof(double) + (size_t)ns * (1 << tb.nbits) * kTabR * sizeof(float);
+  return stat + dyn <= 160 * 1024 ? dyn : 0;
+}
+
+// the host's part of the conditions: the table family, the route enabled, the slab kernel's LDS fits
+static bool hb_host_ok(const lvae_kernel_spec* spec, GramTab& tb) {
+  return gram_tab_build(spec, tb) && hb_enabled() && hb_slab_lds(tb) > 0;
+}
+
+// the plan and the pair codes (after kl_gram_fill's covariate check, on the same stream)
 int kl_hyper_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, void* wsbase,
                   const int* covflag, hipStream_t st) {
   HbWs ws((char*)wsbase, np_, L);
   GramTab tb;
-  const bool ok = gram_tab_build(spec, tb) && hb_enabled();
-  int qs = 0;
-  for (int r = 0; r < spec->n_comp; ++r)
-    for (int f = 0; f < spec->n_fac[r]; ++f) qs = spec->dim[r][f] + 1 > qs ? spec->dim[r][f] + 1 : qs;
-  if (!ok || qs > kHbQ) {
+  if (!hb_host_ok(spec, tb)) {
     if (hipMemsetAsync(ws.dev, 0, sizeof(HbDev), st) != hipSuccess) return LVAE_ERR_LAUNCH;
     return 0;
   }
@@ -603,17 +783,19 @@ int kl_hyper_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n,
 int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, const double* params,
                  const float* Kinv, const float* v, const double* alpha, const double* kdiag, void* wsbase, double* part,
                  int G, hipStream_t st) {
+  (void)x;
+  (void)ldx;
   HbWs ws((char*)wsbase, np_, L);
   GramTab tb;
-  if (!gram_tab_build(spec, tb) || !hb_enabled()) return 0;
-  int qs = 0;
-  for (int r = 0; r < spec->n_comp; ++r)
-    for (int f = 0; f < spec->n_fac[r]; ++f) qs = spec->dim[r][f] + 1 > qs ? spec->dim[r][f] + 1 : qs;
-  if (qs > kHbQ) return 0;
+  if (!hb_host_ok(spec, tb)) return 0;
   const size_t tabb = (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
-  hb_slab_kernel<<<dim3(np_ / kHbT, L), 256, kHbBins * kHbT * sizeof(double) + tabb, st>>>(tb, ws, x, ldx, n, np_, qs,
-                                                                                        params, Kinv, v, alpha);
-  hb_final_kernel<<<L, 256, tabb, st>>>(tb, ws, n, np_, params, alpha, kdiag, part, G);
+  const size_t sdyn = hb_slab_lds(tb), ndyn = sdyn - (size_t)kHbBins * kHbT * sizeof(double);
+  const int nt = np_ / kHbT;
+  hb_tab_kernel<<<dim3((unsigned)((tabb / sizeof(float) + 255) / 256), L), 256, 0, st>>>(tb, ws, params);
+  hb_near_kernel<<<dim3(nt, L), 256, ndyn, st>>>(tb, ws, n, np_, Kinv, alpha);
+  hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, st>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
+  hb_sum_kernel<<<dim3((2 * kHbBins2 + kHbTail + 255) / 256, L), 256, 0, st>>>(ws, np_);
+  hb_final_kernel<<<L, 256, tabb, st>>>(tb, ws, n, np_, alpha, kdiag, part, G, hb_dbg());
   LVAE_CHECK_LAUNCH();
   return 0;
 }
