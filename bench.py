@@ -432,35 +432,57 @@ def run_closed(args, world, rank, dev):
         if use_graph:
             res["phase_timing"] = (f"HIP events around the library's launches over {args.steps} eager steps run "
                                    f"right after the graph-timed region (the same kernels, host-enqueued)")
-        # dominant kernel by GPU time: the S GEMM S = K^-1 V K^-1 (one launch per step), L np^2 (np + 1)
-        # fp32-equivalent flop (lower 256-tiles incl. the diagonal ones, whole), each a 3-product f16 split:
-        # 3 x that in f16 MFMA flop against the dense f16 peak
-        flops = Lr * np_ * np_ * (np_ + 1)
-        if syrk_ms > 0:
+        # the rooflines of the step's throughput-bound kernels, each on its average launch (the committed
+        # rocprofv3 summary of this command where there is one for the shape, else live HIP events); the
+        # primary "roofline" is the one with the most GPU time per step
+        roofs = []
+        hb_ms, hb_n = phase.get("hb_slab", (0.0, 0))
+        hyper_binned = hb_n > 0 and hb_ms > syrk_ms * args.steps  # (the route that did the work: the other exits)
+        res["hyper_route"] = ("binned (kl_hyper.hip: no S GEMM)" if hyper_binned else
+                              "S GEMM + table adjoint (LVAE_KL_HYPER=0 or the binned route's conditions unmet)")
+        headline_prof = world == 1 and Lr == 16 and np_ == 4096
+        if not hyper_binned and syrk_ms > 0:
+            # the S GEMM S = K^-1 V K^-1 (one launch per step), L np^2 (np + 1) fp32-equivalent flop (lower
+            # 256-tiles incl. the diagonal ones, whole), each a 3-product f16 split: 3 x that in f16 MFMA flop
+            flops = Lr * np_ * np_ * (np_ + 1)
             ach_ev = X3_PRODUCTS * flops / (syrk_ms * 1e-3) / 1e12
-            prof = kstats_avg_us("syrk_c16_kernel") if (world == 1 and Lr == 16 and np_ == 4096) else None
+            prof = kstats_avg_us("syrk_c16_kernel") if headline_prof else None
             avg_us = prof[0] if prof else syrk_ms * 1e3
             ach = X3_PRODUCTS * flops / (avg_us * 1e-6) / 1e12
-            res["roofline"] = {"kernel": "syrk_c16_kernel<5> (S = K^-1 V K^-1, syrk_x3.hip on the chunk-major core x3_c16.hpp; "
-                                         "the largest GPU-time share of the step)",
-                               "bound": "mfma", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": ach / F16_MFMA_PEAK_TFLOPS,
-                               "traffic": pmc_traffic(("syrk_c16_kernel",)) if world == 1 else None,
-                               "traffic_source": os.path.basename(PMC_SUMMARY),
-                               "algorithmic_flop_per_launch": X3_PRODUCTS * flops,
-                               "fp32_equivalent_tflops": flops / (avg_us * 1e-6) / 1e12,
-                               "avg_launch_us": avg_us,
-                               "avg_launch_source": (f"profiles/{os.path.basename(KSTATS)} (rocprofv3 --kernel-trace "
-                                                     f"--stats of this bench command, {prof[1]} launches)") if prof
-                                                    else "live HIP events (no committed profile for this shape)",
-                               "achieved_event": ach_ev, "frac_event": ach_ev / F16_MFMA_PEAK_TFLOPS,
-                               "avg_launch_us_event": syrk_ms * 1e3,
-                               "engine": "f16 MFMA (v_mfma_f32_32x32x16_f16), 3-product split: achieved counts the 3 "
-                                         "f16 products per fp32-equivalent product"}
-        # secondary: the trailing rank-256 update of the Cholesky (U2, HBM-streaming); per step the passes
-        # k = 0 .. nt-3 update (nt-k-2)(nt-k-1)/2 tiles per dim, each read and written once in fp32 (at
-        # <= CI_FUSE_MAX_L dims the same launch also turns column k+1's nt-k-2 tiles into the next pass's
-        # planes: read fp32, write 2 fp16 planes, the same 8 bytes per element)
+            roofs.append((syrk_ms, {
+                "kernel": "syrk_c16_kernel<5> (S = K^-1 V K^-1, syrk_x3.hip on the chunk-major core x3_c16.hpp)",
+                "bound": "mfma", "achieved": ach, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / F16_MFMA_PEAK_TFLOPS,
+                "traffic": pmc_traffic(("syrk_c16_kernel",)) if world == 1 else None,
+                "traffic_source": os.path.basename(PMC_SUMMARY), "algorithmic_flop_per_launch": X3_PRODUCTS * flops,
+                "fp32_equivalent_tflops": flops / (avg_us * 1e-6) / 1e12, "avg_launch_us": avg_us,
+                "avg_launch_source": (f"profiles/{os.path.basename(KSTATS)} (rocprofv3 --kernel-trace --stats of this "
+                                      f"bench command, {prof[1]} launches)") if prof else "live HIP events",
+                "achieved_event": ach_ev, "frac_event": ach_ev / F16_MFMA_PEAK_TFLOPS, "avg_launch_us_event": syrk_ms * 1e3,
+                "engine": "f16 MFMA (v_mfma_f32_32x32x16_f16), 3-product split: achieved counts the 3 f16 products "
+                          "per fp32-equivalent product"}))
+        if hyper_binned:
+            # the binned route's slab pass: one streaming read of the symmetric K^-1 (fp32, L np^2 x 4 B) per
+            # launch; its other inputs (bins, keys, tables: O(np)) and its record writes (O(L np/64 x 8 KB)) apart
+            hb_step_ms = hb_ms / args.steps
+            hbytes = Lr * np_ * np_ * 4
+            prof = kstats_avg_us("hb_slab_kernel") if headline_prof else None
+            avg_us = prof[0] if prof else hb_ms / hb_n * 1e3
+            ach = hbytes / (avg_us * 1e-6) / 1e9
+            ach_ev = hbytes / (hb_ms / hb_n * 1e-3) / 1e9
+            roofs.append((hb_step_ms, {
+                "kernel": "hb_slab_kernel (binned hyper-gradient slab pass over K^-1, kl_hyper.hip)",
+                "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                "traffic": pmc_traffic(("hb_slab_kernel",)) if world == 1 else None,
+                "traffic_source": os.path.basename(PMC_SUMMARY), "algorithmic_bytes_per_launch": hbytes,
+                "avg_launch_us": avg_us,
+                "avg_launch_source": (f"profiles/{os.path.basename(KSTATS)} (rocprofv3 --kernel-trace --stats of this "
+                                      f"bench command, {prof[1]} launches)") if prof else "live HIP events",
+                "achieved_event": ach_ev, "frac_event": ach_ev / HBM_PEAK_GBS, "avg_launch_us_event": hb_ms / hb_n * 1e3}))
+        # the trailing rank-256 update of the Cholesky (U2, HBM-streaming); per step the passes k = 0 .. nt-3
+        # update (nt-k-2)(nt-k-1)/2 tiles per dim, each read and written once in fp32 (at <= CI_FUSE_MAX_L dims
+        # the same launch also turns column k+1's nt-k-2 tiles into the next pass's planes: read fp32, write 2
+        # fp16 planes, the same 8 bytes per element)
         nt = np_ // 256
         fused = Lr <= CI_FUSE_MAX_L
         upd_ms, upd_n = phase.get("sweep_update", (0.0, 0))
@@ -468,17 +490,27 @@ def run_closed(args, world, rank, dev):
         upd_bytes = 2 * 4 * 256 * 256 * tiles
         u2_name = U2_NAMES[fused]
         if upd_n:
-            ach = upd_bytes / (upd_ms / args.steps * 1e-3) / 1e9
             launches = upd_n / args.steps
-            res["roofline_secondary"] = {"kernel": f"{u2_name} (potrf trailing rank-256 update U2{' + U1' if fused else ''}, chol_inv.hip)",
-                                         "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                         "frac": ach / HBM_PEAK_GBS,
-                                         "traffic": pmc_traffic((u2_name,), per_step=True) if world == 1 else None,
-                                         "traffic_source": os.path.basename(PMC_SUMMARY),
-                                         "algorithmic_bytes_per_step": upd_bytes,
-                                         "algorithmic_bytes_per_launch": upd_bytes / launches,
-                                         "avg_launch_us": upd_ms / upd_n * 1e3, "launches_per_step": launches,
-                                         "padded_n": int(np_)}
+            prof = kstats_avg_us(u2_name) if headline_prof else None
+            avg_us = prof[0] if prof else upd_ms / upd_n * 1e3
+            ach = upd_bytes / launches / (avg_us * 1e-6) / 1e9
+            ach_ev = upd_bytes / (upd_ms / args.steps * 1e-3) / 1e9
+            roofs.append((upd_ms / args.steps, {
+                "kernel": f"{u2_name} (potrf trailing rank-256 update U2{' + U1' if fused else ''}, chol_inv.hip)",
+                "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                "traffic": pmc_traffic((u2_name,), per_step=True) / launches if (world == 1 and pmc_traffic(
+                    (u2_name,), per_step=True)) else None,
+                "traffic_source": os.path.basename(PMC_SUMMARY),
+                "algorithmic_bytes_per_step": upd_bytes, "algorithmic_bytes_per_launch": upd_bytes / launches,
+                "avg_launch_us": avg_us,
+                "avg_launch_source": (f"profiles/{os.path.basename(KSTATS)} ({prof[1]} launches)") if prof
+                                     else "live HIP events", "launches_per_step": launches,
+                "achieved_event": ach_ev, "frac_event": ach_ev / HBM_PEAK_GBS,
+                "avg_launch_us_event": upd_ms / upd_n * 1e3, "padded_n": int(np_)}))
+        roofs.sort(key=lambda r: -r[0])
+        for i, (ms, r) in enumerate(roofs):
+            r["gpu_ms_per_step"] = ms
+            res["roofline" if i == 0 else ("roofline_secondary" if i == 1 else f"roofline_{i + 1}")] = r
     return res
 
 

@@ -374,7 +374,8 @@ int lvae_predict_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* spec
 enum lvae_phase {
   LVAE_PH_GRAM = 0, LVAE_PH_POTRF = 1 /* potrf (or the whole sweep) */, LVAE_PH_POTRI = 2 /* trtri + lauum */, LVAE_PH_KL_REDUCE = 3, LVAE_PH_SYRK = 4,
   LVAE_PH_GRAM_BWD = 5, LVAE_PH_BWD_ELEM = 6, LVAE_PH_HENSMAN_FWD = 7, LVAE_PH_HENSMAN_BWD = 8,
-  LVAE_PH_NATGRAD = 9, LVAE_PH_SWEEP_UPD = 10 /* the trailing rank-256 update launches (U2), nested in POTRF */, LVAE_N_PHASES = 11
+  LVAE_PH_NATGRAD = 9, LVAE_PH_SWEEP_UPD = 10 /* the trailing rank-256 update launches (U2), nested in POTRF */,
+  LVAE_PH_HB_SLAB = 11 /* the binned hyper-gradient route's slab pass (kl_hyper.hip), nested in GRAM_BWD */, LVAE_N_PHASES = 12
 };
 int lvae_prof_enable(int on);
 int lvae_prof_collect(double* ms, int32_t* count, int n_phases);

@@ -31,6 +31,7 @@
 // on the host: the slab kernel's LDS fits (hb_slab_lds).
 #include "blkinv.hpp"
 #include "gram_tab.hpp"
+#include "prof.hpp"
 
 namespace lvae {
 
@@ -204,10 +205,15 @@ __global__ __launch_bounds__(1024) void hb_plan_kernel(GramTab tb, const double*
     hb_u32x4 key = {0u, 0u, 0u, 0u};  // the near pairs' key: gate values (not the big one) and distance values
     if (i < n) {
       for (int b = 0; b < tb.nbits; ++b) {
-        const int v = (int)x[(int64_t)i * ldx + tb.bdim[b]] - d.gmin[b];
+        const int xv = (int)x[(int64_t)i * ldx + tb.bdim[b]], v = xv - d.gmin[b];
         if (b == d.big) continue;
-        if (v < 0 || v > 63) bad = 1;
-        key.x |= (unsigned)(v & 63) << (6 * b);
+        if (tb.bkind[b] == LVAE_CAT) {
+          if (v < 0 || v > 63) bad = 1;
+          key.x |= (unsigned)(v & 63) << (6 * b);
+        } else {
+          if (xv != 0 && xv != 1) bad = 1;  // (the Bin gate passes when both values are 1: x_i + x_j == 2)
+          key.w |= (unsigned)(xv == 1) << b;
+        }
       }
       for (int g = 0; g < tb.ng; ++g) {
         if (tb.gdim[g] < 0) continue;
@@ -252,24 +258,31 @@ __global__ __launch_bounds__(256) void hb_tab_kernel(GramTab tb, HbWs ws, const 
 }
 
 // a pair's code inside one run of the big covariate, from the two points' keys (hb_plan_kernel): the gate bits
-// and the distance per distance group, [bits | d_0 << 8 | d_1 << 16 | d_2 << 24]
-__device__ inline unsigned hb_pair_code(const GramTab& tb, const int* gmin, hb_u32x4 ki, hb_u32x4 kj) {
-  unsigned c = 0;
-#pragma unroll
-  for (int b = 0; b < kTabMaxBits; ++b) {
-    if (b >= tb.nbits) break;
-    const int vi = (int)((ki.x >> (6 * b)) & 63u), vj = (int)((kj.x >> (6 * b)) & 63u);
-    const bool pass = tb.bkind[b] == LVAE_CAT ? vi == vj : vi + vj + 2 * gmin[b] == 2;
-    c |= pass ? (1u << b) : 0u;
-  }
-  const unsigned di[3] = {ki.y & 0xffffu, ki.y >> 16, ki.z & 0xffffu}, dj[3] = {kj.y & 0xffffu, kj.y >> 16, kj.z & 0xffffu};
-#pragma unroll
-  for (int g = 0; g < kTabMaxG; ++g) {
-    if (g >= tb.ng) break;
-    const unsigned dist = di[g] > dj[g] ? di[g] - dj[g] : dj[g] - di[g];  // (0 without a distance dim)
-    c |= (dist < (unsigned)kTabD ? dist : (unsigned)kTabD) << (8 * (g + 1));
-  }
+// and the distance per distance group, [bits | d_0 << 8 | d_1 << 16 | d_2 << 24].  Branch-free: the Cat gates' 6-bit
+// value fields are compared all at once (a field's OR lands on its low bit, the five low bits are gathered by one
+// multiply: 2^(6b) * 2^(5 (4 - b)) = 2^(b + 20), no two products on one bit), the Bin gates pass where both keys
+// hold a one (key.w, Bin values are 0 / 1); catbits = the Cat gates' bits
+__device__ inline unsigned hb_pair_code(hb_u32x4 ki, hb_u32x4 kj, unsigned catbits, int ng) {
+  const unsigned x = ki.x ^ kj.x, x1 = x | (x >> 1), x3 = x1 | (x1 >> 2), x5 = x3 | (x1 >> 4);
+  const unsigned fail = (((x5 & 0x1041041u) * 0x108421u) >> 20) & 31u;  // Cat fields that differ
+  unsigned c = (catbits & ~fail) | (ki.w & kj.w);
+  const unsigned a0 = ki.y & 0xffffu, b0 = kj.y & 0xffffu, a1 = ki.y >> 16, b1 = kj.y >> 16;
+  const unsigned a2 = ki.z & 0xffffu, b2 = kj.z & 0xffffu;
+  const unsigned d0 = a0 > b0 ? a0 - b0 : b0 - a0, d1 = a1 > b1 ? a1 - b1 : b1 - a1, d2 = a2 > b2 ? a2 - b2 : b2 - a2;
+  const unsigned cap = (unsigned)kTabD;  // (0 without a distance dim: both keys' field 0)
+  c |= (d0 < cap ? d0 : cap) << 8;
+  if (ng > 1) c |= (d1 < cap ? d1 : cap) << 16;
+  if (ng > 2) c |= (d2 < cap ? d2 : cap) << 24;
   return c;
+}
+
+// the Cat gates' bits (uniform)
+__device__ inline unsigned hb_catbits(const GramTab& tb) {
+  unsigned m = 0;
+#pragma unroll
+  for (int b = 0; b < kTabMaxBits; ++b)
+    if (b < tb.nbits && tb.bkind[b] == LVAE_CAT) m |= 1u << b;
+  return m;
 }
 
 // the near slots' tables of dim l into LDS (slot after slot; hb_tab_kernel's) and each slot's distance group
@@ -304,6 +317,7 @@ __global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n
   __syncthreads();
   const float* K = Kinv + (int64_t)l * np_ * np_;
   const double* al = alpha + (int64_t)l * np_;
+  const unsigned catbits = hb_catbits(tb);
   double acc[kHbNear];
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) acc[k] = 0.0;
@@ -314,7 +328,7 @@ __global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n
       const int s = ws.rs[i], len = ws.re[i] - s;
       if (jj >= len) continue;
       const int j = s + jj;
-      const unsigned c = hb_pair_code(tb, d.gmin, ws.rkey[i], ws.rkey[j]);
+      const unsigned c = hb_pair_code(ws.rkey[i], ws.rkey[j], catbits, tb.ng);
       const double val = 0.5 * ((double)K[(int64_t)i * np_ + j] - al[i] * al[j]);
 #pragma unroll
       for (int k = 0; k < kHbNear; ++k)
@@ -337,65 +351,74 @@ __global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n
 // tile by tile, and writes its partial record: M_g = H_g V H_g^T, Q_g = H_g Phi_g (the slab's columns), the near
 // runs' S parts per near slot, the slab's part of tr S and of a = Phi^T alpha.
 //
-//   H_g += Phi_g(tile)^T K^-1(tile, slab): a one-hot GEMM per 32-bin block and 32-column block on
-//     v_mfma_f32_32x32x16_bf16, K^-1 split exactly into three bf16 pieces (hi + mid + lo = the fp32 value), the
-//     one-hot operand exact: fp32 sums of the tile's 64 rows, then fp64 adds into H (each entry owned by one lane)
-//   near runs ending in the tile: 16 x 16 blocks of X V X^T on v_mfma_f32_16x16x4f32, contracted with the near
-//     slots' tables through the pair codes (hb_pair_code, from the rows' keys)
-//   tr S part: from the registers the tile arrives in
-// Tiles arrive two ahead in registers (two prefetch sets, the loop unrolled by two).
+//   tile store: every thread splits its 4 rows x 2 columns exactly into three bf16 pieces (round to nearest:
+//     hi + mid + lo = the fp32 value) and writes them column-major into three planes (8-row chunks swizzled by
+//     the column: conflict-free 16-byte reads), the fp32 rows for the near runs, and its tr S part
+//   H_g += Phi_g(tile)^T K^-1(tile, slab): one-hot GEMMs on v_mfma_f32_32x32x16_bf16, item = (32-bin block,
+//     32-column block), at most two items per wave held in the accumulators across tiles (products exact, fp32
+//     sums over 4 tiles, then folded into H in LDS, fp64, each entry owned by one lane)
+//   near runs ending in the tile: 16 x 16 blocks of X V X^T on v_mfma_f32_16x16x4f32 (the fp32 tile holds X V^(1/2),
+//     v > 0), contracted with the near
+//     slots' tables through the pair codes (hb_pair_code, from the rows' keys); block items dealt from the last
+//     wave down (the H items from the first up)
+// Tiles arrive two ahead in registers (two prefetch sets, the loop unrolled by two, no branch around a load).
 // ------------------------------------------------------------------------------------------
 __device__ inline int hb_row_slot(int row) { return (row >> 6) & 1; }
 
-typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
+#ifdef LVAE_HB_STAMP  // (diagnostic builds only: per-section cycle stamps of the slab pass, printed by workgroup (0, 0))
+#define HB_STAMP(t)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#else
+#define HB_STAMP(t) \
+  do {              \
+  } while (0)
+#endif
+
+typedef float hb_f32x2 __attribute__((ext_vector_type(2)));
 typedef float hb_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 hb_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 hb_bf16x2 __attribute__((ext_vector_type(2)));
 constexpr int kHbBlk = 7;  // 32-bin blocks over the binnings (sum ceil(nb_g / 32) with sum nb_g <= 128, <= 4 binnings)
-
-constexpr int kHbSlabThreads = 512, kHbSlabWaves = kHbSlabThreads / 64;  // (2 waves per SIMD: latency hiding)
-constexpr int kHbPk = kHbT * kHbT / 4 / kHbSlabThreads;                    // float4 per thread per tile
+constexpr int kHbSlabThreads = 512, kHbSlabWaves = kHbSlabThreads / 64;  // (2 waves per SIMD)
+constexpr int kHbFold = 4;  // tiles summed in fp32 by the accumulators before the fp64 fold
 
 struct HbPre {        // one tile's prefetch
-  hb_f32x4 pk[kHbPk]; // K^-1 rows (e >> 4), columns 4 (e & 15) .. + 3, e = tid + kHbSlabThreads u
+  hb_f32x2 pk[4];     // K^-1 rows 4 (tid >> 5) + u, columns 2 (tid & 31) + 0, 1
   int pbn;            // wave w < nbin: bin of row lane in binning w
-  int pre_, prs;      // wave 0: run end / start of row lane
-  hb_u32x4 key;       // wave 0: key of row lane
+  int pre_, prs;      // run end / start of row lane (wave 0's)
+  hb_u32x4 key;       // key of row lane (wave 0's)
 };
 
-// the three bf16 pieces of 8 fp32 values (truncation: t = hi + mid + lo exactly)
-__device__ inline void hb_split8(const float* t, hb_bf16x8& hi, hb_bf16x8& mid, hb_bf16x8& lo) {
-  hb_u32x4 h, m, o;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float a = t[2 * k], b = t[2 * k + 1];
-    const float ah = __uint_as_float(__float_as_uint(a) & 0xffff0000u), bh = __uint_as_float(__float_as_uint(b) & 0xffff0000u);
-    const float a1 = a - ah, b1 = b - bh;
-    const float am = __uint_as_float(__float_as_uint(a1) & 0xffff0000u), bm = __uint_as_float(__float_as_uint(b1) & 0xffff0000u);
-    const float a2 = a1 - am, b2 = b1 - bm;
-    h[k] = __builtin_amdgcn_perm(__float_as_uint(bh), __float_as_uint(ah), 0x07060302u);
-    m[k] = __builtin_amdgcn_perm(__float_as_uint(bm), __float_as_uint(am), 0x07060302u);
-    o[k] = __builtin_amdgcn_perm(__float_as_uint(b2), __float_as_uint(a2), 0x07060302u);
-  }
-  hi = __builtin_bit_cast(hb_bf16x8, h);
-  mid = __builtin_bit_cast(hb_bf16x8, m);
-  lo = __builtin_bit_cast(hb_bf16x8, o);
+__device__ inline unsigned hb_pk_bf16(float a, float b) {  // (round to nearest even: v_cvt_pk_bf16_f32)
+  const hb_bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
 }
+__device__ inline float hb_bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ inline float hb_bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+// dword offset in a bf16 plane of (column c, 8-row chunk k): 32 dwords per column, chunks swizzled by (c >> 1) & 7
+__device__ inline int hb_pl_off(int c, int k) { return c * 32 + ((k ^ ((c >> 1) & 7)) << 2); }
 
 __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbWs ws, int n, int np_,
-                                                      const float* __restrict__ Kinv, const float* __restrict__ vv,
-                                                      const double* __restrict__ alpha, int dbg) {
+                                                                 const float* __restrict__ Kinv,
+                                                                 const float* __restrict__ vv,
+                                                                 const double* __restrict__ alpha, int dbg) {
   __shared__ HbDev d;
-  __shared__ __attribute__((aligned(16))) float T[2][kHbT * kHbTP];  // the row tiles of the window (slot = (row / 64) & 1)
+  __shared__ __attribute__((aligned(16))) float T[2][kHbT * kHbTP];  // fp32 row tiles of the window (near runs)
+  __shared__ __attribute__((aligned(16))) unsigned Pw[3][kHbT * 32];  // the current tile's bf16 planes, column-major
   __shared__ __attribute__((aligned(8))) uint8_t rbin[kHbMaxBin][kHbT];  // bins of the current tile's rows
   __shared__ uint8_t cbin[kHbMaxBin][kHbT];     // bins of the slab's columns
   __shared__ float vs[kHbT];                    // v of the slab's columns
   __shared__ double acol[kHbT];                 // alpha of the slab's columns
-  __shared__ int runs[kHbT], runl[kHbT], nrun;
-  __shared__ hb_u32x4 rk[2][kHbT];                 // the window's row keys
+  __shared__ hb_u32x4 rk[2][kHbT];              // the window's row keys
   __shared__ int sgrp[kHbNear];
   __shared__ int sbg[kHbBlk], sbb[kHbBlk], nbk;  // 32-bin blocks: binning, block index
   __shared__ double red[kHbSlabWaves][kHbNear + 1];
-  extern __shared__ double hdyn[];              // H [kHbBins][64] (fp64), then the near slots' tables (fp32)
+  extern __shared__ double hdyn[];              // H [kHbBins][64] (fp64, folded every kHbFold tiles), then the near tables
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, J = blockIdx.x, l = blockIdx.y, J0 = J * kHbT;
   if (tid == 0) d = *ws.dev;
   __syncthreads();
@@ -403,12 +426,13 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
   double* H = hdyn;
   float* tab = reinterpret_cast<float*>(hdyn + kHbBins * kHbT);
   const int tstride = (1 << tb.nbits) * kTabR;
-  for (int e = tid; e < d.nbins * kHbT; e += kHbSlabThreads) H[e] = 0.0;
   if (tid < kHbT) {
     vs[tid] = vv[(int64_t)l * np_ + J0 + tid];
     acol[tid] = alpha[(int64_t)l * np_ + J0 + tid];
   }
-  for (int e = tid; e < d.nbin * kHbT; e += kHbSlabThreads) cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
+  for (int e = tid; e < d.nbins * kHbT; e += kHbSlabThreads) H[e] = 0.0;
+  for (int e = tid; e < d.nbin * kHbT; e += kHbSlabThreads)
+    cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
   hb_near_tables(tb, d, ws.tab + (int64_t)l * kTabMaxBwdLds, tstride, tab, sgrp);
   if (tid == 0) {  // the 32-bin blocks of the binnings in order
     int t = 0;
@@ -421,116 +445,144 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
   }
   __syncthreads();
   const float* K = Kinv + (int64_t)l * np_ * np_;
-  const int nbin = d.nbin, nnear = d.nnear, bigon = d.big >= 0;
-  // this wave's H work: column block cb = w & 1, the 32-bin blocks t = w >> 1 (mod kHbSlabWaves / 2)
-  const int cb = w & 1, nblk = nbk;
-  int ngrp[kHbNear];
+  const int nbin = d.nbin, nnear = d.nnear, bigon = d.big >= 0, nitem = 2 * nbk;
+  const unsigned catbits = hb_catbits(tb);
+  // H items (item = 2 block + column block): the column block w & 1 for both of a wave's items
+  const int cb = w & 1, hh = lane >> 5, col = 32 * cb + (lane & 31);
+  // items: waves 0-3 take w and w + 4, waves 4-7 take w + 4 and w + 8 (two per wave sharing the B operands; with
+  // <= 8 items waves 4-7 have none and take the near runs first)
+  const int i0 = w < 4 ? w : w + 4, i1 = i0 + 4;
+  const bool it0 = i0 < nitem, it1 = i1 < nitem;
+  int g0 = 0, b00 = 0, g1 = 0, b01 = 0;
+  if (it0) {
+    g0 = sbg[i0 >> 1];
+    b00 = 32 * sbb[i0 >> 1];
+  }
+  if (it1) {
+    g1 = sbg[i1 >> 1];
+    b01 = 32 * sbb[i1 >> 1];
+  }
+  hb_f32x16 acc0 = {}, acc1 = {};
+  // H += acc (rows b0 + (e & 3) + 8 (e >> 2) + 4 hh of binning g, column col), acc = 0
+  auto hb_fold = [&](hb_f32x16& acc, int g, int b0) {
+    const int nb = d.bn[g];
+    double* hc = H + (int64_t)d.boff[g] * kHbT + col;
+    double hv[16];
 #pragma unroll
-  for (int k = 0; k < kHbNear; ++k) ngrp[k] = k < nnear ? sgrp[k] : 0;
+    for (int e = 0; e < 16; ++e) {
+      const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+      hv[e] = hc[(b < nb ? b : 0) * kHbT];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+      if (b < nb) hc[b * kHbT] = hv[e] + (double)acc[e];
+      acc[e] = 0.f;
+    }
+  };
   double nacc[kHbNear];
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) nacc[k] = 0.0;
   double tS = 0.0;
-  float vreg[4];  // v of this thread's 4 columns (the same in every tile)
-#pragma unroll
-  for (int c = 0; c < 4; ++c) vreg[c] = vs[(tid & 15) * 4 + c];
+  const int cp = tid & 31, i4 = tid >> 5;  // this thread's tile part: columns 2 cp + 0, 1; rows 4 i4 + 0..3
+  const float v0 = vs[2 * cp], v1 = vs[2 * cp + 1], r0 = sqrtf(v0), r1 = sqrtf(v1);
   const int nt = np_ / kHbT;
 
   auto fetch = [&](int I, HbPre& p) {
     const int I0 = I * kHbT;
 #pragma unroll
-    for (int u = 0; u < kHbPk; ++u) {
-      const int e = tid + kHbSlabThreads * u, r = e >> 4, c4 = (e & 15) * 4;
-      p.pk[u] = __builtin_nontemporal_load(reinterpret_cast<const hb_f32x4*>(K + (int64_t)(I0 + r) * np_ + J0 + c4));
-    }
-    // (every load unconditional: no branch around loads, so the waits before a tile's use count exactly the
-    // newer tile's loads and leave them in flight)
+    for (int u = 0; u < 4; ++u)
+      p.pk[u] = __builtin_nontemporal_load(
+          reinterpret_cast<const hb_f32x2*>(K + (int64_t)(I0 + 4 * i4 + u) * np_ + J0 + 2 * cp));
     p.pbn = (int)ws.pbin[(size_t)(w < nbin ? w : 0) * np_ + I0 + lane];  // (used by waves w < nbin only)
     p.pre_ = ws.re[I0 + lane];
     p.prs = ws.rs[I0 + lane];
     p.key = ws.rkey[I0 + lane];
   };
 
+  unsigned long long tsec[4] = {0, 0, 0, 0};
   auto body = [&](int I, const int sl, HbPre& p) {
     const int I0 = I * kHbT;
-    float ts = 0.f;
+    unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0;
+    HB_STAMP(st0);
+    {  // the tile into LDS: fp32 rows, the bf16 planes; the tr S part (sum_m v_m (K^-1_im)^2)
+      float ts = 0.f;
 #pragma unroll
-    for (int u = 0; u < kHbPk; ++u) {
-      const int e = tid + kHbSlabThreads * u, r = e >> 4, c4 = (e & 15) * 4;
-      *reinterpret_cast<hb_f32x4*>(&T[sl][r * kHbTP + c4]) = p.pk[u];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) ts += p.pk[u][c] * p.pk[u][c] * vreg[c];  // tr S part: sum_m v_m (K^-1_im)^2
-    }
-    tS += (double)ts;
-    if (w < nbin) rbin[w][lane] = (uint8_t)p.pbn;
-    if (w == 0) {  // the runs of the big covariate ending in this tile, the rows' keys
-      const int i = I0 + lane;
-      rk[sl][lane] = p.key;
-      const bool last = bigon && i < n && p.pre_ == i + 1;
-      const unsigned long long m = __ballot(last);
-      if (last) {
-        const int k = __popcll(m & ((1ull << lane) - 1));
-        runs[k] = p.prs;
-        runl[k] = i + 1 - p.prs;
+      for (int u = 0; u < 4; ++u) {
+        const hb_f32x2 sv = {p.pk[u][0] * r0, p.pk[u][1] * r1};  // (X V^(1/2), v = exp(log var) > 0)
+        *reinterpret_cast<hb_f32x2*>(&T[sl][(4 * i4 + u) * kHbTP + 2 * cp]) = sv;
+        ts += p.pk[u][0] * p.pk[u][0] * v0 + p.pk[u][1] * p.pk[u][1] * v1;
       }
-      if (lane == 0) nrun = __popcll(m);
+      tS += (double)ts;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float a0 = p.pk[0][c], a1 = p.pk[1][c], a2 = p.pk[2][c], a3 = p.pk[3][c];
+        const unsigned h01 = hb_pk_bf16(a0, a1), h23 = hb_pk_bf16(a2, a3);
+        const float r0 = a0 - hb_bf_lo(h01), r1 = a1 - hb_bf_hi(h01), r2 = a2 - hb_bf_lo(h23), r3 = a3 - hb_bf_hi(h23);
+        const unsigned m01 = hb_pk_bf16(r0, r1), m23 = hb_pk_bf16(r2, r3);
+        const float s0 = r0 - hb_bf_lo(m01), s1 = r1 - hb_bf_hi(m01), s2 = r2 - hb_bf_lo(m23), s3 = r3 - hb_bf_hi(m23);
+        const unsigned o01 = hb_pk_bf16(s0, s1), o23 = hb_pk_bf16(s2, s3);
+        const int off = hb_pl_off(2 * cp + c, i4 >> 1) + 2 * (i4 & 1);
+        *reinterpret_cast<uint2*>(&Pw[0][off]) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(&Pw[1][off]) = make_uint2(m01, m23);
+        *reinterpret_cast<uint2*>(&Pw[2][off]) = make_uint2(o01, o23);
+      }
     }
+    if (w < nbin) rbin[w][lane] = (uint8_t)p.pbn;
+    if (w == 0) rk[sl][lane] = p.key;  // the rows' keys
+    // the runs of the big covariate ending in this tile, in every wave's registers (its own copies of the run
+    // bounds): lane e set = a run ends at row I0 + e, its start in lane e of rstart
+    const unsigned long long runmask = __ballot(bigon && I0 + lane < n && p.pre_ == I0 + lane + 1);
+    const int rstart = p.prs;
     __syncthreads();
+    HB_STAMP(st1);
     fetch(I + 2 < nt ? I + 2 : nt - 1, p);  // (in flight under the next two tiles' work; the last two: a dummy)
-    if (!(dbg & 1) && (w >> 1) < nblk) {  // (waves without a block skip the B operands too)
-      // B operands: rows 16 ks + 8 (lane >> 5) + 0..7 of column 32 cb + (lane & 31), three bf16 pieces
-      hb_bf16x8 bh[4], bm[4], bl[4];
-      const int col = 32 * cb + (lane & 31), hh = lane >> 5;
+    if (!(dbg & 1) && it0) {
+      auto onehot = [&](int g, int b0, int ks) {  // A operand: [bin b0 + (lane & 31)][rows 16 ks + 8 hh + 0..7]
+        const unsigned mybin = (unsigned)(b0 + (lane & 31));
+        const uint2 rb = *reinterpret_cast<const uint2*>(&rbin[g][16 * ks + 8 * hh]);
+        hb_u32x4 a;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const unsigned wd = k < 2 ? rb.x : rb.y, sh = 16 * (k & 1);
+          const unsigned lo_ = ((wd >> sh) & 0xffu) == mybin ? 0x3f80u : 0u;
+          const unsigned hi_ = ((wd >> (sh + 8)) & 0xffu) == mybin ? 0x3f800000u : 0u;
+          a[k] = lo_ | hi_;
+        }
+        return __builtin_bit_cast(hb_bf16x8, a);
+      };
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        float t8[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t8[k] = T[sl][(16 * ks + 8 * hh + k) * kHbTP + col];
-        hb_split8(t8, bh[ks], bm[ks], bl[ks]);
+        // B operands: column col, rows 16 ks + 8 hh + 0..7, the three pieces (shared by the wave's two items)
+        const hb_bf16x8 bh = *reinterpret_cast<const hb_bf16x8*>(&Pw[0][hb_pl_off(col, 2 * ks + hh)]);
+        const hb_bf16x8 bm = *reinterpret_cast<const hb_bf16x8*>(&Pw[1][hb_pl_off(col, 2 * ks + hh)]);
+        const hb_bf16x8 bl = *reinterpret_cast<const hb_bf16x8*>(&Pw[2][hb_pl_off(col, 2 * ks + hh)]);
+        const hb_bf16x8 a0 = onehot(g0, b00, ks);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bm, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh, acc0, 0, 0, 0);
+        if (it1) {
+          const hb_bf16x8 a1 = onehot(g1, b01, ks);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bm, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh, acc1, 0, 0, 0);
+        }
       }
-      for (int q = w >> 1; q < nblk; q += kHbSlabWaves / 2) {  // this wave's blocks
-        const int g = sbg[q], b0 = 32 * sbb[q], nb = d.bn[g];
-        const int mybin = b0 + (lane & 31);
-        hb_f32x16 acc = {};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          // A operand (one-hot): [bin b0 + (lane & 31)][rows 16 ks + 8 hh + 0..7]
-          const uint2 rb = *reinterpret_cast<const uint2*>(&rbin[g][16 * ks + 8 * hh]);
-          hb_u32x4 a;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const unsigned wd = k < 2 ? rb.x : rb.y, sh = 16 * (k & 1);
-            const unsigned lo_ = ((wd >> sh) & 0xffu) == (unsigned)mybin ? 0x3f80u : 0u;
-            const unsigned hi_ = ((wd >> (sh + 8)) & 0xffu) == (unsigned)mybin ? 0x3f800000u : 0u;
-            a[k] = lo_ | hi_;
-          }
-          const hb_bf16x8 av = __builtin_bit_cast(hb_bf16x8, a);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bl[ks], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bm[ks], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bh[ks], acc, 0, 0, 0);
-        }
-        // acc[e]: bin b0 + (e & 3) + 8 (e >> 2) + 4 hh, column col
-        double* hc = H + (int64_t)d.boff[g] * kHbT + col;
-        double hv[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          hv[e] = b < nb ? hc[b * kHbT] : 0.0;
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (b < nb) hc[b * kHbT] = hv[e] + (double)acc[e];
-        }
+      if ((I & (kHbFold - 1)) == kHbFold - 1) {  // fold the accumulators into H (fp64, LDS; entries owned by lane)
+        hb_fold(acc0, g0, b00);
+        if (it1) hb_fold(acc1, g1, b01);
       }
     }
-    // near runs ending in this tile: 16 x 16 blocks (bi, bj) of X V X^T, block items dealt to the waves
+    HB_STAMP(st2);
+    // near runs ending in this tile: 16 x 16 blocks (bi, bj) of X V X^T, items dealt from the last wave down
     if (!(dbg & 2)) {
-      int item = w;
-      const int nr = nrun;
-      for (int k = 0; k < nr; ++k) {
-        const int s0 = runs[k], len = runl[k], nb16 = (len + 15) >> 4;
-        for (; item < nb16 * nb16; item += kHbSlabWaves) {
+      const int wr = kHbSlabWaves - 1 - w;
+      int gi0 = 0;
+      for (unsigned long long rm = runmask; rm; rm &= rm - 1) {
+        const int e = __builtin_ctzll(rm);
+        const int s0 = __builtin_amdgcn_readlane(rstart, e), len = I0 + e + 1 - s0;
+        const int nb16 = (len + 15) >> 4, n2 = nb16 * nb16;
+        for (int item = (wr - gi0) & (kHbSlabWaves - 1); item < n2; item += kHbSlabWaves) {
           const int bi = item / nb16, bj = item % nb16;
           const int li = lane & 15, lk = lane >> 4;
           const int ra = s0 + 16 * bi + li, rb = s0 + 16 * bj + li;  // the lane's A row, B column
@@ -538,31 +590,50 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
           const float* ta = &T[hb_row_slot(ra)][(ra & 63) * kHbTP];
           const float* tb2 = &T[hb_row_slot(rb)][(rb & 63) * kHbTP];
           bi_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if (!(dbg & 16)) {  // (two accumulators: half the dependent chain; the operands all read first)
+            float av[16], bv[16];
 #pragma unroll
-          for (int s4 = 0; s4 < kHbT; s4 += 4) {
-            const int m = s4 + lk;
-            const float a = va ? ta[m] * vs[m] : 0.f;
-            const float b = vb ? tb2[m] : 0.f;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+            for (int t = 0; t < 16; ++t) {
+              av[t] = ta[4 * t + lk];
+              bv[t] = tb2[4 * t + lk];
+            }
+            bi_f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < 16; t += 2) {
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? av[t] : 0.f, vb ? bv[t] : 0.f, acc, 0, 0, 0);
+              acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? av[t + 1] : 0.f, vb ? bv[t + 1] : 0.f, acc2, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] += acc2[q];
           }
-          // the lane's 4 pairs (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li)
+          if (dbg & 8) continue;
+          // the lane's 4 pairs (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li); pairs outside the run: rows of
+          // the run (clamped), weight 0 (no branch)
           const hb_u32x4 kj = rk[hb_row_slot(rb)][rb & 63];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int ioff = 16 * bi + 4 * lk + q, i = s0 + ioff;
-            if (ioff >= len || !vb) continue;
-            const unsigned c = hb_pair_code(tb, d.gmin, rk[hb_row_slot(i)][i & 63], kj);
+            const int ioff = 16 * bi + 4 * lk + q, i = s0 + (ioff < len ? ioff : 0);
+            const double wq = (ioff < len && vb) ? (double)acc[q] : 0.0;
+            const unsigned c = hb_pair_code(rk[hb_row_slot(i)][i & 63], kj, catbits, tb.ng);
+            const int cb8 = (int)(c & 0xffu) * kTabR;
 #pragma unroll
             for (int k2 = 0; k2 < kHbNear; ++k2) {
               if (k2 >= nnear) break;
-              nacc[k2] += (double)acc[q] * (double)hb_near_d(tab, k2 * tstride, c, ngrp[k2]);
+              const int g = sgrp[k2];
+              nacc[k2] += wq * (double)tab[k2 * tstride + cb8 + (int)((c >> (8 * (g + 1))) & 0xffu)];
             }
           }
         }
-        item -= nb16 * nb16;  // (this wave's next item index in the following run's block list)
+        gi0 += n2;
       }
     }
-    __syncthreads();  // every reader of slot sl done before tile I + 2 overwrites it (and the run list, the bins)
+    HB_STAMP(st3);
+    __syncthreads();  // every reader of slot sl, the planes, the bins, the run list done before the next store
+    HB_STAMP(st4);
+    tsec[0] += st1 - st0;
+    tsec[1] += st2 - st1;
+    tsec[2] += st3 - st2;
+    tsec[3] += st4 - st3;
   };
 
   HbPre pa, pb;
@@ -572,6 +643,11 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
     body(I, 0, pa);
     body(I + 1, 1, pb);
   }
+  if (it0 && (nt & (kHbFold - 1))) {  // the last fold (nt a multiple of 4: nothing left)
+    hb_fold(acc0, g0, b00);
+    if (it1) hb_fold(acc1, g1, b01);
+  }
+  __syncthreads();
   // Q_g[b][b'] = sum over the slab's columns m in bin b' of H_g[b][m]: thread (g, b) owns row b (LDS scratch = T);
   // a part: thread (g, b) sums alpha over the slab's columns in bin b
   double* Qs = reinterpret_cast<double*>(&T[0][0]);
@@ -616,6 +692,10 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
       }
     }
   }
+#ifdef LVAE_HB_STAMP
+  if (lane == 0 && l == 0 && (J == 0 || J == 17))
+    printf("hbstamp J %d w %d store+bar %llu H %llu near %llu bar %llu\n", J, w, tsec[0], tsec[1], tsec[2], tsec[3]);
+#endif
   // the near slots' S parts and tr S's part: the waves' sums in a fixed order
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) {
@@ -793,7 +873,10 @@ int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   const int nt = np_ / kHbT;
   hb_tab_kernel<<<dim3((unsigned)((tabb / sizeof(float) + 255) / 256), L), 256, 0, st>>>(tb, ws, params);
   hb_near_kernel<<<dim3(nt, L), 256, ndyn, st>>>(tb, ws, n, np_, Kinv, alpha);
-  hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, st>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
+  {
+    ProfScope ps(LVAE_PH_HB_SLAB, st);
+    hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, st>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
+  }
   hb_sum_kernel<<<dim3((2 * kHbBins2 + kHbTail + 255) / 256, L), 256, 0, st>>>(ws, np_);
   hb_final_kernel<<<L, 256, tabb, st>>>(tb, ws, n, np_, alpha, kdiag, part, G, hb_dbg());
   LVAE_CHECK_LAUNCH();

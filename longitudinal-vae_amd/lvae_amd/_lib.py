@@ -155,6 +155,8 @@ def load(path=LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    if path == LIB_PATH:  # (a diagnostic build in place of the in-tree one: scripts/gpu_hbstamp.sh)
+        path = os.environ.get("LVAE_LIB", path)
     if not os.path.exists(path):
         raise RuntimeError(f"lvae_amd: HIP library {path} not built (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)
@@ -202,7 +204,7 @@ def xview(t, stride_b, stride_l):
 
 
 PHASES = ["gram", "potrf", "potri", "kl_reduce", "syrk", "gram_bwd", "bwd_elem", "hensman_fwd", "hensman_bwd",
-          "natgrad", "sweep_update"]
+          "natgrad", "sweep_update", "hb_slab"]
 
 
 def prof_enable(on=True):

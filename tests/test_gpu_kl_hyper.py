@@ -15,7 +15,14 @@ from test_gpu_regime_b import CFG, DEV, _random_hypers, rel, set_raw
 pytestmark = pytest.mark.gpu
 
 
-def _run(P, L, seed, perm=None, hyper=None):
+# Bin gates on far and near components: a Bin kernel (far) and a missing-value mask (covariate 5) on the
+# components of covariate 1 -- the id x covariate-1 one (near).  Far bins: 2 + 16 + 32 (<= 128, sum nb^2 <= 4096)
+HB_GATES = dict(cat_kernel=[2], bin_kernel=[4], sqexp_kernel=[0],
+                cat_int_kernel=[{'cont_covariate': 0, 'cat_covariate': 3}, {'cont_covariate': 1, 'cat_covariate': 2}],
+                bin_int_kernel=[], covariate_missing_val=[{'covariate': 1, 'mask': 5}])
+
+
+def _run(P, L, seed, perm=None, hyper=None, cfg=CFG):
     import lvae_amd as la
     from lvae_amd.data import health_mnist_covariates
     from lvae_amd.elbo import kl_closed_hyper_log
@@ -26,7 +33,7 @@ def _run(P, L, seed, perm=None, hyper=None):
     lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
     if perm is not None:
         X, mu, lv = X[perm], mu[perm], lv[perm]
-    k = la.generate_kernel(**CFG, latent_dim=L).double()
+    k = la.generate_kernel(**cfg, latent_dim=L).double()
     raw = _random_hypers(k, L, np.random.default_rng(seed))
     set_raw(k, raw)
     kd = k.to(DEV)
@@ -51,8 +58,8 @@ def _run(P, L, seed, perm=None, hyper=None):
                 on=int(hlog[0].item()), dnoise=dnoise)
 
 
-def _oracle_grads(r, l):
-    spec = O.spec_full(**CFG)
+def _oracle_grads(r, l, cfg=CFG):
+    spec = O.spec_full(**cfg)
     raw = torch.tensor(r["raw"][l], requires_grad=True)
     ref = O.kl_closed(spec, O.constrain(raw), r["X"], 1.0, r["mu"][:, l], r["lv"][:, l])
     ((l + 1) * ref).backward()
@@ -82,6 +89,20 @@ def test_binned_and_gemm_routes_agree(hip, P, L):
     en = rel(a["dnoise"], b["dnoise"])
     print(f"P={P}: binned vs S-GEMM route raw gradients {e:.2e}, noise {en:.2e}")
     assert e < 2e-5 and en < 2e-5
+
+
+def test_binned_route_bin_gates_vs_oracle(hip):
+    """Bin gates in a far component (a Bin kernel) and in a near one (the missing-value mask on the id x
+    covariate-1 component): the pair codes' Bin rule (both values 1) and the far bins' gate decode."""
+    P, L = 64, 2
+    r = _run(P, L, seed=11, cfg=HB_GATES)
+    assert r["on"] == 1
+    for l in range(L):
+        ref, g = _oracle_grads(r, l, HB_GATES)
+        assert rel(r["kl"][l], ref) < 1e-4
+        e = rel(r["draw"][l], g)
+        print(f"Bin gates dim {l}: binned-route raw-parameter gradients rel err {e:.2e}")
+        assert e < 1e-4
 
 
 def test_binned_route_off_for_unsorted_ids(hip):
