@@ -414,6 +414,16 @@ int lvae_param_pack_fwd_f64(int n_raw, int L, int P, const int* cols, const doub
  * bound kld [1] (fp64): rec = c sum mse, nl = c sum nll (fp32), kd = ks kld, net = nl + kd (use_nll) or
  * rec + w kd (fp64).  Backward: d/d mse_i, d/d nll_i (the same for every image, fp32) and d/d kld from the
  * gradients of net / rec / nl / kd (nullptr: zero).                                                   */
+/* The ConvVAE's bias + ReLU around its library GEMMs and transposed conv (VAE.py:44-75) on [N, C, HW] fp32
+ * (HW = 1: a Linear's [B, F] rows).  Forward: y = relu(y + bias[c]) in place.  Backward: g = gy [y > 0]
+ * (relu != 0; y the forward's output; with relu = 0 g is not written: g = gy) and db[c] = sum over n, hw
+ * of g (per 64-image chunk partials in workspace [lvae_act_bwd_workspace_size(N, C) bytes], then the
+ * chunks in order).  Replaces PyTorch's threshold_backward + the bias reduction of nn.Linear /
+ * nn.ConvTranspose2d's backward (VAE.py:62-75).                                                     */
+int lvae_bias_relu_fwd_f32(float* y, const float* bias, int N, int C, int HW, void* stream);
+size_t lvae_act_bwd_workspace_size(int N, int C);
+int lvae_act_bwd_f32(const float* gy, const float* y, int N, int C, int HW, int relu, float* g, float* db,
+                     void* workspace, void* stream);
 int lvae_step_terms_fwd(const float* mse, const float* nll, int B, const double* kld, float c, double ks, double w,
                         int use_nll, float* rec, float* nl, double* net, double* kd, void* stream);
 int lvae_step_terms_bwd(const double* g_net, const float* g_rec, const float* g_nl, const double* g_kd, float c,

@@ -9,6 +9,11 @@
 //   param_pack      the kernel hyper-parameters exp(m + softplus(raw - m)) (GP_model.py:31-144's
 //                   positivity transform) gathered from their separate [L] tensors into the [L, P] matrix
 //                   the GP kernels read; backward: d raw, scattered back per tensor
+//   bias_act        the ConvVAE's bias + ReLU around its library GEMMs / transposed conv (VAE.py:44-75):
+//                   forward bias + ReLU in place over [N, C, HW] (the transposed conv's output); backward
+//                   g = gy [y > 0] and the bias gradient sum_{n, hw} g in one pass (per-chunk partials, then
+//                   the chunks in order: fixed summation order) -- in place of PyTorch's threshold_backward
+//                   and its strided reduce kernel per layer
 #include "common.hpp"
 
 namespace lvae {
@@ -166,6 +171,70 @@ __global__ void step_terms_bwd_kernel(const double* __restrict__ g_net, const fl
   g_kld[0] = ks * ((use_nll ? gn : w * gn) + (g_kd ? g_kd[0] : 0.0));
 }
 
+// ---- bias_act: [N, C, HW] fp32 (HW = 1: a Linear's [B, F] rows) --------------------------------------------
+// y = relu(y + b[c]) in place
+__global__ __launch_bounds__(256) void bias_relu_fwd_kernel(float* __restrict__ y, const float* __restrict__ b, int C,
+                                                            int HW, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)((e / HW) % C);
+  y[e] = fmaxf(y[e] + b[c], 0.f);
+}
+
+constexpr int kActRows = 64;  // images (rows) per partial chunk
+// HW == 1 (rows of a Linear): grid (cdiv(C, 64), cdiv(N, kActRows)), thread (column tx, row phase ty)
+__global__ __launch_bounds__(256) void act_bwd_rows_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                                                           int N, int C, int relu, float* __restrict__ g,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6, c = blockIdx.x * 64 + tx, n0 = blockIdx.y * kActRows;
+  float s = 0.f;
+  if (c < C) {
+    for (int k = ty; k < kActRows && n0 + k < N; k += 4) {
+      const int64_t o = (int64_t)(n0 + k) * C + c;
+      float v = gy[o];
+      if (relu) v = y[o] > 0.f ? v : 0.f;
+      if (g) g[o] = v;
+      s += v;
+    }
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) part[(int64_t)blockIdx.y * C + c] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+}
+// HW > 1 (NCHW): grid (C, cdiv(N, kActRows)), the workgroup sums channel c over its images' HW planes
+__global__ __launch_bounds__(256) void act_bwd_chan_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                                                           int N, int C, int HW, int relu, float* __restrict__ g,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4];
+  const int c = blockIdx.x, n0 = blockIdx.y * kActRows, tid = threadIdx.x;
+  const int nimg = min(kActRows, N - n0);
+  float s = 0.f;
+  for (int im = 0; im < nimg; ++im) {  // (the image's contiguous HW plane of channel c)
+    const int64_t o0 = ((int64_t)(n0 + im) * C + c) * HW;
+    for (int h = tid; h < HW; h += 256) {
+      float v = gy[o0 + h];
+      if (relu) v = y[o0 + h] > 0.f ? v : 0.f;
+      if (g) g[o0 + h] = v;
+      s += v;
+    }
+  }
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) part[(int64_t)blockIdx.y * C + c] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+// db[c] = the chunks' partials in order
+__global__ __launch_bounds__(256) void act_bwd_sum_kernel(const float* __restrict__ part, int nchunk, int C,
+                                                          float* __restrict__ db) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+#pragma unroll 16
+  for (int k = 0; k < nchunk; ++k) s += part[(int64_t)k * C + c];  // (the loads issued ahead of the adds)
+  db[c] = s;
+}
+
 }  // namespace lvae
 
 using namespace lvae;
@@ -269,6 +338,41 @@ int lvae_step_terms_bwd(const double* g_net, const float* g_rec, const float* g_
   if (!g_mse || !g_nll || !g_kld) return -1;
   step_terms_bwd_kernel<<<1, 64, 0, (hipStream_t)stream>>>(g_net, g_rec, g_nl, g_kd, c, ks, w, use_nll, g_mse, g_nll,
                                                            g_kld);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int lvae_bias_relu_fwd_f32(float* y, const float* bias, int N, int C, int HW, void* stream) {
+  if (!y || !bias) return -1;
+  if (N < 0 || C <= 0 || HW <= 0) return -2;
+  const int64_t total = (int64_t)N * C * HW;
+  if (total == 0) return 0;
+  bias_relu_fwd_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(y, bias, C, HW, total);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+size_t lvae_act_bwd_workspace_size(int N, int C) {
+  return (size_t)((N + kActRows - 1) / kActRows) * (size_t)(C > 0 ? C : 0) * sizeof(float);
+}
+
+int lvae_act_bwd_f32(const float* gy, const float* y, int N, int C, int HW, int relu, float* g, float* db,
+                     void* workspace, void* stream) {
+  if (!gy || !db || !workspace) return -1;
+  if (relu && (!y || !g)) return -1;
+  if (N < 0 || C <= 0 || HW <= 0) return -2;
+  if (N == 0) {
+    if (hipMemsetAsync(db, 0, (size_t)C * sizeof(float), (hipStream_t)stream) != hipSuccess) return LVAE_ERR_LAUNCH;
+    return 0;
+  }
+  const int nchunk = (N + kActRows - 1) / kActRows;
+  float* part = (float*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  if (HW == 1)
+    act_bwd_rows_kernel<<<dim3((C + 63) / 64, nchunk), 256, 0, st>>>(gy, y, N, C, relu, relu ? g : nullptr, part);
+  else
+    act_bwd_chan_kernel<<<dim3(C, nchunk), 256, 0, st>>>(gy, y, N, C, HW, relu, relu ? g : nullptr, part);
+  act_bwd_sum_kernel<<<(C + 255) / 256, 256, 0, st>>>(part, nchunk, C, db);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -96,6 +96,9 @@ SIGNATURES = {
     "lvae_kl_closed_hyper_state": (_I32, [_I32, _I32, _VP, _VP, _VP]),
     "lvae_vae_loss_fwd_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_vae_loss_bwd_partials": (_SZ, [_I32]),
+    "lvae_bias_relu_fwd_f32": (_I32, [_VP, _VP, _I32, _I32, _I32, _VP]),
+    "lvae_act_bwd_workspace_size": (_SZ, [_I32, _I32]),
+    "lvae_act_bwd_f32": (_I32, [_VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_vae_loss_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _VP]),
     "lvae_reparam_fwd_f32": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),
     "lvae_reparam_bwd_f32": (_I32, [_VP, _VP, _VP, _I64, _VP, _VP]),

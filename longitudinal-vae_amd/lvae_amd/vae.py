@@ -183,6 +183,99 @@ def deconv_sigmoid(deconv, z):
     return torch.sigmoid(deconv(z))
 
 
+def _act_bwd(gy, y, relu, N, C, HW):
+    """(g, db): g = gy [y > 0] (gy itself without relu) and the bias gradient, one HIP pass
+    (lvae_act_bwd_f32, glue.hip)."""
+    from . import _lib
+    lib = _lib.lib()
+    g = torch.empty_like(gy) if relu else gy
+    db = torch.empty(C, dtype=gy.dtype, device=gy.device)
+    ws = torch.empty(lib.lvae_act_bwd_workspace_size(N, C) // 4 + 1, dtype=torch.float32, device=gy.device)
+    _lib.check(lib.lvae_act_bwd_f32(_lib.ptr(gy), _lib.ptr(y) if relu else None, N, C, HW, 1 if relu else 0,
+                                    _lib.ptr(g) if relu else None, _lib.ptr(db), _lib.ptr(ws), _lib.stream_ptr()),
+               "act_bwd")
+    return g, db
+
+
+class _LinearAct(torch.autograd.Function):
+    """relu(x W^T + b) or x W^T + b: the ConvVAE's fc layers (VAE.py:44-75).  The GEMMs stay on hipBLASLt
+    (torch.mm / addmm); bias + ReLU is one HIP pass forward (lvae_bias_relu_fwd_f32) and the backward's
+    pre-activation gradient and bias gradient one more (lvae_act_bwd_f32), in place of PyTorch's relu,
+    threshold_backward and the strided bias reduction."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu):
+        from . import _lib
+        x2 = x.contiguous()
+        B, F_ = x2.shape[0], weight.shape[0]
+        if relu:
+            y = torch.mm(x2, weight.t())
+            _lib.check(_lib.lib().lvae_bias_relu_fwd_f32(_lib.ptr(y), _lib.ptr(bias.contiguous()), B, F_, 1,
+                                                          _lib.stream_ptr()), "bias_relu_fwd")
+        else:
+            y = torch.addmm(bias, x2, weight.t())
+        ctx.relu = relu
+        ctx.save_for_backward(x2, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        gy = gy.contiguous()
+        g, db = _act_bwd(gy, y, ctx.relu, gy.shape[0], gy.shape[1], 1)
+        dx = torch.mm(g, w) if ctx.needs_input_grad[0] else None
+        dw = torch.mm(g.t(), x)
+        return dx, dw, db, None
+
+
+class _DeconvRelu(torch.autograd.Function):
+    """relu(ConvTranspose2d(x)) (VAE.py:73, 122): the transposed conv without its bias on MIOpen, then bias +
+    ReLU in place as one HIP pass; backward: the pre-activation and bias gradients in one HIP pass, the
+    input / weight gradients from MIOpen's convolution backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, output_padding, dilation, groups):
+        from . import _lib
+        y = F.conv_transpose2d(x, weight, None, stride, padding, output_padding, groups, dilation).contiguous()
+        N, C = y.shape[0], y.shape[1]
+        _lib.check(_lib.lib().lvae_bias_relu_fwd_f32(_lib.ptr(y), _lib.ptr(bias.contiguous()), N, C,
+                                                      y.shape[2] * y.shape[3], _lib.stream_ptr()), "bias_relu_fwd")
+        ctx.conf = (stride, padding, output_padding, dilation, groups)
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        stride, padding, output_padding, dilation, groups = ctx.conf
+        gy = gy.contiguous()
+        g, db = _act_bwd(gy, y, True, y.shape[0], y.shape[1], y.shape[2] * y.shape[3])
+        dx, dw, _ = torch.ops.aten.convolution_backward(g, x, w, None, list(stride), list(padding), list(dilation),
+                                                        True, list(output_padding), groups,
+                                                        [ctx.needs_input_grad[0], True, False])
+        return dx, dw, db, None, None, None, None, None
+
+
+def _f32_cuda(*ts):
+    return all(t.is_cuda and t.dtype == torch.float32 for t in ts)
+
+
+def linear_act(fc, x, relu):
+    """relu(fc(x)) / fc(x) for the fc layers: the fused bias / ReLU HIP passes for CUDA fp32 2-D inputs."""
+    if fc.bias is not None and x.dim() == 2 and _f32_cuda(x, fc.weight, fc.bias):
+        return _LinearAct.apply(x, fc.weight, fc.bias, relu)
+    y = fc(x)
+    return F.relu(y) if relu else y
+
+
+def deconv_relu(deconv, x):
+    """relu(deconv(x)) for the decoder's first transposed conv: bias + ReLU fused for CUDA fp32."""
+    if deconv.bias is not None and x.dim() == 4 and _f32_cuda(x, deconv.weight, deconv.bias):
+        return _DeconvRelu.apply(x, deconv.weight, deconv.bias, tuple(deconv.stride), tuple(deconv.padding),
+                                 tuple(deconv.output_padding), tuple(deconv.dilation), deconv.groups)
+    return F.relu(deconv(x))
+
+
 def relu_maxpool2(x):
     """pool(relu(x)) of the encoder (VAE.py:44-50): fused HIP kernel for CUDA fp32 activations."""
     if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0:
@@ -233,16 +326,16 @@ class ConvVAE(nn.Module):
     def encode(self, x):
         z = self.dropout2d_1(conv_relu_maxpool2(self.conv1, x))   # pool1(relu(conv1))
         z = self.dropout2d_2(conv_relu_maxpool2(self.conv2, z))   # pool2(relu(conv2))
-        h1 = self.dropout1(F.relu(self.fc1(z.reshape(-1, 32 * 9 * 9))))
-        h2 = self.dropout2(F.relu(self.fc21(h1)))
-        return self.fc211(h2), self.fc221(h2)
+        h1 = self.dropout1(linear_act(self.fc1, z.reshape(-1, 32 * 9 * 9), True))
+        h2 = self.dropout2(linear_act(self.fc21, h1, True))
+        return linear_act(self.fc211, h2, False), linear_act(self.fc221, h2, False)
 
     def decode(self, z):
-        x = self.dropout3(F.relu(self.fc3(z)))
-        x = self.dropout4(F.relu(self.fc31(x)))
-        x = F.relu(self.fc4(x))
+        x = self.dropout3(linear_act(self.fc3, z, True))
+        x = self.dropout4(linear_act(self.fc31, x, True))
+        x = linear_act(self.fc4, x, True)
         x = self.dropout2d_3(x.reshape(-1, 32, 9, 9))
-        x = self.dropout2d_4(F.relu(self.deconv1(x)))
+        x = self.dropout2d_4(deconv_relu(self.deconv1, x))
         return deconv_sigmoid(self.deconv2, x)
 
     def sample_latent(self, mu, log_var, eps=None):

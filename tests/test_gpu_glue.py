@@ -106,3 +106,67 @@ def test_param_pack_fused(hip):
         (Pc * W).sum().backward()
         for (n, pg), (_, pc) in zip(kg.named_parameters(), kc.named_parameters()):
             assert rel(pg.grad, pc.grad) < 1e-13, n
+
+
+@pytest.mark.parametrize("B,fin,fout,relu", [(4096, 2592, 300, True), (67, 300, 2592, True), (130, 30, 16, False),
+                                             (1, 300, 30, True)])
+def test_linear_act_fused(hip, B, fin, fout, relu):
+    """The fc layers' fused bias + ReLU (VAE.py:44-75; glue.hip bias_act): values and the input / weight /
+    bias gradients against fp64 PyTorch; ragged row counts for the 64-row partial chunks."""
+    from lvae_amd.vae import linear_act
+    torch.manual_seed(B + fout)
+    fc = torch.nn.Linear(fin, fout).cuda()
+    x = torch.randn(B, fin, device="cuda", requires_grad=True)
+    y = linear_act(fc, x, relu)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    x64 = x.detach().cpu().double().requires_grad_()
+    w64 = fc.weight.detach().cpu().double().requires_grad_()
+    b64 = fc.bias.detach().cpu().double().requires_grad_()
+    y64 = x64 @ w64.t() + b64
+    if relu:
+        y64 = torch.relu(y64)
+    (y64 * g.cpu().double()).sum().backward()
+    errs = dict(y=rel(y, y64), dx=rel(x.grad, x64.grad), dw=rel(fc.weight.grad, w64.grad), db=rel(fc.bias.grad, b64.grad))
+    print(B, fin, fout, relu, errs)
+    for k, e in errs.items():
+        assert e < 1e-4, (k, e)
+
+
+@pytest.mark.parametrize("N", [4096, 37])
+def test_deconv_relu_fused(hip, N):
+    """The decoder's relu(ConvTranspose2d(32, 16, 4, 2, 1)) (VAE.py:73, 122): bias + ReLU fused forward, the
+    pre-activation / bias gradients fused backward, MIOpen's transposed-conv backward for the rest.  Against
+    PyTorch's own GPU path (the same MIOpen calls: 1e-5) and against fp64 (1e-4) at both sizes.  (At N = 4096
+    MIOpen's Winograd solvers put dx 4.3e-2 from fp64, for PyTorch's path and this one alike; lvae_amd turns
+    them off at import: 5.8e-7.  scripts/deconv_check.py)"""
+    from lvae_amd.vae import deconv_relu
+    torch.manual_seed(N)
+    dc = torch.nn.ConvTranspose2d(32, 16, kernel_size=4, stride=2, padding=1).cuda()
+    x = torch.randn(N, 32, 9, 9, device="cuda", requires_grad=True)
+    g = torch.randn(N, 16, 18, 18, device="cuda")
+    y = deconv_relu(dc, x)
+    (y * g).sum().backward()
+    got = [y.detach().clone(), x.grad.clone(), dc.weight.grad.clone(), dc.bias.grad.clone()]
+    x.grad = None
+    dc.weight.grad = None
+    dc.bias.grad = None
+    yt = torch.relu(dc(x))
+    (yt * g).sum().backward()
+    ref = [yt.detach(), x.grad, dc.weight.grad, dc.bias.grad]
+    errs = {k: rel(a, b) for k, a, b in zip(("y", "dx", "dw", "db"), got, ref)}
+    print(N, "vs torch GPU", errs)
+    for k, e in errs.items():
+        assert e < 1e-5, (k, e)
+    x64 = x.detach().cpu().double().requires_grad_()
+    dc64 = torch.nn.ConvTranspose2d(32, 16, kernel_size=4, stride=2, padding=1).double()
+    with torch.no_grad():
+        dc64.weight.copy_(dc.weight.double().cpu())
+        dc64.bias.copy_(dc.bias.double().cpu())
+    y64 = torch.relu(dc64(x64))
+    (y64 * g.cpu().double()).sum().backward()
+    e64 = {k: rel(a, b) for k, a, b in zip(("y", "dx", "dw", "db"), got,
+                                            (y64, x64.grad, dc64.weight.grad, dc64.bias.grad))}
+    print(N, "vs fp64", e64)
+    for k, e in e64.items():
+        assert e < 1e-4, (k, e)
