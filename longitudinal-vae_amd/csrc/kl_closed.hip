@@ -330,20 +330,24 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
   if (rb_on) {
     lock.lock();
     LVAE_TRY(side_stream(sd));
-    if (!ok(hipEventRecord(sd->rbx, st))) return LVAE_ERR_LAUNCH;
   }
   {
     ProfScope ps(LVAE_PH_GRAM, st);
     LVAE_TRY(kl_gram_fill(spec, x, ldx, n, np_, L, params, noise, ws.A, ws.covflag, st));
   }
-  // the binned hyper-gradient's plan (covariates only; the reduce's lauum and the backward read its flag)
-  LVAE_TRY(kl_hyper_plan(spec, x, ldx, n, np_, L, ws.hb, ws.covflag, st));
+  // (after the fill: the side stream's plans read x and the fill's covariate flag)
+  if (rb_on && !ok(hipEventRecord(sd->rbx, st))) return LVAE_ERR_LAUNCH;
+  // the binned hyper-gradient's plan (covariates and the fill's covariate flag; the reduce's lauum and the
+  // backward read its flag): beside trtri on the side stream with the residual's plan when that runs (behind the
+  // last pivot, so after the fill), else here
+  if (!rb_on) LVAE_TRY(kl_hyper_plan(spec, x, ldx, n, np_, L, ws.hb, ws.covflag, st));
   // Y = L^-1 and log|K|: blocked Cholesky + trtri (chol_inv.hip; phases POTRF / POTRI inside); lauum
   // runs in the reduce
   LVAE_TRY(ci_factor_f32(np_, L, ws.A, ws.chol, ws.planes, ws.Kinv, ws.logdet, info, st));
   if (rb_on) {
     if (!ok(hipStreamWaitEvent(sd->s, sd->rbx, 0))) return LVAE_ERR_LAUNCH;
     LVAE_TRY(kl_resid_bins_plan(spec, x, ldx, n, np_, L, ws.rb, sd->s));
+    LVAE_TRY(kl_hyper_plan(spec, x, ldx, n, np_, L, ws.hb, ws.covflag, sd->s));
     if (!ok(hipEventRecord(sd->rb, sd->s))) return LVAE_ERR_LAUNCH;
     // join the side stream back before returning (the header's contract): the wait sits behind the
     // trtri launches already on `st`, so the plan still runs beside them; each call is self-contained

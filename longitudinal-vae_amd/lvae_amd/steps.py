@@ -62,6 +62,7 @@ class ClosedStep:
             vst.wait_stream(main)  # the previous step's updates, before the factorisation is queued
             factor = kl_closed_prefactor(self.kernel, X, self.lik, self.vae.latent_dim, main)
             enc_done = torch.cuda.Event()
+            mse_mode = self.loss_function == "mse"
             with torch.cuda.stream(vst):
                 gv = None if capturing else self.gvae
                 if gv is not None:
@@ -70,30 +71,37 @@ class ClosedStep:
                     mu, log_var = self.vae.encode(img)
                 enc_done.record(vst)
                 z = self.vae.sample_latent(mu, log_var, eps)
+                # The decoder and the recon loss run from a detached copy of z, and their backward is enqueued
+                # right here -- before the host waits for the factorisation's enqueue (~250 launches from the
+                # worker thread) and enqueues the KL -- so the decoder backward runs beside the Cholesky instead
+                # of behind the KL's host work.  Its dLoss/dz joins the KL's d/d(mu, logvar) in ONE encoder
+                # backward below (the same sums as the single backward over both loss terms).
+                zd = z.detach().requires_grad_()
                 if gv is not None:
-                    recon_loss, nll_loss = gv.decode_loss(z, img, mask)
+                    recon_loss, nll_loss = gv.decode_loss(zd, img, mask)
                 else:
-                    recon = self.vae.decode(z)
+                    recon = self.vae.decode(zd)
                     mse, nll = self.vae.loss_function(recon, img, mask)
                     recon_loss, nll_loss = mse.sum(), nll.sum()
+                rec_term = recon_loss if mse_mode else nll_loss
+                rec_term.backward()
             factor.wait_enqueued()  # (its launches on `main` all precede the wait below)
             main.wait_event(enc_done)
             mu.record_stream(main)
             log_var.record_stream(main)
             kl = KL_closed_batched(self.kernel, X, self.lik, mu, log_var, factor=factor)
             L = mu.shape[1]
-            if self.loss_function == "mse":
+            if mse_mode:
                 gp = kl.sum() / L
-                rec_term, gp_term = recon_loss, self.weight * gp
+                gp_term = self.weight * gp
             else:
                 gp = kl.sum()
-                rec_term, gp_term = nll_loss, gp
-            # The backward from the two loss terms as separate roots, called on the ConvVAE's stream:
-            # the decoder's backward then starts as soon as its forward is done, beside the KL reduce
-            # on the caller's stream, instead of behind it (a root summed on the caller's stream
-            # would hand the decoder its gradient only after everything queued there).
+                gp_term = gp
+            # The encoder backward from dLoss/dz (the decoder's) and the KL term, called on the ConvVAE's stream
+            # (the KL's backward kernels run on their forward's stream; the encoder's join them through the
+            # d/d(mu, logvar) events of elbo._KLClosedFn).
             with torch.cuda.stream(vst):
-                torch.autograd.backward([rec_term, gp_term])
+                torch.autograd.backward([z, gp_term], [zd.grad, None])
             main.wait_stream(vst)
             for t in (recon_loss, nll_loss, rec_term):
                 t.record_stream(main)

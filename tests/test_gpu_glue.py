@@ -135,11 +135,12 @@ def test_linear_act_fused(hip, B, fin, fout, relu):
 
 @pytest.mark.parametrize("N", [4096, 37])
 def test_deconv_relu_fused(hip, N):
-    """The decoder's relu(ConvTranspose2d(32, 16, 4, 2, 1)) (VAE.py:73, 122): bias + ReLU fused forward, the
-    pre-activation / bias gradients fused backward, MIOpen's transposed-conv backward for the rest.  Against
-    PyTorch's own GPU path (the same MIOpen calls: 1e-5) and against fp64 (1e-4) at both sizes.  (At N = 4096
-    MIOpen's Winograd solvers put dx 4.3e-2 from fp64, for PyTorch's path and this one alike; lvae_amd turns
-    them off at import: 5.8e-7.  scripts/deconv_check.py)"""
+    """The decoder's relu(ConvTranspose2d(32, 16, 4, 2, 1)) (VAE.py:73, 122): MIOpen's transposed conv without
+    bias, bias + ReLU fused (glue.hip bias_act) forward, the pre-activation and bias gradients fused backward.
+    The output against fp64, and the input / weight / bias gradients against fp64 through the same ReLU mask
+    (y > 0 of the GPU forward: at 21M outputs a few pre-activations sit within rounding of 0, where a flipped mask
+    is a tie-break, not an error).  MIOpen's Winograd solvers, off by default since r5, had put dx 4.3e-2 from
+    fp64 at N = 4096 (scripts/deconv_check.py)."""
     from lvae_amd.vae import deconv_relu
     torch.manual_seed(N)
     dc = torch.nn.ConvTranspose2d(32, 16, kernel_size=4, stride=2, padding=1).cuda()
@@ -147,26 +148,17 @@ def test_deconv_relu_fused(hip, N):
     g = torch.randn(N, 16, 18, 18, device="cuda")
     y = deconv_relu(dc, x)
     (y * g).sum().backward()
-    got = [y.detach().clone(), x.grad.clone(), dc.weight.grad.clone(), dc.bias.grad.clone()]
-    x.grad = None
-    dc.weight.grad = None
-    dc.bias.grad = None
-    yt = torch.relu(dc(x))
-    (yt * g).sum().backward()
-    ref = [yt.detach(), x.grad, dc.weight.grad, dc.bias.grad]
-    errs = {k: rel(a, b) for k, a, b in zip(("y", "dx", "dw", "db"), got, ref)}
-    print(N, "vs torch GPU", errs)
-    for k, e in errs.items():
-        assert e < 1e-5, (k, e)
     x64 = x.detach().cpu().double().requires_grad_()
     dc64 = torch.nn.ConvTranspose2d(32, 16, kernel_size=4, stride=2, padding=1).double()
     with torch.no_grad():
         dc64.weight.copy_(dc.weight.double().cpu())
         dc64.bias.copy_(dc.bias.double().cpu())
-    y64 = torch.relu(dc64(x64))
-    (y64 * g.cpu().double()).sum().backward()
-    e64 = {k: rel(a, b) for k, a, b in zip(("y", "dx", "dw", "db"), got,
-                                            (y64, x64.grad, dc64.weight.grad, dc64.bias.grad))}
-    print(N, "vs fp64", e64)
-    for k, e in e64.items():
-        assert e < 1e-4, (k, e)
+    pre = dc64(x64)
+    mask = (y.detach().cpu() > 0).double()
+    e_y = rel(y, torch.relu(pre))
+    (pre * mask * g.cpu().double()).sum().backward()
+    errs = dict(y=e_y, dx=rel(x.grad, x64.grad), dw=rel(dc.weight.grad, dc64.weight.grad),
+                db=rel(dc.bias.grad, dc64.bias.grad))
+    print(N, errs)
+    for k, e in errs.items():
+        assert e < 1e-5, (k, e)
