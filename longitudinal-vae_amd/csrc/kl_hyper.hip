@@ -26,7 +26,8 @@
 // Conditions (hb_plan_kernel, on the device; otherwise `on` = 0 and the S GEMM + table adjoint run as before):
 // the table path's (covariate flag 2); the Cat gate covariate of the widest range (> 4 values) is "big" (the id),
 // the other Cat gates span <= 16 values; its values non-decreasing over the points (runs contiguous) with runs of
-// <= 64 points; far binnings <= 4, with <= 128 bins in all and sum nbins^2 <= 4096; <= 8 parameter slots on near
+// <= 64 points; far binnings <= 4, with <= 128 bins in all, <= 4 blocks of 32 bins and sum nbins^2 <= 4096; <= 8
+// parameter slots on near
 // components; Bin gate values within 64 of their minimum, distance values within 65535 of theirs (the row keys);
 // on the host: the slab kernel's LDS fits (hb_slab_lds).
 #include "blkinv.hpp"
@@ -41,7 +42,8 @@ constexpr int kHbBins2 = 4096;  // sum over binnings of nbins^2
 constexpr int kHbRun = 64;      // longest run of the big covariate
 constexpr int kHbSmall = 16;    // Cat gate covariates other than the big one span at most this many values
 constexpr int kHbSmallest = 4;  // the big covariate spans more than this many values
-constexpr int kHbNear = 8;      // parameter slots of the near components
+constexpr int kHbNear = 4;      // parameter slots of the near components
+constexpr int kHbBlk = 4;       // 32-bin blocks over the far binnings (two one-hot GEMM items per wave of four)
 constexpr int kHbT = 64;        // row tile = column slab
 constexpr int kHbTP = 68;       // LDS pitch of a tile row (floats: 16-B aligned rows, 16 rows on distinct banks)
 // the per-(dim, slab) partial record (doubles): M [nb2], Q [nb2] (at kHbBins2), then the tail: the near slots' S
@@ -71,6 +73,7 @@ struct HbWs {
   double* part;   // [L][np / 64][kHbPart] per-slab partials
   float* tab;     // [L][kTabMaxBwdLds] the derivative tables per dim (hb_tab_kernel)
   hb_u32x4* rkey;    // [np] per point: gate values (6 bits each, the big gate's 0), distance values (16 bits each)
+  double* hscr;      // [L][np / 64][kHbBins][64] the slab pass's H per workgroup (its epilogue's input)
   size_t bytes;
   HbWs(char* base, int np_, int L) {
     size_t off = 0;
@@ -86,6 +89,7 @@ struct HbWs {
     part = (double*)take((size_t)L * (np_ / kHbT) * kHbPart * sizeof(double));
     tab = (float*)take((size_t)L * kTabMaxBwdLds * sizeof(float));
     rkey = (hb_u32x4*)take((size_t)np_ * sizeof(hb_u32x4));
+    hscr = (double*)take((size_t)L * (np_ / kHbT) * kHbBins * kHbT * sizeof(double));
     bytes = off;
   }
 };
@@ -176,6 +180,11 @@ __global__ __launch_bounds__(1024) void hb_plan_kernel(GramTab tb, const double*
       p.cbin[r] = g;
     }
     if (p.nbins > kHbBins || p.nb2 > kHbBins2) f = 1;
+    {  // the slab pass's one-hot items: 32-bin blocks of every binning, at most kHbBlk
+      int nblk = 0;
+      for (int g = 0; g < p.nbin; ++g) nblk += (p.bn[g] + 31) / 32;
+      if (nblk > kHbBlk) f = 1;
+    }
     for (int k = 0; k < tb.pbeg[tb.ng] && !f; ++k)
       if (p.cbin[tb.pcomp[tb.porder[k]]] < 0) {
         if (p.nnear == kHbNear) f = 1;
@@ -351,17 +360,20 @@ __global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n
 // tile by tile, and writes its partial record: M_g = H_g V H_g^T, Q_g = H_g Phi_g (the slab's columns), the near
 // runs' S parts per near slot, the slab's part of tr S and of a = Phi^T alpha.
 //
-//   tile store: every thread splits its 4 rows x 2 columns exactly into three bf16 pieces (round to nearest:
-//     hi + mid + lo = the fp32 value) and writes them column-major into three planes (8-row chunks swizzled by
-//     the column: conflict-free 16-byte reads), the fp32 rows for the near runs, and its tr S part
+// 256 threads and < 80 KB of LDS: two workgroups per CU, whose barriers and HBM round trips overlap.
+//   tile store: every thread splits its 8 rows x 2 columns exactly into three bf16 pieces (round to nearest:
+//     hi + mid + lo = the fp32 value) and writes each column's 8-row chunk of each piece as one 16-byte store into
+//     column-major planes (chunks swizzled by the column: conflict-free 16-byte reads and writes), the fp32 rows
+//     (x V^(1/2)) for the near runs, and its tr S part
 //   H_g += Phi_g(tile)^T K^-1(tile, slab): one-hot GEMMs on v_mfma_f32_32x32x16_bf16, item = (32-bin block,
-//     32-column block), at most two items per wave held in the accumulators across tiles (products exact, fp32
-//     sums over 4 tiles, then folded into H in LDS, fp64, each entry owned by one lane)
-//   near runs ending in the tile: 16 x 16 blocks of X V X^T on v_mfma_f32_16x16x4f32 (the fp32 tile holds X V^(1/2),
-//     v > 0), contracted with the near
+//     32-column block), two items per wave (the plan allows at most 4 blocks) held in the accumulators across
+//     tiles (products exact, fp32 sums over 4 tiles, then folded into fp64 registers); H goes to a per-workgroup
+//     scratch in the workspace for the epilogue only
+//   near runs ending in the tile: 16 x 16 blocks of X V X^T on v_mfma_f32_16x16x4f32, contracted with the near
 //     slots' tables through the pair codes (hb_pair_code, from the rows' keys); block items dealt from the last
-//     wave down (the H items from the first up)
-// Tiles arrive two ahead in registers (two prefetch sets, the loop unrolled by two, no branch around a load).
+//     wave down
+// The next tile arrives in registers under the current one's work (no branch around a load); the two workgroups
+// of a CU cover each other's HBM round trips and barriers.
 // ------------------------------------------------------------------------------------------
 __device__ inline int hb_row_slot(int row) { return (row >> 6) & 1; }
 
@@ -382,14 +394,13 @@ typedef float hb_f32x2 __attribute__((ext_vector_type(2)));
 typedef float hb_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 hb_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 hb_bf16x2 __attribute__((ext_vector_type(2)));
-constexpr int kHbBlk = 7;  // 32-bin blocks over the binnings (sum ceil(nb_g / 32) with sum nb_g <= 128, <= 4 binnings)
-constexpr int kHbSlabThreads = 512, kHbSlabWaves = kHbSlabThreads / 64;  // (2 waves per SIMD)
+constexpr int kHbSlabThreads = 256, kHbSlabWaves = kHbSlabThreads / 64;
 constexpr int kHbFold = 4;  // tiles summed in fp32 by the accumulators before the fp64 fold
 
 struct HbPre {        // one tile's prefetch
-  hb_f32x2 pk[4];     // K^-1 rows 4 (tid >> 5) + u, columns 2 (tid & 31) + 0, 1
+  hb_f32x2 pk[8];     // K^-1 rows 8 (tid >> 5) + u, columns 2 (tid & 31) + 0, 1
   int pbn;            // wave w < nbin: bin of row lane in binning w
-  int pre_, prs;      // run end / start of row lane (wave 0's)
+  int pre_, prs;      // run end / start of row lane
   hb_u32x4 key;       // key of row lane (wave 0's)
 };
 
@@ -403,10 +414,25 @@ __device__ inline float hb_bf_hi(unsigned u) { return __uint_as_float(u & 0xffff
 // dword offset in a bf16 plane of (column c, 8-row chunk k): 32 dwords per column, chunks swizzled by (c >> 1) & 7
 __device__ inline int hb_pl_off(int c, int k) { return c * 32 + ((k ^ ((c >> 1) & 7)) << 2); }
 
-__global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbWs ws, int n, int np_,
-                                                                 const float* __restrict__ Kinv,
-                                                                 const float* __restrict__ vv,
-                                                                 const double* __restrict__ alpha, int dbg) {
+// three bf16 pieces of 8 fp32 values, packed by pairs (rows 2 k, 2 k + 1 in dword k)
+__device__ inline void hb_split8(const float* a, hb_u32x4& hi, hb_u32x4& mid, hb_u32x4& lo) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float x0 = a[2 * k], x1 = a[2 * k + 1];
+    const unsigned h = hb_pk_bf16(x0, x1);
+    const float r0 = x0 - hb_bf_lo(h), r1 = x1 - hb_bf_hi(h);
+    const unsigned m = hb_pk_bf16(r0, r1);
+    const float s0 = r0 - hb_bf_lo(m), s1 = r1 - hb_bf_hi(m);
+    hi[k] = h;
+    mid[k] = m;
+    lo[k] = hb_pk_bf16(s0, s1);
+  }
+}
+
+__global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, HbWs ws, int n, int np_,
+                                                                    const float* __restrict__ Kinv,
+                                                                    const float* __restrict__ vv,
+                                                                    const double* __restrict__ alpha, int dbg) {
   __shared__ HbDev d;
   __shared__ __attribute__((aligned(16))) float T[2][kHbT * kHbTP];  // fp32 row tiles of the window (near runs)
   __shared__ __attribute__((aligned(16))) unsigned Pw[3][kHbT * 32];  // the current tile's bf16 planes, column-major
@@ -418,23 +444,20 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
   __shared__ int sgrp[kHbNear];
   __shared__ int sbg[kHbBlk], sbb[kHbBlk], nbk;  // 32-bin blocks: binning, block index
   __shared__ double red[kHbSlabWaves][kHbNear + 1];
-  extern __shared__ double hdyn[];              // H [kHbBins][64] (fp64, folded every kHbFold tiles), then the near tables
+  extern __shared__ float tab[];                // the near slots' tables
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, J = blockIdx.x, l = blockIdx.y, J0 = J * kHbT;
   if (tid == 0) d = *ws.dev;
   __syncthreads();
   if (!d.on) return;  // (uniform)
-  double* H = hdyn;
-  float* tab = reinterpret_cast<float*>(hdyn + kHbBins * kHbT);
   const int tstride = (1 << tb.nbits) * kTabR;
   if (tid < kHbT) {
     vs[tid] = vv[(int64_t)l * np_ + J0 + tid];
     acol[tid] = alpha[(int64_t)l * np_ + J0 + tid];
   }
-  for (int e = tid; e < d.nbins * kHbT; e += kHbSlabThreads) H[e] = 0.0;
   for (int e = tid; e < d.nbin * kHbT; e += kHbSlabThreads)
     cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
   hb_near_tables(tb, d, ws.tab + (int64_t)l * kTabMaxBwdLds, tstride, tab, sgrp);
-  if (tid == 0) {  // the 32-bin blocks of the binnings in order
+  if (tid == 0) {  // the 32-bin blocks of the binnings in order (the plan keeps them <= kHbBlk)
     int t = 0;
     for (int g = 0; g < d.nbin; ++g)
       for (int bb = 0; bb * 32 < d.bn[g] && t < kHbBlk; ++bb, ++t) {
@@ -447,11 +470,9 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
   const float* K = Kinv + (int64_t)l * np_ * np_;
   const int nbin = d.nbin, nnear = d.nnear, bigon = d.big >= 0, nitem = 2 * nbk;
   const unsigned catbits = hb_catbits(tb);
-  // H items (item = 2 block + column block): the column block w & 1 for both of a wave's items
+  // H items (item = 2 block + column block): wave w takes w and w + 4, both of column block w & 1
   const int cb = w & 1, hh = lane >> 5, col = 32 * cb + (lane & 31);
-  // items: waves 0-3 take w and w + 4, waves 4-7 take w + 4 and w + 8 (two per wave sharing the B operands; with
-  // <= 8 items waves 4-7 have none and take the near runs first)
-  const int i0 = w < 4 ? w : w + 4, i1 = i0 + 4;
+  const int i0 = w, i1 = w + kHbSlabWaves;
   const bool it0 = i0 < nitem, it1 = i1 < nitem;
   int g0 = 0, b00 = 0, g1 = 0, b01 = 0;
   if (it0) {
@@ -463,80 +484,76 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
     b01 = 32 * sbb[i1 >> 1];
   }
   hb_f32x16 acc0 = {}, acc1 = {};
-  // H += acc (rows b0 + (e & 3) + 8 (e >> 2) + 4 hh of binning g, column col), acc = 0
-  auto hb_fold = [&](hb_f32x16& acc, int g, int b0) {
-    const int nb = d.bn[g];
-    double* hc = H + (int64_t)d.boff[g] * kHbT + col;
-    double hv[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-      hv[e] = hc[(b < nb ? b : 0) * kHbT];
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-      if (b < nb) hc[b * kHbT] = hv[e] + (double)acc[e];
-      acc[e] = 0.f;
-    }
-  };
+  // H lives in the workgroup's scratch (fp64): the accumulators are added to it every kHbFold tiles by atomics
+  // without return (no wait; one lane per entry, so the adds apply in program order: deterministic), the first
+  // fold storing
+  double* Hs = ws.hscr + ((int64_t)l * (np_ / kHbT) + J) * kHbBins * kHbT;
   double nacc[kHbNear];
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) nacc[k] = 0.0;
   double tS = 0.0;
-  const int cp = tid & 31, i4 = tid >> 5;  // this thread's tile part: columns 2 cp + 0, 1; rows 4 i4 + 0..3
-  const float v0 = vs[2 * cp], v1 = vs[2 * cp + 1], r0 = sqrtf(v0), r1 = sqrtf(v1);
+  const int cp = tid & 31, i8 = tid >> 5;  // this thread's tile part: columns 2 cp + 0, 1; rows 8 i8 + 0..7
+  const float v0 = vs[2 * cp], v1 = vs[2 * cp + 1], r0 = sqrtf(v0), r1 = sqrtf(v1);  // (v = exp(log var) > 0)
   const int nt = np_ / kHbT;
 
   auto fetch = [&](int I, HbPre& p) {
     const int I0 = I * kHbT;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 8; ++u)
       p.pk[u] = __builtin_nontemporal_load(
-          reinterpret_cast<const hb_f32x2*>(K + (int64_t)(I0 + 4 * i4 + u) * np_ + J0 + 2 * cp));
+          reinterpret_cast<const hb_f32x2*>(K + (int64_t)(I0 + 8 * i8 + u) * np_ + J0 + 2 * cp));
     p.pbn = (int)ws.pbin[(size_t)(w < nbin ? w : 0) * np_ + I0 + lane];  // (used by waves w < nbin only)
     p.pre_ = ws.re[I0 + lane];
     p.prs = ws.rs[I0 + lane];
     p.key = ws.rkey[I0 + lane];
   };
 
-  unsigned long long tsec[4] = {0, 0, 0, 0};
-  auto body = [&](int I, const int sl, HbPre& p) {
+  auto fold = [&](hb_f32x16& acc, int g, int b0, bool first) {
+    const int nb = d.bn[g];
+    double* hc = Hs + (int64_t)d.boff[g] * kHbT + col;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int b = b0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+      if (b < nb) {
+        if (first) hc[b * kHbT] = (double)acc[e];
+        else unsafeAtomicAdd(hc + b * kHbT, (double)acc[e]);
+      }
+      acc[e] = 0.f;
+    }
+  };
+
+  auto body = [&](int I, int sl, HbPre& p) {
     const int I0 = I * kHbT;
-    unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0;
-    HB_STAMP(st0);
-    {  // the tile into LDS: fp32 rows, the bf16 planes; the tr S part (sum_m v_m (K^-1_im)^2)
+    {  // the tile into LDS: fp32 rows x V^(1/2), the bf16 planes; the tr S part (sum_m v_m (K^-1_im)^2)
       float ts = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const hb_f32x2 sv = {p.pk[u][0] * r0, p.pk[u][1] * r1};  // (X V^(1/2), v = exp(log var) > 0)
-        *reinterpret_cast<hb_f32x2*>(&T[sl][(4 * i4 + u) * kHbTP + 2 * cp]) = sv;
-        ts += p.pk[u][0] * p.pk[u][0] * v0 + p.pk[u][1] * p.pk[u][1] * v1;
+      for (int u = 0; u < 8; ++u) {
+        const hb_f32x2 sv = {p.pk[u][0] * r0, p.pk[u][1] * r1};
+        *reinterpret_cast<hb_f32x2*>(&T[sl][(8 * i8 + u) * kHbTP + 2 * cp]) = sv;
+        ts += sv[0] * sv[0] + sv[1] * sv[1];
       }
       tS += (double)ts;
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const float a0 = p.pk[0][c], a1 = p.pk[1][c], a2 = p.pk[2][c], a3 = p.pk[3][c];
-        const unsigned h01 = hb_pk_bf16(a0, a1), h23 = hb_pk_bf16(a2, a3);
-        const float r0 = a0 - hb_bf_lo(h01), r1 = a1 - hb_bf_hi(h01), r2 = a2 - hb_bf_lo(h23), r3 = a3 - hb_bf_hi(h23);
-        const unsigned m01 = hb_pk_bf16(r0, r1), m23 = hb_pk_bf16(r2, r3);
-        const float s0 = r0 - hb_bf_lo(m01), s1 = r1 - hb_bf_hi(m01), s2 = r2 - hb_bf_lo(m23), s3 = r3 - hb_bf_hi(m23);
-        const unsigned o01 = hb_pk_bf16(s0, s1), o23 = hb_pk_bf16(s2, s3);
-        const int off = hb_pl_off(2 * cp + c, i4 >> 1) + 2 * (i4 & 1);
-        *reinterpret_cast<uint2*>(&Pw[0][off]) = make_uint2(h01, h23);
-        *reinterpret_cast<uint2*>(&Pw[1][off]) = make_uint2(m01, m23);
-        *reinterpret_cast<uint2*>(&Pw[2][off]) = make_uint2(o01, o23);
+        float a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = p.pk[u][c];
+        hb_u32x4 hi, mid, lo;
+        hb_split8(a, hi, mid, lo);
+        const int off = hb_pl_off(2 * cp + c, i8);
+        *reinterpret_cast<hb_u32x4*>(&Pw[0][off]) = hi;
+        *reinterpret_cast<hb_u32x4*>(&Pw[1][off]) = mid;
+        *reinterpret_cast<hb_u32x4*>(&Pw[2][off]) = lo;
       }
     }
     if (w < nbin) rbin[w][lane] = (uint8_t)p.pbn;
     if (w == 0) rk[sl][lane] = p.key;  // the rows' keys
-    // the runs of the big covariate ending in this tile, in every wave's registers (its own copies of the run
-    // bounds): lane e set = a run ends at row I0 + e, its start in lane e of rstart
+    // the runs of the big covariate ending in this tile, in every wave's registers: lane e set = a run ends at
+    // row I0 + e, its start in lane e of rstart
     const unsigned long long runmask = __ballot(bigon && I0 + lane < n && p.pre_ == I0 + lane + 1);
     const int rstart = p.prs;
     __syncthreads();
-    HB_STAMP(st1);
-    fetch(I + 2 < nt ? I + 2 : nt - 1, p);  // (in flight under the next two tiles' work; the last two: a dummy)
+    fetch(I + 1 < nt ? I + 1 : nt - 1, p);  // (in flight under this tile's work and the other workgroup's)
     if (!(dbg & 1) && it0) {
       auto onehot = [&](int g, int b0, int ks) {  // A operand: [bin b0 + (lane & 31)][rows 16 ks + 8 hh + 0..7]
         const unsigned mybin = (unsigned)(b0 + (lane & 31));
@@ -568,12 +585,11 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh, acc1, 0, 0, 0);
         }
       }
-      if ((I & (kHbFold - 1)) == kHbFold - 1) {  // fold the accumulators into H (fp64, LDS; entries owned by lane)
-        hb_fold(acc0, g0, b00);
-        if (it1) hb_fold(acc1, g1, b01);
+      if ((I & (kHbFold - 1)) == kHbFold - 1) {  // fold the accumulators into H (fp64, the scratch)
+        fold(acc0, g0, b00, I == kHbFold - 1);
+        if (it1) fold(acc1, g1, b01, I == kHbFold - 1);
       }
     }
-    HB_STAMP(st2);
     // near runs ending in this tile: 16 x 16 blocks (bi, bj) of X V X^T, items dealt from the last wave down
     if (!(dbg & 2)) {
       const int wr = kHbSlabWaves - 1 - w;
@@ -590,7 +606,7 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
           const float* ta = &T[hb_row_slot(ra)][(ra & 63) * kHbTP];
           const float* tb2 = &T[hb_row_slot(rb)][(rb & 63) * kHbTP];
           bi_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          if (!(dbg & 16)) {  // (two accumulators: half the dependent chain; the operands all read first)
+          {  // (two accumulators: half the dependent chain; the operands all read first)
             float av[16], bv[16];
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
@@ -606,7 +622,6 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] += acc2[q];
           }
-          if (dbg & 8) continue;
           // the lane's 4 pairs (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li); pairs outside the run: rows of
           // the run (clamped), weight 0 (no branch)
           const hb_u32x4 kj = rk[hb_row_slot(rb)][rb & 63];
@@ -627,26 +642,16 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
         gi0 += n2;
       }
     }
-    HB_STAMP(st3);
-    __syncthreads();  // every reader of slot sl, the planes, the bins, the run list done before the next store
-    HB_STAMP(st4);
-    tsec[0] += st1 - st0;
-    tsec[1] += st2 - st1;
-    tsec[2] += st3 - st2;
-    tsec[3] += st4 - st3;
+    __syncthreads();  // every reader of slot sl, the planes, the bins, the run keys done before the next store
   };
 
-  HbPre pa, pb;
+  HbPre pa;
   fetch(0, pa);
-  fetch(1, pb);  // (nt >= 4)
-  for (int I = 0; I < nt; I += 2) {  // (nt even: np % 256 == 0)
-    body(I, 0, pa);
-    body(I + 1, 1, pb);
-  }
-  if (it0 && (nt & (kHbFold - 1))) {  // the last fold (nt a multiple of 4: nothing left)
-    hb_fold(acc0, g0, b00);
-    if (it1) hb_fold(acc1, g1, b01);
-  }
+  for (int I = 0; I < nt; ++I) body(I, I & 1, pa);
+  // (nt is a multiple of 4 = kHbFold: every tile folded; the scratch's stores and atomics complete and visible to
+  // the workgroup before its epilogue reads them)
+  __builtin_amdgcn_s_waitcnt(0);  // (vmcnt / lgkmcnt / expcnt 0: this wave's stores and atomics done)
+  __threadfence_block();
   __syncthreads();
   // Q_g[b][b'] = sum over the slab's columns m in bin b' of H_g[b][m]: thread (g, b) owns row b (LDS scratch = T);
   // a part: thread (g, b) sums alpha over the slab's columns in bin b
@@ -654,18 +659,19 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
   for (int e = tid; e < d.nb2; e += kHbSlabThreads) Qs[e] = 0.0;
   __syncthreads();
   double* out = ws.part + ((int64_t)l * nt + J) * kHbPart;
-  if (tid < d.nbins) {
+  for (int tb2 = tid; tb2 < d.nbins; tb2 += kHbSlabThreads) {
     int g = 0;
-    while (g + 1 < nbin && tid >= d.boff[g + 1]) ++g;
-    const int b = tid - d.boff[g], nb = d.bn[g];
+    while (g + 1 < nbin && tb2 >= d.boff[g + 1]) ++g;
+    const int b = tb2 - d.boff[g], nb = d.bn[g];
     double* qrow = Qs + d.b2off[g] + b * nb;
+    const double* hr = Hs + (int64_t)tb2 * kHbT;
     double as = 0.0;
     for (int m = 0; m < kHbT; ++m) {
       const int bc = cbin[g][m];
-      if (bc != 255) qrow[bc] += H[tid * kHbT + m];
+      if (bc != 255) qrow[bc] += hr[m];
       if (bc == b) as += acol[m];
     }
-    out[kHbA + tid] = as;
+    out[kHbA + tb2] = as;
   }
   __syncthreads();
   for (int e = tid; e < d.nb2; e += kHbSlabThreads) out[kHbBins2 + e] = Qs[e];
@@ -675,8 +681,8 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
     for (int item = w; item < nb16 * nb16; item += kHbSlabWaves) {
       const int bi = item / nb16, bj = item % nb16, li = lane & 15, lk = lane >> 4;
       const int ba = 16 * bi + li, bb = 16 * bj + li;
-      const double* ha = H + (int64_t)(d.boff[g] + (ba < nb ? ba : 0)) * kHbT;
-      const double* hb = H + (int64_t)(d.boff[g] + (bb < nb ? bb : 0)) * kHbT;
+      const double* ha = Hs + (int64_t)(d.boff[g] + (ba < nb ? ba : 0)) * kHbT;
+      const double* hb = Hs + (int64_t)(d.boff[g] + (bb < nb ? bb : 0)) * kHbT;
       bi_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
       for (int s4 = 0; s4 < kHbT; s4 += 4) {
@@ -692,10 +698,6 @@ __global__ __launch_bounds__(kHbSlabThreads) void hb_slab_kernel(GramTab tb, HbW
       }
     }
   }
-#ifdef LVAE_HB_STAMP
-  if (lane == 0 && l == 0 && (J == 0 || J == 17))
-    printf("hbstamp J %d w %d store+bar %llu H %llu near %llu bar %llu\n", J, w, tsec[0], tsec[1], tsec[2], tsec[3]);
-#endif
   // the near slots' S parts and tr S's part: the waves' sums in a fixed order
 #pragma unroll
   for (int k = 0; k < kHbNear; ++k) {
@@ -835,8 +837,8 @@ static size_t hb_slab_lds(const GramTab& tb) {
     stat = a.sharedSizeBytes;
   }
   const int ns = tb.pbeg[tb.ng] < kHbNear ? tb.pbeg[tb.ng] : kHbNear;
-  const size_t dyn = (size_t)kHbBins * kHbT * sizeof(double) + (size_t)ns * (1 << tb.nbits) * kTabR * sizeof(float);
-  return stat + dyn <= 160 * 1024 ? dyn : 0;
+  const size_t dyn = (size_t)ns * (1 << tb.nbits) * kTabR * sizeof(float);
+  return stat + dyn <= 160 * 1024 ? (dyn ? dyn : 4) : 0;
 }
 
 // the host's part of the conditions: the table family, the route enabled, the slab kernel's LDS fits
@@ -869,7 +871,7 @@ int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   GramTab tb;
   if (!hb_host_ok(spec, tb)) return 0;
   const size_t tabb = (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
-  const size_t sdyn = hb_slab_lds(tb), ndyn = sdyn - (size_t)kHbBins * kHbT * sizeof(double);
+  const size_t sdyn = hb_slab_lds(tb), ndyn = sdyn;
   const int nt = np_ / kHbT;
   hb_tab_kernel<<<dim3((unsigned)((tabb / sizeof(float) + 255) / 256), L), 256, 0, st>>>(tb, ws, params);
   hb_near_kernel<<<dim3(nt, L), 256, ndyn, st>>>(tb, ws, n, np_, Kinv, alpha);
