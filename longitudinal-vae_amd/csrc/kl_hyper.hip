@@ -34,6 +34,8 @@
 #include "gram_tab.hpp"
 #include "prof.hpp"
 
+#include <vector>
+
 namespace lvae {
 
 constexpr int kHbMaxBin = 4;    // far binnings
@@ -46,6 +48,8 @@ constexpr int kHbNear = 4;      // parameter slots of the near components
 constexpr int kHbBlk = 4;       // 32-bin blocks over the far binnings (two one-hot GEMM items per wave of four)
 constexpr int kHbT = 64;        // row tile = column slab
 constexpr int kHbTP = 68;       // LDS pitch of a tile row (floats: 16-B aligned rows, 16 rows on distinct banks)
+constexpr int kHbNB = 24;       // 16 x 16 blocks of a slab's near window (runs ending in the slab: at most 24)
+constexpr int kHbNQ = kHbNB / 4;  // near blocks per wave
 // the per-(dim, slab) partial record (doubles): M [nb2], Q [nb2] (at kHbBins2), then the tail: the near slots' S
 // parts, tr S, the near slots' K^-1 - alpha alpha^T parts (hb_near_kernel, record of row tile I), a = Phi^T alpha
 constexpr int kHbNearS = 2 * kHbBins2;
@@ -74,6 +78,7 @@ struct HbWs {
   float* tab;     // [L][kTabMaxBwdLds] the derivative tables per dim (hb_tab_kernel)
   hb_u32x4* rkey;    // [np] per point: gate values (6 bits each, the big gate's 0), distance values (16 bits each)
   double* hscr;      // [L][np / 64][kHbBins][64] the slab pass's H per workgroup (its epilogue's input)
+  double* nscr;      // [L][np / 64][kHbNB][16][16] the slab pass's near S blocks per workgroup (likewise)
   size_t bytes;
   HbWs(char* base, int np_, int L) {
     size_t off = 0;
@@ -90,6 +95,7 @@ struct HbWs {
     tab = (float*)take((size_t)L * kTabMaxBwdLds * sizeof(float));
     rkey = (hb_u32x4*)take((size_t)np_ * sizeof(hb_u32x4));
     hscr = (double*)take((size_t)L * (np_ / kHbT) * kHbBins * kHbT * sizeof(double));
+    nscr = (double*)take((size_t)L * (np_ / kHbT) * kHbNB * 256 * sizeof(double));
     bytes = off;
   }
 };
@@ -363,19 +369,21 @@ __global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n
 // 256 threads and < 80 KB of LDS: two workgroups per CU, whose barriers and HBM round trips overlap.
 //   tile store: every thread splits its 8 rows x 2 columns exactly into three bf16 pieces (round to nearest:
 //     hi + mid + lo = the fp32 value) and writes each column's 8-row chunk of each piece as one 16-byte store into
-//     column-major planes (chunks swizzled by the column: conflict-free 16-byte reads and writes), the fp32 rows
-//     (x V^(1/2)) for the near runs, and its tr S part
+//     column-major planes (chunks swizzled by the column: conflict-free 16-byte reads and writes), the fp32 tile
+//     (x V^(1/2) of its ROWS, column-major) for the near runs, and its tr S part
 //   H_g += Phi_g(tile)^T K^-1(tile, slab): one-hot GEMMs on v_mfma_f32_32x32x16_bf16, item = (32-bin block,
 //     32-column block), two items per wave (the plan allows at most 4 blocks) held in the accumulators across
-//     tiles (products exact, fp32 sums over 4 tiles, then folded into fp64 registers); H goes to a per-workgroup
-//     scratch in the workspace for the epilogue only
-//   near runs ending in the tile: 16 x 16 blocks of X V X^T on v_mfma_f32_16x16x4f32, contracted with the near
-//     slots' tables through the pair codes (hb_pair_code, from the rows' keys); block items dealt from the last
-//     wave down
-// The next tile arrives in registers under the current one's work (no branch around a load); the two workgroups
-// of a CU cover each other's HBM round trips and barriers.
+//     4 tiles (products exact), then added to the workgroup's fp64 H in the workspace
+//   near runs: the workgroup owns the runs ENDING in its columns; K^-1 is symmetric, so a run's S block
+//     X_run V X_run^T = sum over all rows m of K^-1(m, run)^T v_m K^-1(m, run) accumulates from the column slab
+//     itself, tile by tile: the 16 x 16 blocks of the run window's columns (the slab, plus the previous slab's
+//     columns for a run that starts there, loaded in that case only) on v_mfma_f32_16x16x4f32 (k = 16 rows per
+//     lane group: 16-byte LDS reads), in fp32 accumulators for 4 tiles, then added to fp64 blocks in the
+//     workspace; the pair codes and table contraction run ONCE per pair in the epilogue, not per tile
+// H and the near blocks reach the workspace by atomics without return (no wait; one lane per entry, so they
+// apply in program order: deterministic).  The next tile arrives in registers under the current one's work
+// (no branch around a load); the two workgroups of a CU cover each other's HBM round trips and barriers.
 // ------------------------------------------------------------------------------------------
-__device__ inline int hb_row_slot(int row) { return (row >> 6) & 1; }
 
 #ifdef LVAE_HB_STAMP  // (diagnostic builds only: per-section cycle stamps of the slab pass, printed by workgroup (0, 0))
 #define HB_STAMP(t)                                                                   \
@@ -391,6 +399,7 @@ __device__ inline int hb_row_slot(int row) { return (row >> 6) & 1; }
 #endif
 
 typedef float hb_f32x2 __attribute__((ext_vector_type(2)));
+typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
 typedef float hb_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 hb_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 hb_bf16x2 __attribute__((ext_vector_type(2)));
@@ -400,8 +409,7 @@ constexpr int kHbFold = 4;  // tiles summed in fp32 by the accumulators before t
 struct HbPre {        // one tile's prefetch
   hb_f32x2 pk[8];     // K^-1 rows 8 (tid >> 5) + u, columns 2 (tid & 31) + 0, 1
   int pbn;            // wave w < nbin: bin of row lane in binning w
-  int pre_, prs;      // run end / start of row lane
-  hb_u32x4 key;       // key of row lane (wave 0's)
+  hb_f32x4 vr[2];     // v of rows 8 (tid >> 5) + 0 .. 7 (the near runs' row weights)
 };
 
 __device__ inline unsigned hb_pk_bf16(float a, float b) {  // (round to nearest even: v_cvt_pk_bf16_f32)
@@ -434,13 +442,20 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
                                                                     const float* __restrict__ vv,
                                                                     const double* __restrict__ alpha, int dbg) {
   __shared__ HbDev d;
-  __shared__ __attribute__((aligned(16))) float T[2][kHbT * kHbTP];  // fp32 row tiles of the window (near runs)
+  // the near window's fp32 columns x V^(1/2) of the tile's rows, column-major [window column][row]: columns
+  // 0 .. 63 the previous slab's (a run starting there only), 64 .. 127 this slab's
+  __shared__ __attribute__((aligned(16))) float Tc[2 * kHbT * kHbTP];
   __shared__ __attribute__((aligned(16))) unsigned Pw[3][kHbT * 32];  // the current tile's bf16 planes, column-major
   __shared__ __attribute__((aligned(8))) uint8_t rbin[kHbMaxBin][kHbT];  // bins of the current tile's rows
   __shared__ uint8_t cbin[kHbMaxBin][kHbT];     // bins of the slab's columns
   __shared__ float vs[kHbT];                    // v of the slab's columns
   __shared__ double acol[kHbT];                 // alpha of the slab's columns
-  __shared__ hb_u32x4 rk[2][kHbT];              // the window's row keys
+  __shared__ hb_u32x4 ckey[2 * kHbT];           // the near window's keys
+  __shared__ int rstart[kHbT];                   // start of the run ending at the slab's column e
+  __shared__ unsigned long long runends;        // bit e: a run ends at column J0 + e
+  __shared__ int nblk, nspan;                    // near window: 16 x 16 blocks (lower), a run from the previous slab
+  __shared__ uint8_t blist[kHbNB];               // block t: (bi << 3) | bj, bi >= bj (window column blocks)
+  __shared__ int8_t blkid[64];                   // (bi << 3) | bj -> t
   __shared__ int sgrp[kHbNear];
   __shared__ int sbg[kHbBlk], sbb[kHbBlk], nbk;  // 32-bin blocks: binning, block index
   __shared__ double red[kHbSlabWaves][kHbNear + 1];
@@ -457,6 +472,43 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
   for (int e = tid; e < d.nbin * kHbT; e += kHbSlabThreads)
     cbin[e / kHbT][e % kHbT] = ws.pbin[(size_t)(e / kHbT) * np_ + J0 + e % kHbT];
   hb_near_tables(tb, d, ws.tab + (int64_t)l * kTabMaxBwdLds, tstride, tab, sgrp);
+  if (tid < 2 * kHbT) {  // the near window's keys (columns J0 - 64 .. J0 + 63)
+    const int c = J0 - kHbT + tid;
+    ckey[tid] = c >= 0 ? ws.rkey[c] : hb_u32x4{0u, 0u, 0u, 0u};
+  }
+  if (w == 0) {
+    // the runs ending in the slab's columns (lane e: column J0 + e) and the lower 16 x 16 blocks of the window
+    // their pairs touch: a run [s, c] (<= 64 points) covers window column blocks (s - J0 + 64) / 16 .. (c - J0 +
+    // 64) / 16; at most one run starts in the previous slab, so the union holds at most 15 + 10 - 1 = 24 blocks
+    const int c = J0 + lane;
+    const bool isend = d.big >= 0 && c < n && ws.re[c] == c + 1;
+    const int s0 = isend ? ws.rs[c] : c;
+    rstart[lane] = s0;
+    const int ba = (s0 - J0 + kHbT) >> 4, bz = (c - J0 + kHbT) >> 4;
+    unsigned long long m = 0;
+    if (isend)
+      for (int bi = ba; bi <= bz; ++bi)
+        for (int bj = ba; bj <= bi; ++bj) m |= 1ull << (bi * 8 + bj);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned lo = __shfl_xor((unsigned)m, o, 64), hi = __shfl_xor((unsigned)(m >> 32), o, 64);
+      m |= ((unsigned long long)hi << 32) | lo;
+    }
+    const unsigned long long ends = __ballot(isend), sp = __ballot(isend && s0 < J0);
+    if (lane == 0) {
+      runends = ends;
+      nspan = sp != 0;
+      int t = 0;
+      for (int b = 0; b < 64; ++b) {
+        blkid[b] = -1;
+        if (((m >> b) & 1ull) && t < kHbNB) {
+          blkid[b] = (int8_t)t;
+          blist[t++] = (uint8_t)b;
+        }
+      }
+      nblk = t;
+    }
+  }
   if (tid == 0) {  // the 32-bin blocks of the binnings in order (the plan keeps them <= kHbBlk)
     int t = 0;
     for (int g = 0; g < d.nbin; ++g)
@@ -468,7 +520,7 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
   }
   __syncthreads();
   const float* K = Kinv + (int64_t)l * np_ * np_;
-  const int nbin = d.nbin, nnear = d.nnear, bigon = d.big >= 0, nitem = 2 * nbk;
+  const int nbin = d.nbin, nnear = d.nnear, nitem = 2 * nbk, nbl = nblk, span = nspan;
   const unsigned catbits = hb_catbits(tb);
   // H items (item = 2 block + column block): wave w takes w and w + 4, both of column block w & 1
   const int cb = w & 1, hh = lane >> 5, col = 32 * cb + (lane & 31);
@@ -488,9 +540,12 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
   // without return (no wait; one lane per entry, so the adds apply in program order: deterministic), the first
   // fold storing
   double* Hs = ws.hscr + ((int64_t)l * (np_ / kHbT) + J) * kHbBins * kHbT;
-  double nacc[kHbNear];
+  // the near blocks likewise: wave w takes blocks w + 4 q (q < kHbNQ), [t][16 rows][16 columns] in the scratch
+  double* Ns = ws.nscr + ((int64_t)l * (np_ / kHbT) + J) * kHbNB * 256;
+  const int li = lane & 15, lk = lane >> 4;
+  bi_f32x4 nac[kHbNQ];
 #pragma unroll
-  for (int k = 0; k < kHbNear; ++k) nacc[k] = 0.0;
+  for (int q = 0; q < kHbNQ; ++q) nac[q] = bi_f32x4{0.f, 0.f, 0.f, 0.f};
   double tS = 0.0;
   const int cp = tid & 31, i8 = tid >> 5;  // this thread's tile part: columns 2 cp + 0, 1; rows 8 i8 + 0..7
   const float v0 = vs[2 * cp], v1 = vs[2 * cp + 1], r0 = sqrtf(v0), r1 = sqrtf(v1);  // (v = exp(log var) > 0)
@@ -503,9 +558,9 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
       p.pk[u] = __builtin_nontemporal_load(
           reinterpret_cast<const hb_f32x2*>(K + (int64_t)(I0 + 8 * i8 + u) * np_ + J0 + 2 * cp));
     p.pbn = (int)ws.pbin[(size_t)(w < nbin ? w : 0) * np_ + I0 + lane];  // (used by waves w < nbin only)
-    p.pre_ = ws.re[I0 + lane];
-    p.prs = ws.rs[I0 + lane];
-    p.key = ws.rkey[I0 + lane];
+    const float* vr = vv + (int64_t)l * np_ + I0 + 8 * i8;
+    p.vr[0] = *reinterpret_cast<const hb_f32x4*>(vr);
+    p.vr[1] = *reinterpret_cast<const hb_f32x4*>(vr + 4);
   };
 
   auto fold = [&](hb_f32x16& acc, int g, int b0, bool first) {
@@ -522,15 +577,14 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
     }
   };
 
-  auto body = [&](int I, int sl, HbPre& p) {
+  auto body = [&](int I, HbPre& p) {
     const int I0 = I * kHbT;
-    {  // the tile into LDS: fp32 rows x V^(1/2), the bf16 planes; the tr S part (sum_m v_m (K^-1_im)^2)
+    {  // the tile into LDS: the bf16 planes, the near window's columns; the tr S part (sum_m v_m (K^-1_im)^2)
       float ts = 0.f;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const hb_f32x2 sv = {p.pk[u][0] * r0, p.pk[u][1] * r1};
-        *reinterpret_cast<hb_f32x2*>(&T[sl][(8 * i8 + u) * kHbTP + 2 * cp]) = sv;
-        ts += sv[0] * sv[0] + sv[1] * sv[1];
+        const float s0 = p.pk[u][0] * r0, s1 = p.pk[u][1] * r1;
+        ts += s0 * s0 + s1 * s1;
       }
       tS += (double)ts;
 #pragma unroll
@@ -547,11 +601,33 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
       }
     }
     if (w < nbin) rbin[w][lane] = (uint8_t)p.pbn;
-    if (w == 0) rk[sl][lane] = p.key;  // the rows' keys
-    // the runs of the big covariate ending in this tile, in every wave's registers: lane e set = a run ends at
-    // row I0 + e, its start in lane e of rstart
-    const unsigned long long runmask = __ballot(bigon && I0 + lane < n && p.pre_ == I0 + lane + 1);
-    const int rstart = p.prs;
+    if (nbl > 0) {  // (uniform) near runs end in the slab: its columns x v^(1/2) of the rows, column-major
+      float sr[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sr[u] = sqrtf(p.vr[u >> 2][u & 3]);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float* dst = &Tc[(kHbT + 2 * cp + c) * kHbTP + 8 * i8];
+        *reinterpret_cast<hb_f32x4*>(dst) = hb_f32x4{p.pk[0][c] * sr[0], p.pk[1][c] * sr[1], p.pk[2][c] * sr[2],
+                                                     p.pk[3][c] * sr[3]};
+        *reinterpret_cast<hb_f32x4*>(dst + 4) = hb_f32x4{p.pk[4][c] * sr[4], p.pk[5][c] * sr[5],
+                                                         p.pk[6][c] * sr[6], p.pk[7][c] * sr[7]};
+      }
+      if (span) {  // (uniform, rare) a run starts in the previous slab: its columns too
+        hb_f32x2 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          q[u] = *reinterpret_cast<const hb_f32x2*>(K + (int64_t)(I0 + 8 * i8 + u) * np_ + J0 - kHbT + 2 * cp);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          float* dst = &Tc[(2 * cp + c) * kHbTP + 8 * i8];
+          *reinterpret_cast<hb_f32x4*>(dst) = hb_f32x4{q[0][c] * sr[0], q[1][c] * sr[1], q[2][c] * sr[2],
+                                                       q[3][c] * sr[3]};
+          *reinterpret_cast<hb_f32x4*>(dst + 4) = hb_f32x4{q[4][c] * sr[4], q[5][c] * sr[5], q[6][c] * sr[6],
+                                                           q[7][c] * sr[7]};
+        }
+      }
+    }
     __syncthreads();
     fetch(I + 1 < nt ? I + 1 : nt - 1, p);  // (in flight under this tile's work and the other workgroup's)
     if (!(dbg & 1) && it0) {
@@ -590,72 +666,57 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
         if (it1) fold(acc1, g1, b01, I == kHbFold - 1);
       }
     }
-    // near runs ending in this tile: 16 x 16 blocks (bi, bj) of X V X^T, items dealt from the last wave down
+    // near blocks: C[r][c] += sum over the tile's 64 rows m of Tc[16 bi + r][m] Tc[16 bj + c][m]; lane group lk
+    // takes rows 16 lk .. 16 lk + 15 (the k slots of 16 MFMAs: any row order works when A and B share it)
     if (!(dbg & 2)) {
-      const int wr = kHbSlabWaves - 1 - w;
-      int gi0 = 0;
-      for (unsigned long long rm = runmask; rm; rm &= rm - 1) {
-        const int e = __builtin_ctzll(rm);
-        const int s0 = __builtin_amdgcn_readlane(rstart, e), len = I0 + e + 1 - s0;
-        const int nb16 = (len + 15) >> 4, n2 = nb16 * nb16;
-        for (int item = (wr - gi0) & (kHbSlabWaves - 1); item < n2; item += kHbSlabWaves) {
-          const int bi = item / nb16, bj = item % nb16;
-          const int li = lane & 15, lk = lane >> 4;
-          const int ra = s0 + 16 * bi + li, rb = s0 + 16 * bj + li;  // the lane's A row, B column
-          const bool va = 16 * bi + li < len, vb = 16 * bj + li < len;
-          const float* ta = &T[hb_row_slot(ra)][(ra & 63) * kHbTP];
-          const float* tb2 = &T[hb_row_slot(rb)][(rb & 63) * kHbTP];
-          bi_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          {  // (two accumulators: half the dependent chain; the operands all read first)
-            float av[16], bv[16];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-              av[t] = ta[4 * t + lk];
-              bv[t] = tb2[4 * t + lk];
-            }
-            bi_f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < kHbNQ; ++q) {
+        const int t = w + kHbSlabWaves * q;
+        if (t < nbl) {  // (uniform)
+          const int bb = blist[t], bi = bb >> 3, bj = bb & 7;
+          const float* pa = &Tc[(16 * bi + li) * kHbTP + 16 * lk];
+          const float* pb = &Tc[(16 * bj + li) * kHbTP + 16 * lk];
+          hb_f32x4 a4[4], b4[4];
 #pragma unroll
-            for (int t = 0; t < 16; t += 2) {
-              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? av[t] : 0.f, vb ? bv[t] : 0.f, acc, 0, 0, 0);
-              acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(va ? av[t + 1] : 0.f, vb ? bv[t + 1] : 0.f, acc2, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] += acc2[q];
+          for (int s4 = 0; s4 < 4; ++s4) {
+            a4[s4] = *reinterpret_cast<const hb_f32x4*>(pa + 4 * s4);
+            b4[s4] = *reinterpret_cast<const hb_f32x4*>(pb + 4 * s4);
           }
-          // the lane's 4 pairs (i, j) = (s0 + 16 bi + 4 lk + q, s0 + 16 bj + li); pairs outside the run: rows of
-          // the run (clamped), weight 0 (no branch)
-          const hb_u32x4 kj = rk[hb_row_slot(rb)][rb & 63];
+          bi_f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = {0.f, 0.f, 0.f, 0.f};  // (two chains: half the dependency)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int ioff = 16 * bi + 4 * lk + q, i = s0 + (ioff < len ? ioff : 0);
-            const double wq = (ioff < len && vb) ? (double)acc[q] : 0.0;
-            const unsigned c = hb_pair_code(rk[hb_row_slot(i)][i & 63], kj, catbits, tb.ng);
-            const int cb8 = (int)(c & 0xffu) * kTabR;
+          for (int s4 = 0; s4 < 4; ++s4) {
+            x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s4][0], b4[s4][0], x0, 0, 0, 0);
+            x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s4][1], b4[s4][1], x1, 0, 0, 0);
+            x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s4][2], b4[s4][2], x0, 0, 0, 0);
+            x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s4][3], b4[s4][3], x1, 0, 0, 0);
+          }
+          nac[q] += x0 + x1;
+          if ((I & (kHbFold - 1)) == kHbFold - 1) {  // fold into the fp64 blocks: element e = C[4 lk + e][li]
+            double* nb = Ns + t * 256 + (4 * lk) * 16 + li;
 #pragma unroll
-            for (int k2 = 0; k2 < kHbNear; ++k2) {
-              if (k2 >= nnear) break;
-              const int g = sgrp[k2];
-              nacc[k2] += wq * (double)tab[k2 * tstride + cb8 + (int)((c >> (8 * (g + 1))) & 0xffu)];
+            for (int e = 0; e < 4; ++e) {
+              if (I == kHbFold - 1) nb[e * 16] = (double)nac[q][e];
+              else unsafeAtomicAdd(nb + e * 16, (double)nac[q][e]);
             }
+            nac[q] = bi_f32x4{0.f, 0.f, 0.f, 0.f};
           }
         }
-        gi0 += n2;
       }
     }
-    __syncthreads();  // every reader of slot sl, the planes, the bins, the run keys done before the next store
+    __syncthreads();  // every reader of the planes, the window columns and the bins done before the next store
   };
 
   HbPre pa;
   fetch(0, pa);
-  for (int I = 0; I < nt; ++I) body(I, I & 1, pa);
+  for (int I = 0; I < nt; ++I) body(I, pa);
   // (nt is a multiple of 4 = kHbFold: every tile folded; the scratch's stores and atomics complete and visible to
   // the workgroup before its epilogue reads them)
   __builtin_amdgcn_s_waitcnt(0);  // (vmcnt / lgkmcnt / expcnt 0: this wave's stores and atomics done)
   __threadfence_block();
   __syncthreads();
-  // Q_g[b][b'] = sum over the slab's columns m in bin b' of H_g[b][m]: thread (g, b) owns row b (LDS scratch = T);
+  // Q_g[b][b'] = sum over the slab's columns m in bin b' of H_g[b][m]: thread (g, b) owns row b (LDS scratch = Tc);
   // a part: thread (g, b) sums alpha over the slab's columns in bin b
-  double* Qs = reinterpret_cast<double*>(&T[0][0]);
+  double* Qs = reinterpret_cast<double*>(&Tc[0]);
   for (int e = tid; e < d.nb2; e += kHbSlabThreads) Qs[e] = 0.0;
   __syncthreads();
   double* out = ws.part + ((int64_t)l * nt + J) * kHbPart;
@@ -695,6 +756,30 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
       for (int q = 0; q < 4; ++q) {  // C[lk + 4 q][li]
         const int r = 16 * bi + lk + 4 * q, c = 16 * bj + li;
         if (r < nb && c < nb) out[d.b2off[g] + r * nb + c] = acc[q];
+      }
+    }
+  }
+  // the near runs' pairs, once each: S_ij from the fp64 blocks, contracted with the near slots' tables through the
+  // pair codes (the runs in column order, a run's len^2 ordered pairs dealt to the threads)
+  double nacc[kHbNear];
+#pragma unroll
+  for (int k = 0; k < kHbNear; ++k) nacc[k] = 0.0;
+  if (!(dbg & 2)) {
+    for (unsigned long long rm = runends; rm; rm &= rm - 1) {
+      const int e = __builtin_ctzll(rm), s0 = rstart[e], len = e + 1 - (s0 - J0);
+      for (int pq = tid; pq < len * len; pq += kHbSlabThreads) {
+        const int wi = s0 - J0 + kHbT + pq / len, wj = s0 - J0 + kHbT + pq % len;  // window columns
+        const int lo_ = min(wi, wj), hi_ = max(wi, wj);
+        const int t = blkid[((hi_ >> 4) << 3) | (lo_ >> 4)];
+        const double sv = t >= 0 ? Ns[t * 256 + (hi_ & 15) * 16 + (lo_ & 15)] : 0.0;  // (t >= 0: <= 24 blocks)
+        const unsigned c = hb_pair_code(ckey[wi], ckey[wj], catbits, tb.ng);
+        const int cb8 = (int)(c & 0xffu) * kTabR;
+#pragma unroll
+        for (int k2 = 0; k2 < kHbNear; ++k2) {
+          if (k2 >= nnear) break;
+          const int g = sgrp[k2];
+          nacc[k2] += sv * (double)tab[k2 * tstride + cb8 + (int)((c >> (8 * (g + 1))) & 0xffu)];
+        }
       }
     }
   }
@@ -875,7 +960,32 @@ int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   const int nt = np_ / kHbT;
   hb_tab_kernel<<<dim3((unsigned)((tabb / sizeof(float) + 255) / 256), L), 256, 0, st>>>(tb, ws, params);
   hb_near_kernel<<<dim3(nt, L), 256, ndyn, st>>>(tb, ws, n, np_, Kinv, alpha);
-  {
+  // LVAE_HB_CUMASK=F (dev A/B): the slab pass on a stream whose CU mask leaves the last F CUs free (for the
+  // ConvVAE's encoder backward, which runs beside it)
+  static const int cufree = getenv("LVAE_HB_CUMASK") ? atoi(getenv("LVAE_HB_CUMASK")) : 0;
+  static hipStream_t ms = nullptr;
+  static hipEvent_t mev[2] = {};
+  if (cufree > 0 && !ms) {
+    int dev = 0, ncu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu - cufree; ++c) mask[c >> 5] |= 1u << (c & 31);
+    if (hipExtStreamCreateWithCUMask(&ms, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
+        hipEventCreateWithFlags(&mev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&mev[1], hipEventDisableTiming) != hipSuccess)
+      return LVAE_ERR_LAUNCH;
+  }
+  if (ms) {
+    if (hipEventRecord(mev[0], st) != hipSuccess || hipStreamWaitEvent(ms, mev[0], 0) != hipSuccess)
+      return LVAE_ERR_LAUNCH;
+    {
+      ProfScope ps(LVAE_PH_HB_SLAB, ms);
+      hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, ms>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
+    }
+    if (hipEventRecord(mev[1], ms) != hipSuccess || hipStreamWaitEvent(st, mev[1], 0) != hipSuccess)
+      return LVAE_ERR_LAUNCH;
+  } else {
     ProfScope ps(LVAE_PH_HB_SLAB, st);
     hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, st>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
   }
