@@ -48,9 +48,9 @@ DTYPE = "f16x3-split (fp32-equivalent)"
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r4_pmc_summary.json")
 # The committed rocprofv3 --kernel-trace --stats summary of the default closed bench on the final tree
-# (scripts/gpu_r4a.sh): the roofline's `frac` is priced on its average launch duration of the dominant
+# (scripts/gpu_r5g.sh): the roofline's `frac` is priced on its average launch duration of the dominant
 # kernel, so that it recomputes from profiles/; the live HIP-event figure is reported beside it.
-KSTATS = os.path.join(ROOT, "profiles", "r4_headline_kernel_stats.csv")
+KSTATS = os.path.join(ROOT, "profiles", "r5_headline_kernel_stats.csv")
 # the Cholesky's trailing rank-256 update (chol_inv.hip): U2 alone (MODE kCiU2) when the lookahead chain
 # runs on the side stream (schedule (b), > CI_FUSE_MAX_L dims per call), else fused with U1 (kCiU12)
 CI_FUSE_MAX_L = 16

@@ -34,8 +34,6 @@
 #include "gram_tab.hpp"
 #include "prof.hpp"
 
-#include <vector>
-
 namespace lvae {
 
 constexpr int kHbMaxBin = 4;    // far binnings
@@ -960,32 +958,7 @@ int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   const int nt = np_ / kHbT;
   hb_tab_kernel<<<dim3((unsigned)((tabb / sizeof(float) + 255) / 256), L), 256, 0, st>>>(tb, ws, params);
   hb_near_kernel<<<dim3(nt, L), 256, ndyn, st>>>(tb, ws, n, np_, Kinv, alpha);
-  // LVAE_HB_CUMASK=F (dev A/B): the slab pass on a stream whose CU mask leaves the last F CUs free (for the
-  // ConvVAE's encoder backward, which runs beside it)
-  static const int cufree = getenv("LVAE_HB_CUMASK") ? atoi(getenv("LVAE_HB_CUMASK")) : 0;
-  static hipStream_t ms = nullptr;
-  static hipEvent_t mev[2] = {};
-  if (cufree > 0 && !ms) {
-    int dev = 0, ncu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu - cufree; ++c) mask[c >> 5] |= 1u << (c & 31);
-    if (hipExtStreamCreateWithCUMask(&ms, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
-        hipEventCreateWithFlags(&mev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&mev[1], hipEventDisableTiming) != hipSuccess)
-      return LVAE_ERR_LAUNCH;
-  }
-  if (ms) {
-    if (hipEventRecord(mev[0], st) != hipSuccess || hipStreamWaitEvent(ms, mev[0], 0) != hipSuccess)
-      return LVAE_ERR_LAUNCH;
-    {
-      ProfScope ps(LVAE_PH_HB_SLAB, ms);
-      hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, ms>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
-    }
-    if (hipEventRecord(mev[1], ms) != hipSuccess || hipStreamWaitEvent(st, mev[1], 0) != hipSuccess)
-      return LVAE_ERR_LAUNCH;
-  } else {
+  {
     ProfScope ps(LVAE_PH_HB_SLAB, st);
     hb_slab_kernel<<<dim3(nt, L), kHbSlabThreads, sdyn, st>>>(tb, ws, n, np_, Kinv, v, alpha, hb_dbg());
   }
