@@ -46,7 +46,7 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r4_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r5_pmc_summary.json")
 # The committed rocprofv3 --kernel-trace --stats summary of the default closed bench on the final tree
 # (scripts/gpu_r5g.sh): the roofline's `frac` is priced on its average launch duration of the dominant
 # kernel, so that it recomputes from profiles/; the live HIP-event figure is reported beside it.
