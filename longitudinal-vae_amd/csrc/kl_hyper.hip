@@ -371,12 +371,12 @@ __global__ __launch_bounds__(256) void hb_near_kernel(GramTab tb, HbWs ws, int n
 //     (x V^(1/2) of its ROWS, column-major) for the near runs, and its tr S part
 //   H_g += Phi_g(tile)^T K^-1(tile, slab): one-hot GEMMs on v_mfma_f32_32x32x16_bf16, item = (32-bin block,
 //     32-column block), two items per wave (the plan allows at most 4 blocks) held in the accumulators across
-//     4 tiles (products exact), then added to the workgroup's fp64 H in the workspace
+//     kHbFold tiles (products exact), then added to the workgroup's fp64 H in the workspace
 //   near runs: the workgroup owns the runs ENDING in its columns; K^-1 is symmetric, so a run's S block
 //     X_run V X_run^T = sum over all rows m of K^-1(m, run)^T v_m K^-1(m, run) accumulates from the column slab
 //     itself, tile by tile: the 16 x 16 blocks of the run window's columns (the slab, plus the previous slab's
 //     columns for a run that starts there, loaded in that case only) on v_mfma_f32_16x16x4f32 (k = 16 rows per
-//     lane group: 16-byte LDS reads), in fp32 accumulators for 4 tiles, then added to fp64 blocks in the
+//     lane group: 16-byte LDS reads), in fp32 accumulators for kHbFold tiles, then added to fp64 blocks in the
 //     workspace; the pair codes and table contraction run ONCE per pair in the epilogue, not per tile
 // H and the near blocks reach the workspace by atomics without return (no wait; one lane per entry, so they
 // apply in program order: deterministic).  The next tile arrives in registers under the current one's work
@@ -402,7 +402,10 @@ typedef float hb_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 hb_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 hb_bf16x2 __attribute__((ext_vector_type(2)));
 constexpr int kHbSlabThreads = 256, kHbSlabWaves = kHbSlabThreads / 64;
-constexpr int kHbFold = 4;  // tiles summed in fp32 by the accumulators before the fp64 fold
+#ifndef LVAE_HB_FOLD
+#define LVAE_HB_FOLD 16
+#endif
+constexpr int kHbFold = LVAE_HB_FOLD;  // tiles summed in fp32 by the accumulators before the fp64 fold (power of 2)
 
 struct HbPre {        // one tile's prefetch
   hb_f32x2 pk[8];     // K^-1 rows 8 (tid >> 5) + u, columns 2 (tid & 31) + 0, 1
@@ -577,6 +580,8 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
 
   auto body = [&](int I, HbPre& p) {
     const int I0 = I * kHbT;
+    // the accumulators go to the fp64 scratch every kHbFold tiles and after the last (the first fold stores)
+    const bool fold_now = (I & (kHbFold - 1)) == kHbFold - 1 || I == nt - 1, fold_first = I < kHbFold;
     {  // the tile into LDS: the bf16 planes, the near window's columns; the tr S part (sum_m v_m (K^-1_im)^2)
       float ts = 0.f;
 #pragma unroll
@@ -659,9 +664,9 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
           acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh, acc1, 0, 0, 0);
         }
       }
-      if ((I & (kHbFold - 1)) == kHbFold - 1) {  // fold the accumulators into H (fp64, the scratch)
-        fold(acc0, g0, b00, I == kHbFold - 1);
-        if (it1) fold(acc1, g1, b01, I == kHbFold - 1);
+      if (fold_now) {  // fold the accumulators into H (fp64, the scratch)
+        fold(acc0, g0, b00, fold_first);
+        if (it1) fold(acc1, g1, b01, fold_first);
       }
     }
     // near blocks: C[r][c] += sum over the tile's 64 rows m of Tc[16 bi + r][m] Tc[16 bj + c][m]; lane group lk
@@ -689,11 +694,11 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
             x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s4][3], b4[s4][3], x1, 0, 0, 0);
           }
           nac[q] += x0 + x1;
-          if ((I & (kHbFold - 1)) == kHbFold - 1) {  // fold into the fp64 blocks: element e = C[4 lk + e][li]
+          if (fold_now) {  // fold into the fp64 blocks: element e = C[4 lk + e][li]
             double* nb = Ns + t * 256 + (4 * lk) * 16 + li;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              if (I == kHbFold - 1) nb[e * 16] = (double)nac[q][e];
+              if (fold_first) nb[e * 16] = (double)nac[q][e];
               else unsafeAtomicAdd(nb + e * 16, (double)nac[q][e]);
             }
             nac[q] = bi_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -707,7 +712,7 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
   HbPre pa;
   fetch(0, pa);
   for (int I = 0; I < nt; ++I) body(I, pa);
-  // (nt is a multiple of 4 = kHbFold: every tile folded; the scratch's stores and atomics complete and visible to
+  // (the last tile folds too; the scratch's stores and atomics complete and visible to
   // the workgroup before its epilogue reads them)
   __builtin_amdgcn_s_waitcnt(0);  // (vmcnt / lgkmcnt / expcnt 0: this wave's stores and atomics done)
   __threadfence_block();

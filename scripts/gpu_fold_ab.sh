@@ -4,8 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/fold_ab; mkdir -p $OUT
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
-for f in 4 8 16; do
-  if [ $f = 4 ]; then LIB=$ROOT/longitudinal-vae_amd/lvae_amd/liblvae_hip.so; else LIB=$ROOT/build_f$f/liblvae_hip.so; fi
+for f in ${FOLDS:-4 8 16}; do
+  if [ $f = ${TREE_FOLD:-4} ]; then LIB=$ROOT/longitudinal-vae_amd/lvae_amd/liblvae_hip.so; else LIB=$ROOT/build_f$f/liblvae_hip.so; fi
   LVAE_LIB=$LIB timeout -k 10 300 $PYT tests/test_gpu_kl_hyper.py -x -s > $OUT/hyper_$f.log 2>&1 || { tail -20 $OUT/hyper_$f.log; exit 1; }
   echo "== fold $f"; grep -E "passed|rel err|routes agree|raw gradients" $OUT/hyper_$f.log | tail -12
   (cd /tmp && export TMPDIR=/tmp && LVAE_LIB=$LIB timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/m$f -o run \
