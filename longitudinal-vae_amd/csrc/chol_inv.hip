@@ -361,6 +361,13 @@ static unsigned long long* g_pivot_prof = nullptr;
     if (prof && threadIdx.x == 0) prof[((int64_t)kb * L + l) * 8 + (q)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
+// (dev builds, LVAE_PV_STAMP_CHOL: stamp i < 24 of pivot kb == 1 only, slots of kb = 1 + i / 8)
+#define CI_STAMPX(i)                                                                                \
+  do {                                                                                              \
+    if (prof && kb == 1 && threadIdx.x == 0)                                                        \
+      prof[((int64_t)(1 + (i) / 8) * L + l) * 8 + (i) % 8] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+
 // G == 1: one workgroup per dim (blockIdx = dim); G == kCiPvG (pending only): the split pivot, workgroup b
 // of dim b % Lr, slab b / Lr (Lr = gridDim.x / G, a multiple of 8; dims >= L exit)
 template <int G>
@@ -375,7 +382,11 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
   if (l >= L) return;  // (uniform; padding dims of the split grid)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rl = lane & 31, hh = lane >> 5;
   const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
+#ifdef LVAE_PV_STAMP_CHOL
+  if (hs == 0) CI_STAMPX(0);
+#else
   if (hs == 0) CI_STAMP(0);
+#endif
   if (tid == 0) {
     bad_s = INT_MAX;
     ymax_s = 0u;
@@ -415,7 +426,11 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
     for (int b = 0; b < kPvBlocks; ++b) lf[b * kPvBlk + r * kPvL + c] = v[b];
   }
   __syncthreads();
+#ifdef LVAE_PV_STAMP_CHOL
+  CI_STAMPX(1);
+#else
   CI_STAMP(1);
+#endif
   double ld = 0.0;
   int bad = INT_MAX;
 
@@ -441,6 +456,9 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
       __syncthreads();  // pv_panel2's barrier
     }
     __syncthreads();
+#ifdef LVAE_PV_STAMP_CHOL  // (dev builds: pivot 1's panel q end at stamp 2 + 2 q, its update's at 3 + 2 q)
+    CI_STAMPX(2 + 2 * q);
+#endif
     const int m = 7 - q, nb = m * (m + 1) / 2;
     for (int t = w; t < nb; t += 16) {
       int jj = 0, u = t;
@@ -456,8 +474,13 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
       pv_store(acc, Bij, rl, hh);
     }
     __syncthreads();
+#ifdef LVAE_PV_STAMP_CHOL
+    CI_STAMPX(3 + 2 * q);
+#endif
   }
+#ifndef LVAE_PV_STAMP_CHOL
   CI_STAMP(2);
+#endif
   if (S.lout) {  // (potrf-only) L_kk, zero strict upper part, into tile (kb, kb) of lout
     float* O = S.lout + (int64_t)l * np_ * np_ + (int64_t)kb * kSwB * np_ + kb * kSwB;
     for (int e = tid; e < kSwBB; e += 1024) {
@@ -467,7 +490,9 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
   }
   if (w < 8) pv_trinv(pv_blk(lf, w, w), lane);
   __syncthreads();
+#ifndef LVAE_PV_STAMP_CHOL
   CI_STAMP(3);
+#endif
 
   // 2. L^-1 in place by recursive doubling (levels of 64, 128, 256 rows; see spd_sweep.hip's pivot)
   if (w < 4) {
@@ -519,7 +544,9 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
     __syncthreads();
   }
 
+#ifndef LVAE_PV_STAMP_CHOL
   CI_STAMP(4);
+#endif
   // 3. max |Y_kk| -> its split scale; out: D (row-major planes; the diagonal copy puts them into the
   //    Y and Y^T planes after potrf).  Thread (r0 = tid >> 6, c = 4 (tid & 63)) covers rows r0, r0 + 16,
   //    ... (a wave writes one whole row: half4 runs).
@@ -555,7 +582,11 @@ __global__ __launch_bounds__(1024) void ci_pivot_kernel(const float* __restrict_
   }
   if (w == 0 && lane == 0) bad_s = bad;
   __syncthreads();
+#ifdef LVAE_PV_STAMP_CHOL
+  CI_STAMPX(18);
+#else
   CI_STAMP(5);
+#endif
   if (tid == 0) {
     S.ysc[((int64_t)l * S.nt + kb) * S.nt + kb] = sY;
     logdet[l] += ld;
