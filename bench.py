@@ -517,7 +517,7 @@ def run_closed(args, world, rank, dev):
 # ------------------------------------------------------------------------------------------
 # Regime A: Hensman SVI step, HIP-graph replayed
 # ------------------------------------------------------------------------------------------
-def run_hensman(args, world, rank, dev):
+def run_hensman(args, world, rank, dev, dp_hooks=False):
     import lvae_amd as la
     from lvae_amd.data import health_mnist_batch
     from lvae_amd.samplers import check_same_permutation, hensman_batches, SubjectSampler
@@ -540,7 +540,7 @@ def run_hensman(args, world, rank, dev):
     opt = torch.optim.Adam([{"params": k0.parameters()}, {"params": k1.parameters()},
                             {"params": vae.parameters()}], lr=1e-3, capturable=True, fused=True)
     hook = ngr = None
-    if world > 1:
+    if world > 1 or dp_hooks:  # (dp_hooks at world 1: the data-parallel step through a world-1 RCCL group)
         from lvae_amd.distributed import GradAllReduce, allreduce_tensors
         hook = GradAllReduce(list(vae.parameters()) + list(k0.parameters()) + list(k1.parameters()), world)
         ngr = lambda ts: allreduce_tensors(ts, average=False)
@@ -583,13 +583,39 @@ def run_hensman(args, world, rank, dev):
             "dtype": "fp64 GP (f64 MFMA / VALU) + fp32 ConvVAE",
             "config": {"workload": f"Hensman step: P_tot={P} subjects x T={T} (N={N}), L={L}, M={M}, P_b={P_b} "
                                    f"subjects per rank per step, natural gradient, one HIP graph per step"
-                                   + (" (two around the all-reduces)" if world > 1 else ""),
+                                   + (" (two around the all-reduces)" if world > 1 or dp_hooks else ""),
                        "parallelism": f"dp{world} over subject mini-batches"}}
 
 
 # ------------------------------------------------------------------------------------------
 # C2: HIP Gram + inverse vs PyTorch-ROCm Gram + torch.linalg.cholesky (N = 1024, L = 8)
 # ------------------------------------------------------------------------------------------
+def run_hensman_dp_world1(args, dev):
+    """Regime A's data-parallel step at world 1: the SUM all-reduces of the Adam gradients and of the natural-
+    gradient statistics through a world-1 RCCL ("nccl") group, i.e. the step as two HIP graphs around the eager
+    collectives (GraphedStep with grad_hook / ng_reduce) -- the per-rank shape of the N-GPU Regime A line without
+    the other ranks.  Reported beside the one-graph step (the same batches)."""
+    created = False
+    if not dist.is_initialized():
+        import socket
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        dist.init_process_group("nccl", device_id=dev)
+        created = True
+    try:
+        r = run_hensman(args, 1, 0, dev, dp_hooks=True)
+    finally:
+        if created:
+            dist.destroy_process_group()
+    return {"ms_per_step": r["ms_per_step"], "value": r["value"], "unit": r["unit"],
+            "config": r["config"]["workload"],
+            "note": "world-1 RCCL group: GradAllReduce + natural-gradient statistics all-reduce between the two graphs"}
+
+
 def torch_gram_f32(params, X):
     """The sample-config additive Gram (+ noise = 1 on the diagonal) in plain PyTorch fp32 ops."""
     x = X.to(torch.float32)
@@ -747,7 +773,9 @@ def main():
     ap.add_argument("--P_b", type=int, default=5, help="Regime A: subjects per batch per rank")
     ap.add_argument("--M", type=int, default=120, help="Regime A: inducing points")
     ap.add_argument("--h-steps", dest="h_steps", type=int, default=100, help="Regime A timed steps")
-    ap.add_argument("--regime", choices=["both", "closed", "hensman"], default="both")
+    # default: both regimes on one GPU; the exact-KL line alone at N > 1 (Regime A's data-parallel two-graph replay
+    # through RCCL is opt-in there: DESIGN.md section 5)
+    ap.add_argument("--regime", choices=["auto", "both", "closed", "hensman"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-timing", action="store_true")
     ap.add_argument("--no-c2", action="store_true")
@@ -759,17 +787,38 @@ def main():
     ap.add_argument("--rank-share", dest="rank_share", type=int, default=0,
                     help="one GPU: time rank 0's share of a W-rank latent-sharded step (L/W dims, N/W images; "
                          "collectives replaced by local stand-ins) -- the per-rank compute of the W-GPU line")
+    ap.add_argument("--dp-world1", dest="dp_world1", action="store_true",
+                    help="one GPU: also time Regime A's data-parallel step (two graphs around the all-reduces) "
+                         "through a world-1 RCCL group (opt-in: see DESIGN.md section 5 on this path)")
     ap.add_argument("--vae-stream-priority", dest="vae_stream_priority", type=int, default=-1,
                     help="priority of the ConvVAE's stream in the closed step (lower = higher; 0 = default)")
     args = ap.parse_args()
 
     world, rank, local = setup_dist(force_group=args.sharded_world1)
     dev = torch.device("cuda", local)
+    if args.regime == "auto":
+        args.regime = "both" if world == 1 else "closed"
     res = None
     if args.regime in ("both", "closed"):
         res = run_closed(args, world, rank, dev)
     if args.regime in ("both", "hensman"):
-        ra = run_hensman(args, world, rank, dev)
+        if res is not None:
+            # (the sub-record of the closed line: a failure here is recorded in it, the line itself stands)
+            try:
+                ra = run_hensman(args, world, rank, dev)
+            except Exception as e:
+                if os.environ.get("LVAE_BENCH_RAISE") == "1":
+                    raise
+                ra = {"error": f"{type(e).__name__}: {e}"[:300]}
+        else:
+            ra = run_hensman(args, world, rank, dev)
+        if world == 1 and args.dp_world1:
+            try:
+                ra["dp_world1_rccl"] = run_hensman_dp_world1(args, dev)
+            except Exception as e:  # (a record of the failure; the line itself stands)
+                if os.environ.get("LVAE_BENCH_RAISE") == "1":
+                    raise
+                ra["dp_world1_rccl"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if res is None:
             res = dict(ra, n_gpus=world, warmup=args.warmup, higher_is_better=True, vs_baseline=None,
                        data="synthetic (Health-MNIST-shaped covariates/images, random-init ConvVAE)")
@@ -782,9 +831,9 @@ def main():
             if args.regime in ("both", "closed"):
                 res["cpu_baseline"] = cpu_baseline_closed(args.P, args.T, args.L)
                 res["vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]
-            if args.regime in ("both", "hensman"):
+            ra = res["regime_a"] if "regime_a" in res else res
+            if args.regime in ("both", "hensman") and "value" in ra:
                 cb = cpu_baseline_hensman(args.P, args.T, args.L, args.M, args.P_b)
-                ra = res["regime_a"] if "regime_a" in res else res
                 ra["cpu_baseline"] = cb
                 ra["vs_cpu_baseline"] = ra["value"] / cb["value"]
                 if "regime_a" not in res:
