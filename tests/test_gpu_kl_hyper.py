@@ -22,12 +22,14 @@ HB_GATES = dict(cat_kernel=[2], bin_kernel=[4], sqexp_kernel=[0],
                 bin_int_kernel=[], covariate_missing_val=[{'covariate': 1, 'mask': 5}])
 
 
-def _run(P, L, seed, perm=None, hyper=None, cfg=CFG):
+def _run(P, L, seed, perm=None, hyper=None, cfg=CFG, T=16, xfn=None):
+    """perm: row indices (a permutation, or an increasing subset: ragged subjects); xfn: edits the covariates"""
     import lvae_amd as la
     from lvae_amd.data import health_mnist_covariates
     from lvae_amd.elbo import kl_closed_hyper_log
-    T = 16
     X = torch.tensor(health_mnist_covariates(P, T, seed=seed))
+    if xfn is not None:
+        X = xfn(X)
     gen = torch.Generator().manual_seed(seed)
     mu = torch.randn(P * T, L, generator=gen, dtype=torch.float64)
     lv = 0.1 * torch.randn(P * T, L, generator=gen, dtype=torch.float64)
@@ -121,3 +123,30 @@ def test_binned_route_deterministic(hip):
     a = _run(64, 2, seed=9)
     b = _run(64, 2, seed=9)
     assert torch.equal(a["draw"], b["draw"])
+
+
+def test_binned_route_ragged_runs_across_slabs_vs_oracle(hip):
+    """Id runs of 18..32 points that start anywhere: 24 subjects of T = 16, each cut to a random prefix of 9..16
+    points, and every two consecutive subjects given one id (covariate 2).  Many runs then cross the slab pass's
+    64-column boundaries, and its near blocks take the previous slab's columns too (kl_hyper.hip: a run ending in
+    slab J that starts in slab J - 1).  ~300 points, padded to 512."""
+    P, T, L = 24, 16, 2
+    rng = np.random.default_rng(5)
+    keep = np.concatenate([np.arange(s * T, s * T + int(rng.integers(9, T + 1))) for s in range(P)])
+
+    def pair_ids(X):
+        X = X.clone()
+        X[:, 2] = torch.floor(X[:, 2] / 2)
+        return X
+
+    r = _run(P, L, seed=17, perm=torch.tensor(keep), xfn=pair_ids)
+    assert r["on"] == 1, "the binned route should run on these subject-contiguous runs (<= 64 points each)"
+    starts = np.flatnonzero(np.diff(np.r_[-1, r["X"][:, 2].numpy()]))
+    ends = np.r_[starts[1:], len(keep)] - 1
+    assert any(s // 64 != e // 64 for s, e in zip(starts, ends)), "no run crosses a 64-point slab boundary"
+    for l in range(L):
+        ref, g = _oracle_grads(r, l)
+        assert rel(r["kl"][l], ref) < 1e-4
+        e = rel(r["draw"][l], g)
+        print(f"ragged runs dim {l}: binned-route raw-parameter gradients rel err {e:.2e}")
+        assert e < 1e-4
