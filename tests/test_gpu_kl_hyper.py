@@ -125,9 +125,11 @@ def test_binned_route_deterministic(hip):
     assert torch.equal(a["draw"], b["draw"])
 
 
-def test_binned_route_ragged_runs_across_slabs_vs_oracle(hip):
-    """Id runs of 18..32 points that start anywhere: 24 subjects of T = 16, each cut to a random prefix of 9..16
-    points, and every two consecutive subjects given one id (covariate 2).  Many runs then cross the slab pass's
+@pytest.mark.parametrize("group", [2, 4])
+def test_binned_route_ragged_runs_across_slabs_vs_oracle(hip, group):
+    """Id runs of 18..32 (group 2) or 36..64 points (group 4, up to the route's 64-point bound and its 24 near
+    blocks) that start anywhere: 24 subjects of T = 16, each cut to a random prefix of 9..16 points, and every
+    `group` consecutive subjects given one id (covariate 2).  Many runs then cross the slab pass's
     64-column boundaries, and its near blocks take the previous slab's columns too (kl_hyper.hip: a run ending in
     slab J that starts in slab J - 1).  ~300 points, padded to 512."""
     P, T, L = 24, 16, 2
@@ -136,7 +138,7 @@ def test_binned_route_ragged_runs_across_slabs_vs_oracle(hip):
 
     def pair_ids(X):
         X = X.clone()
-        X[:, 2] = torch.floor(X[:, 2] / 2)
+        X[:, 2] = torch.floor(X[:, 2] / group)
         return X
 
     r = _run(P, L, seed=17, perm=torch.tensor(keep), xfn=pair_ids)
@@ -148,5 +150,5 @@ def test_binned_route_ragged_runs_across_slabs_vs_oracle(hip):
         ref, g = _oracle_grads(r, l)
         assert rel(r["kl"][l], ref) < 1e-4
         e = rel(r["draw"][l], g)
-        print(f"ragged runs dim {l}: binned-route raw-parameter gradients rel err {e:.2e}")
+        print(f"ragged runs (group {group}) dim {l}: binned-route raw-parameter gradients rel err {e:.2e}")
         assert e < 1e-4
