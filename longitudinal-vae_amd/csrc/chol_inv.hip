@@ -53,6 +53,9 @@
 #ifndef LVAE_PV_SAMEAB
 #define LVAE_PV_SAMEAB 1
 #endif
+#ifndef LVAE_CI_KREV
+#define LVAE_CI_KREV 1
+#endif
 
 namespace lvae {
 
@@ -1223,8 +1226,12 @@ __device__ inline void ci_gemm_body(const CiGemmArgs& g, const CiScratch& S, con
       __syncthreads();  // (kl_mu / kl_sv written above)
       inv = 1.f;
     } else {
-      C16BlockRescale rs{sprod, 1.f};
-      c16_gemm<4>(A, B, nkb * (kSwB / kC16BK), lds, acc, rs);
+      // lauum and trtri's X step: the K ranges of a launch's tiles END together (lauum: at the last block for every
+      // tile; X: at o + h in an instance), so their chunks run from the end (LVAE_CI_KREV=0: in order)
+      constexpr bool krev = LVAE_CI_KREV && (MODE == kCiLauum || MODE == kCiLauumKL || MODE == kCiX);
+      const int nk = nkb * (kSwB / kC16BK);
+      C16BlockRescale rs{sprod, 1.f, krev ? nk : 0};
+      c16_gemm<4>(A, B, nk, lds, acc, rs, krev);
       inv = 1.0f / rs.scur;
     }
   } else {

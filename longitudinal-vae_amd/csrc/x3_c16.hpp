@@ -63,6 +63,7 @@ struct C16Dma {
   const _Float16* g;  // + lane_off, + (w & 1) * 4 blocks
   int64_t cs, bs;
   int doff;           // LDS offset (halves) of the wave's first piece in a stage
+  int rev_nk;         // 0: chunks in order; nk: step c reads chunk nk - 1 - c (the K range from its end)
 };
 __device__ inline C16Dma c16_dma(const C16Opnd& A, const C16Opnd& B) {
   // the wave id through readfirstlane: provably uniform, so the LDS base (M0) needs no waterfall loop
@@ -76,10 +77,11 @@ __device__ inline C16Dma c16_dma(const C16Opnd& A, const C16Opnd& B) {
   const int64_t lane_off = ld ? (lane >> 1) * ld + 8 * ((lane & 1) ^ ((lane >> 4) & 1)) : 8 * lane;
   d.g = reinterpret_cast<const _Float16*>(hi) + (p & 1) * lo + 4 * (w & 1) * d.bs + lane_off;
   d.doff = p * kC16Part + (w & 1) * 2048;
+  d.rev_nk = 0;
   return d;
 }
 __device__ inline void c16_issue(const C16Dma& d, int c, _Float16* __restrict__ stage) {
-  const _Float16* g = d.g + (int64_t)c * d.cs;
+  const _Float16* g = d.g + (int64_t)(d.rev_nk ? d.rev_nk - 1 - c : c) * d.cs;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     __builtin_amdgcn_global_load_lds((const void*)(g + q * d.bs), (void*)(stage + d.doff + q * 512), 16, 0, 0);
@@ -168,11 +170,13 @@ struct C16NoRescale {
 
 // acc[a][b] += A B^T over nk 16-deep chunks (A, B: C16Opnd panels); lds = NS * kC16Stage halves, the
 // kernel's only staging object; nk even; rescale(s, acc) at the top of every step (state kept in the
-// caller's functor).  Returns with no DMA outstanding.
+// caller's functor).  rev: the chunks from the last to the first (tiles whose K ranges end together then read
+// the same chunks at the same time: the shared panels stay in L2).  Returns with no DMA outstanding.
 template <int NS, typename Rescale>
 __device__ inline void c16_gemm(const C16Opnd& A, const C16Opnd& B, int nk, _Float16* __restrict__ lds,
-                                sx_f32x16 (&acc)[4][2], Rescale& rescale) {
-  const C16Dma dma = c16_dma(A, B);
+                                sx_f32x16 (&acc)[4][2], Rescale& rescale, bool rev = false) {
+  C16Dma dma = c16_dma(A, B);
+  dma.rev_nk = rev ? nk : 0;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) c16_issue(dma, min(s, nk - 1), lds + s * kC16Stage);
   c16_wait_vm<4 * (NS - 2)>();
@@ -201,11 +205,13 @@ __device__ inline void c16_gemm(const C16Opnd& A, const C16Opnd& B, int nk, _Flo
 struct C16BlockRescale {
   const float* sprod;
   float scur;
+  int rev_nk = 0;  // (c16_gemm's rev: step s is chunk rev_nk - 1 - s; nk a multiple of 16)
   __device__ void operator()(int s, sx_f32x16 (&acc)[4][2]) {
+    const int b = (rev_nk ? rev_nk - 1 - s : s) >> 4;
     if (s == 0) {
-      scur = sprod[0];
+      scur = sprod[b];
     } else if ((s & 15) == 0) {
-      const float snew = sprod[s >> 4], ratio = snew / scur;
+      const float snew = sprod[b], ratio = snew / scur;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
