@@ -342,6 +342,13 @@ int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin);
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
                                 int Cin, int H, int W, float* dw, float* db, void* workspace, void* stream);
+/* The input gradient of the same layer (the second encoder conv, VAE.py:48-50; torch's conv2d backward-data
+ * in the reference's autograd): gx [N, Cin, H, W] = the conv's backward-data of the routed gradient (gy at
+ * each window's argmax where y > 0), formed per image in LDS, never in HBM.  w [C, Cin, 3, 3].  Cin == 16
+ * (-3 otherwise) and lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 64 KB (-4 otherwise).                 */
+size_t lvae_conv3x3_pool_dgrad_lds(int C, int H, int W);
+int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* w, int N, int C,
+                                int Cin, int H, int W, float* gx, void* stream);
 /* ConvVAE decoder output (VAE.py:75, 124): out = sigmoid(ConvTranspose2d(Cin, 1, 4, stride 2, padding 1)
  * (z) + bias), z [N, Cin, Hi, Wi] (Cin <= 16), w [Cin, 1, 4, 4], bias [1] -> out [N, 1, 2Hi, 2Wi].
  * Backward from g = dLoss/dout and the saved out: gz [N, Cin, Hi, Wi], dw [Cin, 1, 4, 4], db [1]

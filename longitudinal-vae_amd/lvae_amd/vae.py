@@ -5,10 +5,16 @@ reference runs it in fp64 (LVAE.py:139-140, 152); here it runs in the dtype of i
 (fp32 by default: mu / logvar drift ~1e-7 relative vs fp64).
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
 from torch import nn
+
+
+# LVAE_CONV_DGRAD=0: the second encoder conv's input gradient on MIOpen (routed gradient + backward-data conv)
+# instead of lvae_conv3x3_pool_dgrad_f32 (A/B runs)
+_CONV_DGRAD = os.environ.get("LVAE_CONV_DGRAD", "1") != "0"
 
 
 class _ReluMaxPool2(torch.autograd.Function):
@@ -48,8 +54,9 @@ class _ConvReluMaxPool2(torch.autograd.Function):
     Forward: a 1-channel input (the first conv) is one direct HIP pass (lvae_conv1_relu_maxpool2_fwd_f32);
     otherwise the conv runs without its bias on MIOpen and bias add, relu and pool are one HIP pass
     (lvae_relu_maxpool2_bias_fwd_f32).  Backward: weight and bias gradients straight from the pooled
-    gradient (lvae_conv3x3_pool_wgrad_f32); the routed full-resolution gradient is formed only for the
-    input gradient (MIOpen backward-data), which the first conv does not need."""
+    gradient (lvae_conv3x3_pool_wgrad_f32), and for 16 input channels the input gradient too
+    (lvae_conv3x3_pool_dgrad_f32; the first conv needs none); otherwise the routed full-resolution
+    gradient is formed for MIOpen's backward-data conv."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -85,9 +92,8 @@ class _ConvReluMaxPool2(torch.autograd.Function):
         Cin = x.shape[1]
         if N >= 512 and C * Cin <= 1024 and 4 * (Cin * (((H + 2) * (W + 2)) | 1) + 2 * C * (H // 2) * (W // 2)) <= 65536:
             # (below a few hundred images the per-image kernel cannot fill the GPU: MIOpen path)
-            # weight and bias gradients from the pooled gradient (lvae_conv3x3_pool_wgrad_f32); the routed
-            # full-resolution gradient only feeds the input gradient (MIOpen backward-data), and the
-            # first conv (image input) needs none
+            # weight and bias gradients from the pooled gradient (lvae_conv3x3_pool_wgrad_f32); the first
+            # conv (image input) needs no input gradient
             xc = x.contiguous()
             dw = torch.empty_like(weight)
             db = torch.empty(C, dtype=gy.dtype, device=gy.device)
@@ -97,7 +103,14 @@ class _ConvReluMaxPool2(torch.autograd.Function):
                                                         H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
                                                         _lib.stream_ptr()), "conv3x3_pool_wgrad")
             gx = None
-            if ctx.needs_input_grad[0]:
+            if ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536:
+                # the input gradient straight from the pooled gradient too (lvae_conv3x3_pool_dgrad_f32: the
+                # routed gradient formed per image in LDS; no MIOpen backward-data conv, no transposes)
+                gx = torch.empty(N, Cin, H, W, dtype=gy.dtype, device=gy.device)
+                _lib.check(lib.lvae_conv3x3_pool_dgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx),
+                                                            _lib.ptr(weight.contiguous()), N, C, Cin, H, W,
+                                                            _lib.ptr(gx), _lib.stream_ptr()), "conv3x3_pool_dgrad")
+            elif ctx.needs_input_grad[0]:
                 g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
                 _lib.check(lib.lvae_relu_maxpool2_bwd_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), N * C, H, W,
                                                            _lib.ptr(g0), _lib.stream_ptr()), "relu_maxpool2_bwd")

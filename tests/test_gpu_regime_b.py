@@ -397,6 +397,36 @@ def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw, xgrad):
     assert all(e < tol for e, tol in zip(errs, tols)), errs
 
 
+@pytest.mark.parametrize("n,c,hw", [(3, 4, 8), (37, 32, 18), (2, 8, 30), (513, 32, 18)])
+def test_conv3x3_pool_dgrad_vs_fp64(hip, n, c, hw):
+    """lvae_conv3x3_pool_dgrad_f32 (the second encoder conv's input gradient from the pooled gradient, the
+    routed gradient formed in LDS) vs fp64 conv2d backward-data of the routed gradient (routed by the same
+    argmax / relu decisions), to 1e-5 of its max; ties of the window max (idx = first maximum) and
+    windows with y = 0 included.  Unsupported shapes return -3 (Cin != 16) / -4 (LDS)."""
+    from lvae_amd import _lib
+    import torch.nn.functional as F
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    cin, ho = 16, hw // 2
+    w = torch.randn(c, cin, 3, 3, device=DEV, generator=gen)
+    gy = torch.randn(n, c, ho, ho, device=DEV, generator=gen)
+    y = torch.randn(n, c, ho, ho, device=DEV, generator=gen).clamp_min(0.0)  # ~half the windows relu'd off
+    idx = torch.randint(0, 4, (n, c, ho, ho), device=DEV, generator=gen, dtype=torch.int32).to(torch.uint8)
+    gx = torch.full((n, cin, hw, hw), float("nan"), device=DEV)
+    rc = hip.lvae_conv3x3_pool_dgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(w), n, c, cin, hw, hw,
+                                         _lib.ptr(gx), _lib.stream_ptr())
+    assert rc == 0
+    g = torch.where(y > 0, gy, torch.zeros_like(gy)).double()
+    g0 = torch.zeros(n, c, ho, ho, 4, dtype=torch.float64, device=DEV)
+    g0.scatter_(-1, idx.long().unsqueeze(-1), g.unsqueeze(-1))
+    g0 = g0.view(n, c, ho, ho, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(n, c, hw, hw)  # k = 2 dy + dx
+    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w.double(), g0, padding=1)
+    assert rel(gx, ref) < 1e-5
+    assert hip.lvae_conv3x3_pool_dgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(w), n, c, 5, hw, hw,
+                                           _lib.ptr(gx), _lib.stream_ptr()) == -3
+    assert hip.lvae_conv3x3_pool_dgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(w), n, 64, cin, 36, 36,
+                                           _lib.ptr(gx), _lib.stream_ptr()) == -4
+
+
 @pytest.mark.parametrize("n,cin,hw", [(5, 16, 18), (37, 16, 18), (3, 5, 7), (2051, 16, 18)])
 def test_deconv_sigmoid_matches_torch(hip, n, cin, hw):
     """Decoder output layer sigmoid(ConvTranspose2d(cin, 1, 4, 2, 1)(z)) as one HIP pass each way vs
