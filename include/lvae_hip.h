@@ -345,7 +345,7 @@ int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* 
 /* The input gradient of the same layer (the second encoder conv, VAE.py:48-50; torch's conv2d backward-data
  * in the reference's autograd): gx [N, Cin, H, W] = the conv's backward-data of the routed gradient (gy at
  * each window's argmax where y > 0), formed per image in LDS, never in HBM.  w [C, Cin, 3, 3].  Cin == 16
- * (-3 otherwise) and lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 64 KB (-4 otherwise).                 */
+ * (-3 otherwise), H W <= 1024 and lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 64 KB (-4 otherwise).      */
 size_t lvae_conv3x3_pool_dgrad_lds(int C, int H, int W);
 int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* w, int N, int C,
                                 int Cin, int H, int W, float* gx, void* stream);

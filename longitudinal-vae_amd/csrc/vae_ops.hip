@@ -14,6 +14,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace lvae {
 
@@ -449,58 +450,72 @@ __global__ __launch_bounds__(256) void wgrad_sum_kernel(const float* __restrict_
 
 // Input gradient of the same conv + relu + pool (the second encoder conv's, VAE.py:48-50), from the pooled
 // gradient: gx[ci][a][b] = sum_{co, ky, kx} g0[co][a + 1 - ky][b + 1 - kx] W[co][ci][ky][kx], g0 the routed
-// full-resolution gradient (gy at each window's argmax where y > 0, 0 elsewhere).  One block per image: g0 is
-// formed in LDS with a zero border straight from (gy, y, idx) -- never written to HBM -- and each thread owns one
-// output pixel with all CI input channels in registers (pairs: packed fp32 FMAs); the 9 taps of a co are read
-// from LDS once for the CI channels, and W's addresses are uniform across the block (scalar loads).  Replaces
-// relu_maxpool2_bwd's full-resolution write plus MIOpen's backward-data conv and its NCHW <-> NHWC transposes.
+// full-resolution gradient (gy at each window's argmax where y > 0, 0 elsewhere).  One block per image, one
+// thread per output pixel with all CI input channels in registers (pairs: packed fp32 FMAs).  g0 is formed in
+// LDS with a zero border straight from (gy, y, idx) -- never written to HBM -- CC channels per stage (a
+// smaller LDS stage: more blocks per CU); the 9 taps of a co are read from LDS once for the CI channels, and
+// W's addresses are uniform across the block (scalar loads).  Replaces relu_maxpool2_bwd's full-resolution
+// write plus MIOpen's backward-data conv and its NCHW <-> NHWC transposes.
 template <int CI>
-__global__ __launch_bounds__(384) void conv3x3_pool_dgrad_kernel(const float* __restrict__ gy,
-                                                                 const float* __restrict__ y,
-                                                                 const uint8_t* __restrict__ idx,
-                                                                 const float* __restrict__ w, int C, int Ho, int Wo,
-                                                                 float* __restrict__ gx) {
+__global__ __launch_bounds__(1024) void conv3x3_pool_dgrad_kernel(const float* __restrict__ gy,
+                                                                  const float* __restrict__ y,
+                                                                  const uint8_t* __restrict__ idx,
+                                                                  const float* __restrict__ w, int C, int Ho, int Wo,
+                                                                  int CC, float* __restrict__ gx) {
   extern __shared__ float sm[];
   const int H = 2 * Ho, W = 2 * Wo, Wp = W + 2, HWp = (H + 2) * Wp, P = Ho * Wo;
   const int t = threadIdx.x, nthr = blockDim.x;
   const int64_t n = blockIdx.x;
-  for (int e = t; e < C * HWp; e += nthr) sm[e] = 0.f;
-  __syncthreads();
+  for (int e = t; e < CC * HWp; e += nthr) sm[e] = 0.f;  // (the border stays zero: each stage rewrites the interior)
   const int64_t b0 = n * C * P;
-  for (int e = t; e < C * P; e += nthr) {
-    const float yv = y[b0 + e], gv = gy[b0 + e];
-    const int k = idx[b0 + e], co = e / P, r = e % P, i = r / Wo, j = r % Wo;
-    if (yv > 0.f) sm[co * HWp + (2 * i + (k >> 1) + 1) * Wp + 2 * j + (k & 1) + 1] = gv;
-  }
-  __syncthreads();
-  float* gxn = gx + n * CI * H * W;
-  for (int p = t; p < H * W; p += nthr) {
-    const int a = p / W, b = p % W;
-    vo_f32x2 acc[CI / 2];
+  const bool act = t < H * W;
+  const int a = t / W, b = t % W;
+  vo_f32x2 acc[CI / 2];
 #pragma unroll
-    for (int c = 0; c < CI / 2; ++c) acc[c] = vo_f32x2{0.f, 0.f};
-    // tap (ky, kx) of output (a, b) reads g0 at padded (a + 2 - ky, b + 2 - kx)
-    const float* g0 = sm + a * Wp + b;
-    for (int co = 0; co < C; ++co) {
-      const float* gc = g0 + co * HWp;
-      const float* wc = w + (int64_t)co * CI * 9;
-      float gt[9];
+  for (int c = 0; c < CI / 2; ++c) acc[c] = vo_f32x2{0.f, 0.f};
+  // tap (ky, kx) of output (a, b) reads g0 at padded (a + 2 - ky, b + 2 - kx)
+  const float* g0 = sm + a * Wp + b;
+  for (int c0 = 0; c0 < C; c0 += CC) {
+    const int cc = min(CC, C - c0);
+    __syncthreads();  // the previous stage's reads (and the zeroing) are done
+    for (int e = t; e < cc * P; e += nthr) {
+      const int c = e / P, r = e % P, i = r / Wo, j = r % Wo;
+      const int64_t s = b0 + (int64_t)c0 * P + e;
+      const float yv = y[s], gv = gy[s];
+      const int k = idx[s];
+      const float g = yv > 0.f ? gv : 0.f;
+      float* q = sm + c * HWp + (2 * i + 1) * Wp + 2 * j + 1;
+      q[0] = k == 0 ? g : 0.f;
+      q[1] = k == 1 ? g : 0.f;
+      q[Wp] = k == 2 ? g : 0.f;
+      q[Wp + 1] = k == 3 ? g : 0.f;
+    }
+    __syncthreads();
+    if (act) {
+      for (int co = 0; co < cc; ++co) {
+        const float* gc = g0 + co * HWp;
+        const float* wc = w + (int64_t)(c0 + co) * CI * 9;
+        float gt[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) gt[k] = gc[(2 - k / 3) * Wp + 2 - k % 3];
+        for (int k = 0; k < 9; ++k) gt[k] = gc[(2 - k / 3) * Wp + 2 - k % 3];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const vo_f32x2 g2{gt[k], gt[k]};
+        for (int k = 0; k < 9; ++k) {
+          const vo_f32x2 g2{gt[k], gt[k]};
 #pragma unroll
-        for (int c = 0; c < CI / 2; ++c) {
-          const vo_f32x2 w2{wc[(2 * c) * 9 + k], wc[(2 * c + 1) * 9 + k]};
-          acc[c] = __builtin_elementwise_fma(g2, w2, acc[c]);
+          for (int c = 0; c < CI / 2; ++c) {
+            const vo_f32x2 w2{wc[(2 * c) * 9 + k], wc[(2 * c + 1) * 9 + k]};
+            acc[c] = __builtin_elementwise_fma(g2, w2, acc[c]);
+          }
         }
       }
     }
+  }
+  if (act) {
+    float* gxn = gx + n * CI * H * W + t;
 #pragma unroll
     for (int c = 0; c < CI / 2; ++c) {
-      gxn[(int64_t)(2 * c) * H * W + p] = acc[c][0];
-      gxn[(int64_t)(2 * c + 1) * H * W + p] = acc[c][1];
+      gxn[(int64_t)(2 * c) * H * W] = acc[c][0];
+      gxn[(int64_t)(2 * c + 1) * H * W] = acc[c][1];
     }
   }
 }
@@ -640,7 +655,17 @@ int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* 
   return 0;
 }
 
-size_t lvae_conv3x3_pool_dgrad_lds(int C, int H, int W) { return sizeof(float) * (size_t)C * (H + 2) * (W + 2); }
+// channels per LDS stage of conv3x3_pool_dgrad_kernel: LVAE_DGRAD_CC (A/B runs), default 0 = all C in one stage
+// (at the headline shape 243-256 us vs 257-269 with 16-channel stages and 268-278 with 8: the smaller stage's
+// extra blocks per CU do not pay for its extra barriers; profiles/r5_conv_dgrad_ab.txt)
+static int dgrad_cc(int C) {
+  static const int v = getenv("LVAE_DGRAD_CC") ? atoi(getenv("LVAE_DGRAD_CC")) : 0;
+  return v <= 0 || v > C ? C : v;
+}
+
+size_t lvae_conv3x3_pool_dgrad_lds(int C, int H, int W) {
+  return sizeof(float) * (size_t)dgrad_cc(C) * (H + 2) * (W + 2);
+}
 
 int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* w, int N, int C,
                                 int Cin, int H, int W, float* gx, void* stream) {
@@ -648,10 +673,11 @@ int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* 
   if (N < 0 || C <= 0 || Cin <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return -2;
   if (Cin != 16) return -3;
   const size_t lds = lvae_conv3x3_pool_dgrad_lds(C, H, W);
-  if (lds > 64 * 1024) return -4;
+  if (lds > 64 * 1024 || H * W > 1024) return -4;
   if (N == 0) return 0;
-  const int nthr = (int)std::min<int64_t>(384, cdiv((int64_t)H * W, 64) * 64);
-  conv3x3_pool_dgrad_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2, gx);
+  const int nthr = (int)cdiv((int64_t)H * W, 64) * 64;
+  conv3x3_pool_dgrad_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2, dgrad_cc(C),
+                                                                       gx);
   LVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -103,7 +103,8 @@ class _ConvReluMaxPool2(torch.autograd.Function):
                                                         H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
                                                         _lib.stream_ptr()), "conv3x3_pool_wgrad")
             gx = None
-            if ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536:
+            if (ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and H * W <= 1024
+                    and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536):
                 # the input gradient straight from the pooled gradient too (lvae_conv3x3_pool_dgrad_f32: the
                 # routed gradient formed per image in LDS; no MIOpen backward-data conv, no transposes)
                 gx = torch.empty(N, Cin, H, W, dtype=gy.dtype, device=gy.device)
