@@ -15,6 +15,17 @@ from torch import nn
 # LVAE_CONV_DGRAD=0: the second encoder conv's input gradient on MIOpen (routed gradient + backward-data conv)
 # instead of lvae_conv3x3_pool_dgrad_f32 (A/B runs)
 _CONV_DGRAD = os.environ.get("LVAE_CONV_DGRAD", "1") != "0"
+# LVAE_CONV_BWD_FORK=0: that layer's weight-gradient and input-gradient kernels one after the other on the
+# backward's stream instead of side by side (the weight gradient on a side stream, joined before returning)
+_CONV_BWD_FORK = os.environ.get("LVAE_CONV_BWD_FORK", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 class _ReluMaxPool2(torch.autograd.Function):
@@ -95,22 +106,32 @@ class _ConvReluMaxPool2(torch.autograd.Function):
             # weight and bias gradients from the pooled gradient (lvae_conv3x3_pool_wgrad_f32); the first
             # conv (image input) needs no input gradient
             xc = x.contiguous()
-            dw = torch.empty_like(weight)
-            db = torch.empty(C, dtype=gy.dtype, device=gy.device)
-            ws = torch.empty(lib.lvae_conv3x3_pool_wgrad_workspace_size(N, C, Cin) // 4 + 1, dtype=torch.float32,
-                             device=gy.device)
-            _lib.check(lib.lvae_conv3x3_pool_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N, C, Cin,
-                                                        H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
-                                                        _lib.stream_ptr()), "conv3x3_pool_wgrad")
+            dgrad = (ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and H * W <= 1024
+                     and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536)
+            cur = torch.cuda.current_stream(gy.device)
+            side = _side_stream(gy.device) if dgrad and _CONV_BWD_FORK else None
+            if side is not None:  # (the weight gradient beside the input gradient; joined below)
+                side.wait_stream(cur)
+            with torch.cuda.stream(side if side is not None else cur):
+                dw = torch.empty_like(weight)
+                db = torch.empty(C, dtype=gy.dtype, device=gy.device)
+                ws = torch.empty(lib.lvae_conv3x3_pool_wgrad_workspace_size(N, C, Cin) // 4 + 1, dtype=torch.float32,
+                                 device=gy.device)
+                _lib.check(lib.lvae_conv3x3_pool_wgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), _lib.ptr(xc), N, C,
+                                                            Cin, H, W, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                                            _lib.stream_ptr()), "conv3x3_pool_wgrad")
             gx = None
-            if (ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and H * W <= 1024
-                    and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536):
+            if dgrad:
                 # the input gradient straight from the pooled gradient too (lvae_conv3x3_pool_dgrad_f32: the
                 # routed gradient formed per image in LDS; no MIOpen backward-data conv, no transposes)
                 gx = torch.empty(N, Cin, H, W, dtype=gy.dtype, device=gy.device)
                 _lib.check(lib.lvae_conv3x3_pool_dgrad_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx),
                                                             _lib.ptr(weight.contiguous()), N, C, Cin, H, W,
                                                             _lib.ptr(gx), _lib.stream_ptr()), "conv3x3_pool_dgrad")
+                if side is not None:
+                    cur.wait_stream(side)
+                    dw.record_stream(cur)
+                    db.record_stream(cur)
             elif ctx.needs_input_grad[0]:
                 g0 = torch.empty(N, C, H, W, dtype=gy.dtype, device=gy.device)
                 _lib.check(lib.lvae_relu_maxpool2_bwd_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(idx), N * C, H, W,
