@@ -109,7 +109,10 @@ class _ConvReluMaxPool2(torch.autograd.Function):
             dgrad = (ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and H * W <= 1024
                      and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536)
             cur = torch.cuda.current_stream(gy.device)
-            side = _side_stream(gy.device) if dgrad and _CONV_BWD_FORK else None
+            # (eager only: a fork inside a HIP graph capture crashed the capture's end -- test_gpu_rccl's
+            # test_graphed_closed_step_matches_eager; captured steps keep the one-stream order)
+            side = (_side_stream(gy.device) if dgrad and _CONV_BWD_FORK and not torch.cuda.is_current_stream_capturing()
+                    else None)
             if side is not None:  # (the weight gradient beside the input gradient; joined below)
                 side.wait_stream(cur)
             with torch.cuda.stream(side if side is not None else cur):
