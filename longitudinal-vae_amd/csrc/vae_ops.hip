@@ -520,6 +520,70 @@ __global__ __launch_bounds__(1024) void conv3x3_pool_dgrad_kernel(const float* _
   }
 }
 
+// The same input gradient with one thread per horizontal pixel pair (a, b), (a, b + 1) (b even): the packed
+// FMAs pair the two pixels (g from two adjacent LDS words, W's scalar broadcast to both halves) instead of two
+// input channels, so W's per-tap scalar loads serve twice the FMAs and no SGPR pairs need assembling.
+template <int CI>
+__global__ __launch_bounds__(512) void conv3x3_pool_dgrad2_kernel(const float* __restrict__ gy,
+                                                                  const float* __restrict__ y,
+                                                                  const uint8_t* __restrict__ idx,
+                                                                  const float* __restrict__ w, int C, int Ho, int Wo,
+                                                                  float* __restrict__ gx) {
+  extern __shared__ float sm[];
+  const int H = 2 * Ho, W = 2 * Wo, Wp = W + 2, HWp = (H + 2) * Wp, P = Ho * Wo;
+  const int t = threadIdx.x, nthr = blockDim.x;
+  const int64_t n = blockIdx.x;
+  for (int e = t; e < (H + 2) * Wp; e += nthr) {  // the zero border of every channel plane
+    const int r = e / Wp, c = e % Wp;
+    if (r == 0 || r == H + 1 || c == 0 || c == W + 1)
+      for (int co = 0; co < C; ++co) sm[co * HWp + e] = 0.f;
+  }
+  const int64_t b0 = n * C * P;
+  for (int e = t; e < C * P; e += nthr) {
+    const int c = e / P, r = e % P, i = r / Wo, j = r % Wo;
+    const float yv = y[b0 + e], gv = gy[b0 + e];
+    const int k = idx[b0 + e];
+    const float g = yv > 0.f ? gv : 0.f;
+    float* q = sm + c * HWp + (2 * i + 1) * Wp + 2 * j + 1;
+    q[0] = k == 0 ? g : 0.f;
+    q[1] = k == 1 ? g : 0.f;
+    q[Wp] = k == 2 ? g : 0.f;
+    q[Wp + 1] = k == 3 ? g : 0.f;
+  }
+  __syncthreads();
+  const int a = t / Wo, b = 2 * (t % Wo);
+  if (t >= H * Wo) return;  // (after the only barrier)
+  vo_f32x2 acc[CI];
+#pragma unroll
+  for (int c = 0; c < CI; ++c) acc[c] = vo_f32x2{0.f, 0.f};
+  // tap (ky, kx) of pixel (a, b + d) reads g0 at padded (a + 2 - ky, b + d + 2 - kx)
+  const float* g0 = sm + a * Wp + b;
+  for (int co = 0; co < C; ++co) {
+    const float* gc = g0 + co * HWp;
+    const float* wc = w + (int64_t)co * CI * 9;
+    vo_f32x2 gp[9];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const vo_f32x2 lo = *reinterpret_cast<const vo_f32x2*>(gc + (2 - ky) * Wp);
+      const vo_f32x2 hi = *reinterpret_cast<const vo_f32x2*>(gc + (2 - ky) * Wp + 2);
+      gp[3 * ky + 0] = hi;
+      gp[3 * ky + 1] = vo_f32x2{lo[1], hi[0]};
+      gp[3 * ky + 2] = lo;
+    }
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const float wv = wc[c * 9 + k];
+        acc[c] = __builtin_elementwise_fma(gp[k], vo_f32x2{wv, wv}, acc[c]);
+      }
+    }
+  }
+  float* gxn = gx + n * CI * H * W + a * W + b;
+#pragma unroll
+  for (int c = 0; c < CI; ++c) *reinterpret_cast<vo_f32x2*>(gxn + (int64_t)c * H * W) = acc[c];
+}
+
 }  // namespace lvae
 
 using namespace lvae;
@@ -675,9 +739,17 @@ int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* 
   const size_t lds = lvae_conv3x3_pool_dgrad_lds(C, H, W);
   if (lds > 64 * 1024 || H * W > 1024) return -4;
   if (N == 0) return 0;
-  const int nthr = (int)cdiv((int64_t)H * W, 64) * 64;
-  conv3x3_pool_dgrad_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2, dgrad_cc(C),
-                                                                       gx);
+  // LVAE_DGRAD_PAIR=1: one thread per pixel pair (pixel-paired FMAs) instead of per pixel (channel-paired); off by
+  // default until measured (scripts/gpu_dgrad_pair.sh)
+  static const bool pair = getenv("LVAE_DGRAD_PAIR") && atoi(getenv("LVAE_DGRAD_PAIR")) != 0;
+  if (pair && dgrad_cc(C) == C) {
+    const int nthr = (int)cdiv((int64_t)H * W / 2, 64) * 64;
+    conv3x3_pool_dgrad2_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2, gx);
+  } else {
+    const int nthr = (int)cdiv((int64_t)H * W, 64) * 64;
+    conv3x3_pool_dgrad_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2,
+                                                                         dgrad_cc(C), gx);
+  }
   LVAE_CHECK_LAUNCH();
   return 0;
 }
