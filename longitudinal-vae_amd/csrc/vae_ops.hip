@@ -739,9 +739,10 @@ int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* 
   const size_t lds = lvae_conv3x3_pool_dgrad_lds(C, H, W);
   if (lds > 64 * 1024 || H * W > 1024) return -4;
   if (N == 0) return 0;
-  // LVAE_DGRAD_PAIR=1: one thread per pixel pair (pixel-paired FMAs) instead of per pixel (channel-paired); off by
-  // default until measured (scripts/gpu_dgrad_pair.sh)
-  static const bool pair = getenv("LVAE_DGRAD_PAIR") && atoi(getenv("LVAE_DGRAD_PAIR")) != 0;
+  // LVAE_DGRAD_PAIR=0: one thread per pixel (channel-paired FMAs) instead of per pixel pair (pixel-paired: 209-221
+  // vs 244-256 us at the headline shape; the step is unchanged, the weight-gradient kernel beside it is the longer
+  // of the two; profiles/r5_conv_dgrad_ab.txt)
+  static const bool pair = !getenv("LVAE_DGRAD_PAIR") || atoi(getenv("LVAE_DGRAD_PAIR")) != 0;
   if (pair && dgrad_cc(C) == C) {
     const int nthr = (int)cdiv((int64_t)H * W / 2, 64) * 64;
     conv3x3_pool_dgrad2_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2, gx);
