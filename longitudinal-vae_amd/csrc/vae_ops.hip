@@ -687,8 +687,15 @@ static size_t conv3x3_pool_wgrad_lds(int C, int Cin, int H, int W) {
   return sizeof(float) * (stage > 2560 ? stage : 2560);
 }
 
+// images per block of conv3x3_pool_wgrad_kernel: imgs_per_block, or LVAE_WGRAD_PER (A/B runs; read once, so the
+// workspace size query and the launch agree)
+static int wgrad_per(int N) {
+  static const int v = getenv("LVAE_WGRAD_PER") ? atoi(getenv("LVAE_WGRAD_PER")) : 0;
+  return v > 0 ? v : imgs_per_block(N);
+}
+
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin) {
-  return N <= 0 || C <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)C * Cin * 9 + C) * (size_t)cdiv(N, imgs_per_block(N));
+  return N <= 0 || C <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)C * Cin * 9 + C) * (size_t)cdiv(N, wgrad_per(N));
 }
 
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
@@ -705,7 +712,7 @@ int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* 
     (void)hipMemsetAsync(db, 0, sizeof(float) * C, st);
     return 0;
   }
-  const int per = imgs_per_block(N), nb = (int)cdiv(N, per), m = Q * 9 + C;
+  const int per = wgrad_per(N), nb = (int)cdiv(N, per), m = Q * 9 + C;
   float* part = (float*)workspace;
   const int Ho = H / 2, Wo = W / 2;
   switch (NP) {
