@@ -304,7 +304,8 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
  * iH: H^-1 if the caller already has it (e.g. workspace + lvae_hensman_iH_offset after the
  * forward on the same H), else NULL (H is inverted here, as training.py:130-131 does).
  * info[l] (may be NULL): the first failed factorisation of dim l (H's, then iH''s), LAPACK-style;
- * a dim whose factorisation fails keeps its (m, H) unchanged.
+ * if any dim's factorisation fails, NO dim's (m, H) is changed (the reference's batched
+ * torch.cholesky raises before assigning, training.py:130-134).
  * workspace: lvae_natgrad_workspace_size(L, M) bytes.                                        */
 size_t lvae_natgrad_workspace_size(int L, int M);
 int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* grad_m,

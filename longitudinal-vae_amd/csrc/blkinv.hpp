@@ -218,10 +218,13 @@ struct BlkInvLds {
 //   in : element (i, j) at in[i * ldi + j], i, j < n; only the lower triangle is read
 //   out: A^-1 element (i, j) at out[i * ldo + j]
 //   logdet: log|A| (accumulate = 1: +=);  info: first bad pivot column + col_offset
-template <typename T, int TS, int TPW>
-__device__ inline void blk_inverse(int n, const T* __restrict__ in, int64_t ldi, T* __restrict__ out, int64_t ldo,
+//   MODE 1 (the N x N potrf's diagonal blocks, potrf.hip): stop after pass 2 -- L into lout (lower, i >= j),
+//   Y = L^-1's strict lower part TRANSPOSED into out's strict upper triangle (out[j * ldo + i], i > j; out may be
+//   null).  in / out / lout may alias: every read of in precedes the first write.
+template <typename T, int TS, int TPW, int MODE = 0>
+__device__ inline void blk_inverse(int n, const T* in, int64_t ldi, T* out, int64_t ldo,
                                    double* __restrict__ logdet, int accumulate, int32_t* __restrict__ info,
-                                   int col_offset) {
+                                   int col_offset, T* lout = nullptr, int64_t ldl = 0) {
   typedef BiTraits<T> Tr;
   typedef typename Tr::acc_t acc_t;
   typedef BlkInvLds<T, TS> Lds;
@@ -369,6 +372,25 @@ __device__ inline void blk_inverse(int n, const T* __restrict__ in, int64_t ldi,
     }
   }
 
+  if constexpr (MODE == 1) {
+    if (out) {
+#pragma unroll
+      for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = tr * 16 + rw[r], j = (tc0 + u) * 16 + lc;
+          if (j < i && i < n) out[(int64_t)j * ldo + i] = acc[u][r];
+        }
+    }
+    for (int e = t; e < 256 * TS * TS; e += NT) {
+      const int i = e / (16 * TS), j = e % (16 * TS);
+      if (j <= i && i < n) {
+        const int I = i >> 4, J = j >> 4;
+        lout[(int64_t)i * ldl + j] = I == J ? sm.Lkk[I][(i & 15) * BLD + (j & 15)]
+                                            : sm.W[I * (I - 1) / 2 + J][(i & 15) * BLD + (j & 15)];
+      }
+    }
+  } else {
   // ---------------- pass 3: A^-1 = L^-T Y ----------------
   for (int k = TS - 1; k >= 0; --k) {
     LVAE_BI_ROW_SOLVE(k, TS, true, k > 0);  // R_k <- X_k^T R_k
@@ -396,6 +418,7 @@ __device__ inline void blk_inverse(int n, const T* __restrict__ in, int64_t ldi,
       const int i = tr * 16 + rw[r], j = (tc0 + u) * 16 + lc;
       if (i < n && j < n) out[(int64_t)i * ldo + j] = acc[u][r];
     }
+  }
   // log|A| = 2 sum log L_jj over the pivot blocks (off the step critical path)
   double lgd = 0.0;
   for (int i = t; i < 16 * TS; i += NT) lgd += log((double)sm.pdiag[i]);

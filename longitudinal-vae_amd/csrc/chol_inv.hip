@@ -1497,9 +1497,9 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     std::lock_guard<std::recursive_mutex> lock(side_mutex());
     SideStream* sd = nullptr;
     LVAE_TRY(side_stream(sd));
-    (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
-    (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
-    (void)hipMemsetAsync(S.cnt, 0, CiScratch::cnt_bytes(L, nt), st);  // the split pivots' tickets
+    (void)zero_async(logdet, sizeof(double) * L, st);
+    (void)zero_async(info, sizeof(int32_t) * L, st);
+    (void)zero_async(S.cnt, CiScratch::cnt_bytes(L, nt), st);  // the split pivots' tickets
     if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
     const bool fuse = L <= kCiFuseMaxL;
     const int pmode = lout ? 0 : ci_pipe_mode(np_, L);  // (implies fuse and the XR planes)

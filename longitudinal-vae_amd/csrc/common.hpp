@@ -23,6 +23,37 @@ constexpr int kWave = 64;
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Zero `bytes` bytes at p (4-byte aligned) on st with a kernel.  The library never calls hipMemsetAsync: a memset
+// captured into a HIP graph by stream capture was found not to zero its target on the replays after the first
+// (ROCm 7.0 runtime; scripts/dp_replay_diag.py: the natural-gradient update's info array kept stale bytes in
+// the data-parallel step's second graph), while kernel nodes replay exactly.
+static __global__ __launch_bounds__(256) void lvae_zero_kernel(uint32_t* __restrict__ p, int64_t words,
+                                                               uint8_t* __restrict__ tail, int ntail) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < words) p[e] = 0u;
+  if (e < ntail) tail[e] = 0;
+}
+// dst[0..words) = src[0..words) (4-byte words): small device-to-device copies as a kernel node, like zero_async
+static __global__ __launch_bounds__(256) void lvae_copy_words_kernel(uint32_t* __restrict__ dst,
+                                                                     const uint32_t* __restrict__ src, int64_t words) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < words) dst[e] = src[e];
+}
+static inline int copy_words_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  const int64_t words = (int64_t)(bytes / 4);
+  if (words <= 0) return 0;
+  lvae_copy_words_kernel<<<(unsigned)((words + 255) / 256), 256, 0, st>>>((uint32_t*)dst, (const uint32_t*)src, words);
+  return hipGetLastError() == hipSuccess ? 0 : LVAE_ERR_LAUNCH;
+}
+static inline int zero_async(void* p, size_t bytes, hipStream_t st) {
+  if (!p || !bytes) return 0;
+  const int64_t words = (int64_t)(bytes / 4);
+  const int ntail = (int)(bytes & 3);
+  const int64_t n = words > ntail ? words : ntail;
+  lvae_zero_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>((uint32_t*)p, words, (uint8_t*)p + 4 * words, ntail);
+  return hipGetLastError() == hipSuccess ? 0 : LVAE_ERR_LAUNCH;
+}
+
 // Split scale of the fp32-accurate f16 GEMMs (mfma_x3.hpp, x3_dma.hpp): x sc = hi + lo in fp16.
 // The power of two 2^floor(log2(2^14 / bound)), clamped to [2^-40, 2^40] (bound 0 or inf / NaN ->
 // 1): every |x| <= bound splits without overflow, and the largest entries keep 2^13..2^14 -- the

@@ -172,13 +172,14 @@ __global__ void step_terms_bwd_kernel(const double* __restrict__ g_net, const fl
 }
 
 // ---- bias_act: [N, C, HW] fp32 (HW = 1: a Linear's [B, F] rows) --------------------------------------------
-// y = relu(y + b[c]) in place
+// y = relu(y + b[c]) in place; NaN stays NaN (torch.relu), so a diverging layer shows in the loss
 __global__ __launch_bounds__(256) void bias_relu_fwd_kernel(float* __restrict__ y, const float* __restrict__ b, int C,
                                                             int HW, int64_t total) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
   const int c = (int)((e / HW) % C);
-  y[e] = fmaxf(y[e] + b[c], 0.f);
+  const float v = y[e] + b[c];
+  y[e] = v < 0.f ? 0.f : v;
 }
 
 constexpr int kActRows = 64;  // images (rows) per partial chunk
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(256) void act_bwd_rows_kernel(const float* __restri
     for (int k = ty; k < kActRows && n0 + k < N; k += 4) {
       const int64_t o = (int64_t)(n0 + k) * C + c;
       float v = gy[o];
-      if (relu) v = y[o] > 0.f ? v : 0.f;
+      if (relu) v = y[o] <= 0.f ? 0.f : v;  // (torch's threshold_backward: NaN y passes the gradient)
       if (g) g[o] = v;
       s += v;
     }
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void act_bwd_chan_kernel(const float* __restri
     const int64_t o0 = ((int64_t)(n0 + im) * C + c) * HW;
     for (int h = tid; h < HW; h += 256) {
       float v = gy[o0 + h];
-      if (relu) v = y[o0 + h] > 0.f ? v : 0.f;
+      if (relu) v = y[o0 + h] <= 0.f ? 0.f : v;
       if (g) g[o0 + h] = v;
       s += v;
     }
@@ -362,7 +363,7 @@ int lvae_act_bwd_f32(const float* gy, const float* y, int N, int C, int HW, int 
   if (relu && (!y || !g)) return -1;
   if (N < 0 || C <= 0 || HW <= 0) return -2;
   if (N == 0) {
-    if (hipMemsetAsync(db, 0, (size_t)C * sizeof(float), (hipStream_t)stream) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (zero_async(db, (size_t)C * sizeof(float), (hipStream_t)stream) != 0) return LVAE_ERR_LAUNCH;
     return 0;
   }
   const int nchunk = (N + kActRows - 1) / kActRows;

@@ -462,9 +462,9 @@ int lvae_hensman_bwd_f64(const lvae_kernel_spec* spec0, const lvae_kernel_spec* 
   gb_kernel<<<blocks(LTT), 256, 0, st>>>(P_b, T, L, kc, gkld, w.iB, w.s, w.iBVB, w.iBK0iB, w.QB, d.seg_len, w.GB,
                                           w.GK0);
   // hyper-parameter gradients through the four Grams
-  (void)hipMemsetAsync(dparams0, 0, sizeof(double) * L * spec0->n_params, st);
-  (void)hipMemsetAsync(dparams1, 0, sizeof(double) * L * spec1->n_params, st);
-  if (dnoise) (void)hipMemsetAsync(dnoise, 0, sizeof(double) * L, st);
+  (void)zero_async(dparams0, sizeof(double) * L * spec0->n_params, st);
+  (void)zero_async(dparams1, sizeof(double) * L * spec1->n_params, st);
+  if (dnoise) (void)zero_async(dnoise, sizeof(double) * L, st);
   const lvae_xview xv{x, 0, 0, Q}, zv{z, 0, (int64_t)M * Q, Q}, xs{x, (int64_t)T * Q, 0, Q};
   {
     const GramBwdJob jobs[4] = {
@@ -497,9 +497,12 @@ size_t lvae_natgrad_workspace_size(int L, int M) {
 }
 
 // iHn = iH + lr (gH + gH^T) in one pass (was a copy, an axpy and a transpose-add)
+// (and inf0[0..L) = 0 when H^-1 came from the caller: no factorisation of H here -- a kernel store, not a
+// hipMemsetAsync node: see DESIGN.md section 5 on the captured memsets)
 __global__ void natgrad_ih_kernel(int L, int M, double lr, const double* __restrict__ iH, const double* __restrict__ gH,
-                                  double* __restrict__ iHn) {
+                                  double* __restrict__ iHn, int32_t* __restrict__ inf0) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, MM = (int64_t)M * M;
+  if (inf0 && e < L) inf0[e] = 0;
   if (e >= L * MM) return;
   const int64_t b = e / MM, r = (e % MM) / M, c = e % M;
   iHn[e] = iH[e] + lr * (gH[e] + gH[b * MM + c * M + r]);
@@ -512,20 +515,21 @@ __global__ void natgrad_y_kernel(int64_t n, double lr, const double* __restrict_
   if (e < n) y[e] = v[e] - lr * gm[e] + 2.0 * lr * gw[e];
 }
 
-// commit: per dim l, (m, H) <- (mn, Hn) only if both factorisations (H^-1 when it was computed here, iH'^-1)
-// succeeded; info[l] = the first failure's LAPACK code (H's, else iH''s), 0 = ok.  A failed dim keeps its
-// (m, H) (the reference raises from torch.cholesky before assigning them, training.py:130-134).
+// commit: (m, H) <- (mn, Hn) for EVERY dim only if all factorisations of all dims (H^-1 when it was computed here,
+// iH'^-1) succeeded, as the reference's batched torch.cholesky raises before anything is assigned
+// (training.py:130-134); info[l] = dim l's first failure's LAPACK code (H's, else iH''s), 0 = ok
 __global__ void natgrad_commit_kernel(int L, int M, const int32_t* __restrict__ inf, const double* __restrict__ Hn,
                                       const double* __restrict__ mn, double* __restrict__ H, double* __restrict__ m,
                                       int32_t* __restrict__ info) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, MM = (int64_t)M * M;
+  int bad = 0;
+  for (int q = 0; q < 2 * L; ++q) bad |= inf[q];
   if (e < L * MM) {
-    const int l = (int)(e / MM);
-    if (inf[l] == 0 && inf[L + l] == 0) H[e] = Hn[e];
+    if (!bad) H[e] = Hn[e];
   } else if (e < L * MM + (int64_t)L * M) {
     const int64_t q = e - L * MM;
     const int l = (int)(q / M);
-    if (inf[l] == 0 && inf[L + l] == 0) m[q] = mn[q];
+    if (!bad) m[q] = mn[q];
     if (q % M == 0 && info) info[l] = inf[l] != 0 ? inf[l] : inf[L + l];
   }
 }
@@ -549,13 +553,9 @@ int lvae_natgrad_update_f64(int L, int M, double* m, double* H, const double* gr
   double* y = (double*)(base + 3 * mmb + 2 * vb);
   double* ld = (double*)(base + 3 * mmb + 3 * vb);
   int32_t* inf = (int32_t*)(base + 3 * mmb + 3 * vb + align256((size_t)L * sizeof(double)));
-  if (iH_in) {
-    (void)hipMemsetAsync(inf, 0, sizeof(int32_t) * L, st);
-  } else {
-    LVAE_TRY(spd_inv_small_f64(M, L, H, MM, iH, MM, ld, inf, st));
-  }
+  if (!iH_in) LVAE_TRY(spd_inv_small_f64(M, L, H, MM, iH, MM, ld, inf, st));
   // iH' = iH + lr (gH + gH^T)
-  natgrad_ih_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, iHc, grad_H, iHn);
+  natgrad_ih_kernel<<<blocks(L * MM), 256, 0, st>>>(L, M, lr, iHc, grad_H, iHn, iH_in ? inf : nullptr);
   // v = iH m ; gw = gH m; Hn = iH'^-1; y = v - lr gm + 2 lr gw ; mn = Hn y (into gw, dead after y); then the
   // commit writes (mn, Hn) over (m, H) for the dims whose factorisations succeeded
   LVAE_TRY(gemm_small_f64(0, 0, M, 1, M, 1.0, iHc, M, MM, 0, m, 1, M, 0, 0.0, v, 1, M, 0, L, 1, st));

@@ -474,8 +474,8 @@ int lvae_kl_closed_refine_state(int n, int L, const void* workspace, double* est
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemcpyAsync(est, ws.rest, (size_t)L * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(flag, ws.rflag, (size_t)L * sizeof(int32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+  if (copy_words_async(est, ws.rest, (size_t)L * sizeof(double), st) != 0 ||
+      copy_words_async(flag, ws.rflag, (size_t)L * sizeof(int32_t), st) != 0)
     return LVAE_ERR_LAUNCH;
   return 0;
 }

@@ -940,7 +940,7 @@ int kl_hyper_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n,
   HbWs ws((char*)wsbase, np_, L);
   GramTab tb;
   if (!hb_host_ok(spec, tb)) {
-    if (hipMemsetAsync(ws.dev, 0, sizeof(HbDev), st) != hipSuccess) return LVAE_ERR_LAUNCH;
+    if (zero_async(ws.dev, sizeof(HbDev), st) != 0) return LVAE_ERR_LAUNCH;
     return 0;
   }
   hb_plan_kernel<<<1, 1024, 0, st>>>(tb, x, ldx, n, np_, covflag, ws, 1);
@@ -957,7 +957,10 @@ int kl_hyper_bwd(const lvae_kernel_spec* spec, const double* x, int ldx, int n, 
   (void)ldx;
   HbWs ws((char*)wsbase, np_, L);
   GramTab tb;
-  if (!hb_host_ok(spec, tb)) return 0;
+  // (not hb_host_ok: LVAE_KL_HYPER is the forward's decision, recorded in the plan's device flag -- the kernels
+  // below exit at once when it is off -- so a change of the variable between forward and backward cannot leave
+  // the S-GEMM half skipped and this half unlaunched)
+  if (!gram_tab_build(spec, tb) || hb_slab_lds(tb) == 0) return 0;
   const size_t tabb = (size_t)tb.pbeg[tb.ng] * (1 << tb.nbits) * kTabR * sizeof(float);
   const size_t sdyn = hb_slab_lds(tb), ndyn = sdyn;
   const int nt = np_ / kHbT;
@@ -984,7 +987,6 @@ extern "C" int lvae_kl_closed_hyper_state(int n, int L, const void* workspace, i
   const int np_ = (n + 255) / 256 * 256;
   const char* hb = (const char*)workspace + kl_hyper_offset_in_kl_ws(np_, L);
   const lvae::HbWs ws(const_cast<char*>(hb), np_, L);
-  if (hipMemcpyAsync(on, &ws.dev->on, sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess)
-    return LVAE_ERR_LAUNCH;
+  if (lvae::copy_words_async(on, &ws.dev->on, sizeof(int32_t), (hipStream_t)stream) != 0) return LVAE_ERR_LAUNCH;
   return 0;
 }

@@ -300,8 +300,8 @@ int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n
                    double* part, double* est, int* flag, hipStream_t st) {
   const int mode = refine_mode();
   if (mode == 0) {  // off: only the state lvae_kl_closed_refine_state reports
-    if (hipMemsetAsync(est, 0, (size_t)L * sizeof(double), st) != hipSuccess ||
-        hipMemsetAsync(flag, 0, (size_t)L * sizeof(int), st) != hipSuccess)
+    if (zero_async(est, (size_t)L * sizeof(double), st) != 0 ||
+        zero_async(flag, (size_t)L * sizeof(int), st) != 0)
       return LVAE_ERR_LAUNCH;
     return 0;
   }

@@ -2,9 +2,10 @@
 //   LK1 = torch.cholesky(K1);  torch.cholesky_solve(B, LK1);  2 sum log diag(LK1)      (elbo_functions.py:26-29)
 // as LAPACK-shaped calls over L batched matrices:
 //   lvae_potrf_f64   blocked right-looking Cholesky in fp64: 64-wide block columns; per pass one launch factors
-//                    the diagonal block in LDS and solves the panel L_ik L_kk^T = A_ik by substitution (as
-//                    LAPACK's potrf + trsm), one launch applies the trailing update A_IJ -= L_Ik L_Jk^T on
-//                    v_mfma_f64_16x16x4f64 (the n^3/3 flops)
+//                    the diagonal block and inverts its factor (16 x 16 pivots in f64 MFMA accumulators), one
+//                    solves the panel as the product L_ik = A_ik L_kk^-T (the trtri-based trsm of MAGMA /
+//                    rocSOLVER), one applies the trailing update A_IJ -= L_Ik L_Jk^T -- all on
+//                    v_mfma_f64_16x16x4f64
 //   lvae_potrf_f32   the exact KL's own factorisation (chol_inv.hip: 256-wide blocks, pivots in LDS on fp32
 //                    MFMA, panels / trailing updates on the f16 cores with the 3-product split), stopped after
 //                    potrf and exported as an fp32 L
@@ -33,88 +34,6 @@ __device__ inline void p64_tri(int t, int& I, int& J) {  // t -> (I, J), J <= I,
   J = t - r * (r + 1) / 2;
 }
 
-// the SPD block in S (lower triangle valid; padding rows / columns = identity) -> its Cholesky factor in place
-// (lower; the strict upper part is not touched).  All 256 threads, 3 barriers per column.  bad_s: the first
-// column whose pivot is not positive (-1: none); such a pivot's square root is NaN and propagates, as the
-// caller reports info and the values are then undefined (LAPACK's contract).
-__device__ inline void p64_chol_lds(double* __restrict__ S, double* __restrict__ piv, int* bad_s) {
-  const int tid = threadIdx.x;
-  for (int j = 0; j < kPB; ++j) {
-    if (tid == 0) {
-      const double d = S[j * kPBL + j];
-      if (!(d > 0.0 && isfinite(d)) && *bad_s < 0) *bad_s = j;
-      const double p = sqrt(d);
-      S[j * kPBL + j] = p;
-      piv[j] = p;
-    }
-    __syncthreads();
-    const double ip = 1.0 / piv[j];
-    for (int i = j + 1 + tid; i < kPB; i += 256) S[i * kPBL + j] *= ip;
-    __syncthreads();
-    const int m = kPB - j - 1;
-    for (int e = tid; e < m * m; e += 256) {
-      const int i = j + 1 + e / m, c = j + 1 + e % m;
-      if (c <= i) S[i * kPBL + c] -= S[i * kPBL + j] * S[c * kPBL + j];
-    }
-    __syncthreads();
-  }
-}
-
-// pass k of the fp64 potrf, workgroup (b, l): block row i = k + b.  Every workgroup factors A_kk in LDS (the
-// panel then waits for no other launch); b = 0 writes L_kk and zeroes the rest of its block row's upper part,
-// adds 2 sum log L_jj to logdet[l], sets info[l] LAPACK-style; b > 0 solves X L_kk^T = A_ik column by column
-// (right-looking substitution) and writes L_ik = X.
-__global__ __launch_bounds__(256) void p64_panel_kernel(double* __restrict__ A, int64_t lda, int64_t sa, int n, int k,
-                                                        double* __restrict__ logdet, int32_t* __restrict__ info) {
-  __shared__ double S[kPB * kPBL];
-  __shared__ double X[kPB * kPBL];
-  __shared__ double piv[kPB];
-  __shared__ int bad_s;
-  const int l = blockIdx.y, b = blockIdx.x, tid = threadIdx.x;
-  double* Al = A + (int64_t)l * sa;
-  const int k0 = k * kPB, nbk = min(kPB, n - k0), i0 = (k + b) * kPB, nbi = min(kPB, n - i0);
-  if (tid == 0) bad_s = -1;
-  for (int e = tid; e < kPB * kPB; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    S[r * kPBL + c] = (r < nbk && c < nbk) ? (c <= r ? Al[(int64_t)(k0 + r) * lda + k0 + c] : 0.0) : (r == c ? 1.0 : 0.0);
-    if (b > 0) X[r * kPBL + c] = (r < nbi && c < nbk) ? Al[(int64_t)(i0 + r) * lda + k0 + c] : 0.0;
-  }
-  __syncthreads();
-  p64_chol_lds(S, piv, &bad_s);
-  if (b == 0) {
-    for (int e = tid; e < nbk * kPB; e += 256) {
-      const int r = e >> 6, c = e & 63;
-      if (c < nbk) Al[(int64_t)(k0 + r) * lda + k0 + c] = c <= r ? S[r * kPBL + c] : 0.0;
-    }
-    for (int r = 0; r < nbk; ++r)  // the strict upper part right of the diagonal block
-      for (int c = k0 + nbk + tid; c < n; c += 256) Al[(int64_t)(k0 + r) * lda + c] = 0.0;
-    if (tid < 64) {
-      double v = tid < nbk ? log(piv[tid]) : 0.0;
-      v = wave_sum(v);
-      if (tid == 0) {
-        logdet[l] += 2.0 * v;
-        if (bad_s >= 0 && bad_s < nbk && info[l] == 0) info[l] = k0 + bad_s + 1;
-      }
-    }
-    return;
-  }
-  for (int c = 0; c < kPB; ++c) {
-    const double ip = 1.0 / S[c * kPBL + c];
-    if (tid < kPB) X[tid * kPBL + c] *= ip;
-    __syncthreads();
-    const int m = kPB - c - 1;
-    for (int e = tid; e < kPB * m; e += 256) {
-      const int r = e / m, cc = c + 1 + e % m;
-      X[r * kPBL + cc] -= X[r * kPBL + c] * S[cc * kPBL + c];
-    }
-    __syncthreads();
-  }
-  for (int e = tid; e < nbi * kPB; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    if (c < nbk) Al[(int64_t)(i0 + r) * lda + k0 + c] = X[r * kPBL + c];
-  }
-}
-
 // 64 x 64 x 64 product on the f64 MFMA: wave w owns rows 16 w .. 16 w + 15 of the tile, acc[cb] its 16 x 16
 // block of columns 16 cb ..; A operand As[row][kk], B operand Bs[kk][col] (v_mfma_f64_16x16x4f64, lane
 // (li = lane & 15, lk = lane >> 4): A[li][lk], B[lk][li]; acc[cb][r] = C[lk + 4 r][li])
@@ -127,6 +46,68 @@ __device__ inline void p64_mma(const double* __restrict__ As, const double* __re
     for (int cb = 0; cb < 4; ++cb)
       acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Bs[(kk + lk) * kPBL + 16 * cb + li], acc[cb], 0, 0, 0);
   }
+}
+
+// pass k, the diagonal block (one 256-thread workgroup per matrix): L_kk and Y_kk = L_kk^-1 by the 16-block
+// Cholesky in f64 MFMA accumulators (blkinv.hpp, MODE 1: no thread-serial pivots, the 16 x 16 pivots in
+// registers).  L_kk goes to A's lower part, Y_kk's strict lower part transposed into A_kk's strict upper part
+// (the panel launch's operand, zeroed by the next pass's diagonal launch; the last block writes no Y).  Also
+// zeroes the strict upper part right of the block, adds 2 sum log L_jj to logdet[l] and sets info[l]
+// LAPACK-style.  Only this launch writes A_kk: the panel launch after it reads it (the former
+// fused diagonal + panel launch had one workgroup overwrite A_kk while others of the same launch still read it).
+__global__ __launch_bounds__(256) void p64_diag_kernel(double* __restrict__ A, int64_t lda, int64_t sa, int n, int k,
+                                                       double* __restrict__ logdet, int32_t* __restrict__ info) {
+  const int l = blockIdx.x, tid = threadIdx.x, nt = (n + kPB - 1) / kPB;
+  double* Al = A + (int64_t)l * sa;
+  const int k0 = k * kPB, nbk = min(kPB, n - k0);
+  if (k > 0) {  // the previous diagonal block's Y^T (its panel launch is done)
+    const int p0 = k0 - kPB;
+    for (int e = tid; e < kPB * kPB; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      if (c > r) Al[(int64_t)(p0 + r) * lda + p0 + c] = 0.0;
+    }
+  }
+  for (int r = 0; r < nbk; ++r)  // the strict upper part right of the diagonal block
+    for (int c = k0 + nbk + tid; c < n; c += 256) Al[(int64_t)(k0 + r) * lda + c] = 0.0;
+  double* D = Al + (int64_t)k0 * lda + k0;
+  const bool last = k + 1 == nt;
+  if (last) {  // no panel reads Y: the strict upper part of the block is zero
+    for (int e = tid; e < nbk * nbk; e += 256) {
+      const int r = e / nbk, c = e % nbk;
+      if (c > r) D[(int64_t)r * lda + c] = 0.0;
+    }
+    __syncthreads();
+  }
+  blk_inverse<double, 4, 4, 1>(nbk, D, lda, last ? nullptr : D, lda, logdet + l, 1, info + l, k0, D, lda);
+}
+
+// pass k, the panel: L_ik = A_ik Y_kk^T for the block rows i > k, one workgroup per (block, matrix) on the f64
+// MFMA; Y_kk^T's strict upper part from A_kk's strict upper triangle, its diagonal 1 / L_jj
+__global__ __launch_bounds__(256) void p64_panel_kernel(double* __restrict__ A, int64_t lda, int64_t sa, int n, int k) {
+  __shared__ double As[kPB * kPBL];  // A_ik [row][kk]
+  __shared__ double Bs[kPB * kPBL];  // Y_kk^T [kk][col]
+  const int l = blockIdx.y, tid = threadIdx.x;
+  double* Al = A + (int64_t)l * sa;
+  const int k0 = k * kPB, nbk = min(kPB, n - k0), i0 = (k + 1 + blockIdx.x) * kPB, nbi = min(kPB, n - i0);
+  for (int e = tid; e < kPB * kPB; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    As[r * kPBL + c] = (r < nbi && c < nbk) ? Al[(int64_t)(i0 + r) * lda + k0 + c] : 0.0;
+    const double y = Al[(int64_t)(k0 + min(r, nbk - 1)) * lda + k0 + min(c, nbk - 1)];
+    Bs[r * kPBL + c] = (r < nbk && c < nbk && c >= r) ? (c > r ? y : 1.0 / y) : 0.0;
+  }
+  __syncthreads();
+  bi_f64x4 acc[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = bi_f64x4{0.0, 0.0, 0.0, 0.0};
+  p64_mma(As, Bs, acc);
+  const int lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * w + lk + 4 * r, col = 16 * cb + li;
+      if (row < nbi && col < nbk) Al[(int64_t)(i0 + row) * lda + k0 + col] = acc[cb][r];
+    }
 }
 
 // trailing update of pass k: A_IJ -= L_Ik L_Jk^T for the lower tiles k < J <= I, one workgroup per tile
@@ -184,13 +165,16 @@ int potrf_f64(int n, int L, const double* A, int64_t lda, int64_t sa, double* Lo
   } else if (lda != ldo || sa != so) {
     return -7;
   }
-  (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
-  (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
+  (void)zero_async(logdet, sizeof(double) * L, st);
+  (void)zero_async(info, sizeof(int32_t) * L, st);
   const int nt = cdiv(n, kPB);
   for (int k = 0; k < nt; ++k) {
-    p64_panel_kernel<<<dim3(nt - k, L), 256, 0, st>>>(Lo, ldo, so, n, k, logdet, info);
+    p64_diag_kernel<<<L, 256, 0, st>>>(Lo, ldo, so, n, k, logdet, info);
     const int m = nt - k - 1;
-    if (m > 0) p64_update_kernel<<<dim3(m * (m + 1) / 2, L), 256, 0, st>>>(Lo, ldo, so, n, k);
+    if (m > 0) {
+      p64_panel_kernel<<<dim3(m, L), 256, 0, st>>>(Lo, ldo, so, n, k);
+      p64_update_kernel<<<dim3(m * (m + 1) / 2, L), 256, 0, st>>>(Lo, ldo, so, n, k);
+    }
   }
   LVAE_CHECK_LAUNCH();
   return 0;

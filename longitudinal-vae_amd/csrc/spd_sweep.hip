@@ -878,8 +878,8 @@ int spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Kinv, double* 
   const int nt = np_ / kSwB;
   const int ntl2 = (nt - 2) * (nt - 1) / 2, ntll = (nt - 1) * nt / 2;
   auto ok = [](hipError_t e) { return e == hipSuccess; };
-  (void)hipMemsetAsync(logdet, 0, sizeof(double) * L, st);
-  (void)hipMemsetAsync(info, 0, sizeof(int32_t) * L, st);
+  (void)zero_async(logdet, sizeof(double) * L, st);
+  (void)zero_async(info, sizeof(int32_t) * L, st);
   if (!ok(hipEventRecord(sd->fork, st)) || !ok(hipStreamWaitEvent(sd->s, sd->fork, 0))) return LVAE_ERR_LAUNCH;
   sw_pivot_kernel<<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0);
   const bool fuse = L <= kSwFuseMaxL;

@@ -651,8 +651,8 @@ int lvae_deconv2_sigmoid_bwd_f32(const float* g, const float* out, const float* 
   if (N < 0 || Cin <= 0 || Cin > 16 || Hi <= 0 || Wi <= 0) return -2;
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) {
-    (void)hipMemsetAsync(dw, 0, sizeof(float) * Cin * 16, st);
-    (void)hipMemsetAsync(db, 0, sizeof(float), st);
+    (void)zero_async(dw, sizeof(float) * Cin * 16, st);
+    (void)zero_async(db, sizeof(float), st);
     return 0;
   }
   const int nb = deconv2_blocks(N, Hi, Wi), m = Cin * 16 + 1;
@@ -708,8 +708,8 @@ int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* 
   if (lds > 64 * 1024) return -4;
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) {
-    (void)hipMemsetAsync(dw, 0, sizeof(float) * Q * 9, st);
-    (void)hipMemsetAsync(db, 0, sizeof(float) * C, st);
+    (void)zero_async(dw, sizeof(float) * Q * 9, st);
+    (void)zero_async(db, sizeof(float) * C, st);
     return 0;
   }
   const int per = wgrad_per(N), nb = (int)cdiv(N, per), m = Q * 9 + C;
@@ -769,7 +769,7 @@ int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8
   const int Ho = H / 2, Wo = W / 2;
   hipStream_t st = (hipStream_t)stream;
   if (N == 0) {
-    (void)hipMemsetAsync(db, 0, sizeof(float) * C, st);
+    (void)zero_async(db, sizeof(float) * C, st);
     return 0;
   }
   const int nb = (int)cdiv(N, kPoolBiasPer);

@@ -566,7 +566,7 @@ def natural_gradient_update_(m, H, grad_m, grad_H, natural_gradient_lr):
     from torch.autograd.graph import increment_version
     increment_version(m)
     increment_version(H)
-    _check_info(info, "natural-gradient update cholesky")  # (a failed dim kept its m, H: natgrad_commit_kernel)
+    _check_info(info, "natural-gradient update cholesky")  # (any failure: no dim was updated, natgrad_commit_kernel)
     return True
 
 

@@ -279,7 +279,9 @@ class GraphedStep:
         self.g2 = None
         if comm:
             self.g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g2, stream=self.stream):
+            import os
+            pool = self.g1.pool() if os.environ.get("DIAG_POOL") == "shared" else None
+            with torch.cuda.graph(self.g2, stream=self.stream, pool=pool):
                 step.apply()
         self.pending = take_pending()
         self.comm = comm

@@ -133,6 +133,25 @@ def test_linear_act_fused(hip, B, fin, fout, relu):
         assert e < 1e-4, (k, e)
 
 
+def test_linear_act_fused_nan(hip):
+    """A NaN pre-activation stays NaN through the fused bias + ReLU, and its gradient passes like
+    torch.relu / threshold_backward (fmaxf had mapped it to 0, hiding a diverging layer)."""
+    from lvae_amd.vae import linear_act
+    torch.manual_seed(0)
+    fc = torch.nn.Linear(8, 5).cuda()
+    x = torch.randn(3, 8, device="cuda")
+    x[1, 2] = float("nan")
+    x.requires_grad_()
+    y = linear_act(fc, x, True)
+    xr = x.detach().clone().requires_grad_()
+    yr = torch.relu(torch.nn.functional.linear(xr, fc.weight.detach(), fc.bias.detach()))
+    assert torch.equal(torch.isnan(y), torch.isnan(yr)) and bool(torch.isnan(y[1]).all())
+    g = torch.ones_like(y)
+    (y * g).sum().backward()
+    (yr * g).sum().backward()
+    assert torch.equal(torch.isnan(x.grad), torch.isnan(xr.grad))
+
+
 @pytest.mark.parametrize("N", [4096, 37])
 def test_deconv_relu_fused(hip, N):
     """The decoder's relu(ConvTranspose2d(32, 16, 4, 2, 1)) (VAE.py:73, 122): MIOpen's transposed conv without

@@ -59,6 +59,22 @@ def test_potrf_f64_vs_oracle(hip, n, L):
     assert torch.equal(torch.triu(Lg.cpu(), 1), torch.zeros_like(Lr))  # torch.cholesky's zero upper part
 
 
+def test_potrf_f64_many_workgroups(hip):
+    """n = 2048, L = 16: the first pass launches 31 x 16 panel workgroups, more than are resident at once
+    (the former fused diagonal + panel launch raced on A_kk exactly when its workgroups did not all
+    start together; the tests above all fit in one wave of workgroups)."""
+    import lvae_amd.linalg as LA
+    n, L = 2048, 16
+    g = torch.Generator().manual_seed(5)
+    B = torch.randn(L, n, n, generator=g, dtype=torch.float64)
+    A = B @ B.transpose(-1, -2) / n + torch.eye(n, dtype=torch.float64)
+    Lr, ldr = O.potrf(A)
+    Lg, ldg, info = LA.cholesky_ex(A.to(DEV))
+    assert int(info.abs().sum()) == 0
+    assert rel(Lg, Lr) < 1e-11
+    assert rel(ldg, ldr) < 1e-12
+
+
 def test_potrf_f64_in_place(hip):
     """Lout == A: the factor overwrites A's lower triangle (upper zeroed)."""
     n, L = 300, 2

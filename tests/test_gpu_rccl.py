@@ -142,6 +142,78 @@ def test_rccl_world1_graphed_hensman_two_graphs(hip):
         assert rel(p, q) < 1e-9, n
 
 
+@pytest.mark.parametrize("comm", [True, False])
+def test_rccl_world1_two_graphs_back_to_back(hip, comm):
+    """The bench's own pattern (bench.py run_hensman): 100 back-to-back replays of the data-parallel Hensman step
+    as two HIP graphs around the collectives (world-1 RCCL group; comm=False: the one-graph step), a single
+    deferred info check at the end, then (m, H), the kernel hyper-parameters and the last loss terms against the
+    eager step on the same batch sequence.  Round 5 left this path corrupt: a hipMemsetAsync captured into the
+    second graph did not zero the natural-gradient update's info words on replays after the first
+    (scripts/dp_replay_diag.py); the library now zeroes with kernel nodes only."""
+    from lvae_amd.distributed import GradAllReduce, allreduce_tensors
+    from lvae_amd.steps import GraphedStep, HensmanStep
+    from lvae_amd.vae import ConvVAE
+    la, img, mask, X, z, batches, eps = _hensman_setup()
+    L, M, T, P = 4, 40, 16, 32
+    n_steps = 100
+
+    def make(hooks):
+        torch.manual_seed(3)
+        vae = ConvVAE(L, 1296, p_input=0.0, p=0.0).to(DEV)
+        k0, k1 = la.generate_kernel_batched(L, **CFG, id_covariate=2)
+        k0, k1 = k0.to(DEV), k1.to(DEV)
+        lik = la.GaussianLikelihood(L, noise=1.0, constrain=False).to(DEV)
+        with torch.no_grad():
+            H = k0(z, z).evaluate() + 1e-6 * torch.eye(M, dtype=torch.float64, device=DEV)
+        m = torch.zeros(L, M, 1, dtype=torch.float64, device=DEV)
+        params = list(k0.parameters()) + list(k1.parameters()) + list(vae.parameters())
+        opt = torch.optim.Adam(params, lr=1e-3, capturable=True, fused=True)
+        kw = {}
+        if hooks:
+            kw = dict(world=1, grad_hook=GradAllReduce(params, 1),
+                      ng_reduce=lambda ts: allreduce_tensors(ts, average=False))
+        return HensmanStep(vae, k0, k1, lik, opt, m, H, z, P, T, **kw), k0
+
+    la.set_sync_checks(False)
+    try:
+        eager, k0_e = make(False)
+        eager(img[batches[0]], mask[batches[0]], X[batches[0]], eps)  # = the graph's warm-up step
+        for i in range(n_steps):
+            b = batches[i % len(batches)]
+            out_e = [float(v) for v in eager(img[b], mask[b], X[b], eps)]
+        torch.cuda.synchronize()
+        ctx = _NcclWorld1() if comm else None
+        if ctx is not None:
+            ctx.__enter__()
+        try:
+            graph_step, k0_g = make(comm)
+            s = (img[batches[0]].clone(), mask[batches[0]].clone(), X[batches[0]].clone(), eps)
+            g = GraphedStep(graph_step, s, warmup=1)
+            assert (g.g2 is not None) == comm
+            for i in range(n_steps):
+                b = batches[i % len(batches)]
+                torch.index_select(img, 0, b, out=s[0])
+                torch.index_select(mask, 0, b, out=s[1])
+                torch.index_select(X, 0, b, out=s[2])
+                out = g()
+            torch.cuda.synchronize()
+            g.check()
+            out_g = [float(v) for v in out]
+        finally:
+            if ctx is not None:
+                ctx.__exit__(None, None, None)
+    finally:
+        la.set_sync_checks(True)
+    print("last step eager", out_e, "graphed", out_g)
+    print("m", rel(graph_step.m, eager.m), "H", rel(graph_step.H, eager.H))
+    # 100 natural-gradient + Adam steps carry the fp32 ConvVAE backward's run-to-run rounding (MIOpen
+    # reductions, ~1e-7) into the state: m at ~1e-5 of its size, the loss terms at ~1e-5
+    assert np.allclose(out_e, out_g, rtol=1e-4), (out_e, out_g)
+    assert rel(graph_step.m, eager.m) < 1e-4 and rel(graph_step.H, eager.H) < 1e-5
+    for (n, p), (_, q) in zip(k0_g.named_parameters(), k0_e.named_parameters()):
+        assert rel(p, q) < 1e-6, n
+
+
 def test_graphed_closed_step_matches_eager(hip):
     """ClosedStep (the bench's exact-KL step: the factorisation on the caller's stream with the inverse's
     own side stream, the ConvVAE on a second stream joined by events) captured as ONE HIP graph and
