@@ -256,9 +256,10 @@ class GraphedStep:
     step is one graph; with a ``grad_hook`` / ``ng_reduce`` (data parallel) the step is two graphs
     around the eager collectives.  The optimiser must be capturable (torch.optim.Adam(...,
     capturable=True)); numerical-failure checks are deferred (set_sync_checks(False)) and
-    ``check()`` reads the captured info arrays, which every replay rewrites."""
+    ``check()`` reads the captured info arrays, which every replay rewrites.  shared_pool: capture the
+    second graph into the first one's memory pool (diagnostics, scripts/dp_replay_diag.py)."""
 
-    def __init__(self, step, inputs, warmup=3):
+    def __init__(self, step, inputs, warmup=3, shared_pool=False):
         self.step, self.inputs = step, inputs
         if getattr(step, "gvae", None) is not None:
             step.gvae = None  # (the whole step is one graph here: no graphed ConvVAE parts inside the capture)
@@ -279,9 +280,7 @@ class GraphedStep:
         self.g2 = None
         if comm:
             self.g2 = torch.cuda.CUDAGraph()
-            import os
-            pool = self.g1.pool() if os.environ.get("DIAG_POOL") == "shared" else None
-            with torch.cuda.graph(self.g2, stream=self.stream, pool=pool):
+            with torch.cuda.graph(self.g2, stream=self.stream, pool=self.g1.pool() if shared_pool else None):
                 step.apply()
         self.pending = take_pending()
         self.comm = comm

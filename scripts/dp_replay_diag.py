@@ -99,7 +99,7 @@ def main():
     hist = os.environ.get("DIAG_HIST") == "1"
     if hist:
         torch.cuda.memory._record_memory_history(max_entries=200000)
-    g = GraphedStep(step, (s_img, s_mask, s_X, eps), warmup=3)
+    g = GraphedStep(step, (s_img, s_mask, s_X, eps), warmup=3, shared_pool=os.environ.get("DIAG_POOL") == "shared")
     torch.cuda.empty_cache = real_empty
     print(f"comm={comm} pool={os.environ.get('DIAG_POOL', 'own')} L={L} M={M} two graphs: {g.g2 is not None}",
           flush=True)
