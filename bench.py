@@ -9,9 +9,12 @@ refinement of K^-1 mu, S GEMM, Gram adjoint) + Adam.
   sharded over the ranks and the images split over them (lvae_amd.distributed.
   LatentShardedClosedStep): strong scaling, value = whole-job ELBO-steps/s.
 
-Sub-record `regime_a` (BASELINE configs[3], the path config/LVAE_config_sample.txt selects): the
-Hensman SVI step (training.py:90-140) at L = 16, M = 120, P_b = 5 subjects x T = 16 per rank, data
-parallel over subject mini-batches for N > 1 (weak scaling), replayed as HIP graphs.
+Sub-record `regime_a` (BASELINE configs[3], the path config/LVAE_config_sample.txt selects), at every N:
+the Hensman SVI step (training.py:90-140) at L = 16, M = 120, P_b = 5 subjects x T = 16 per rank, data
+parallel over subject mini-batches for N > 1 (weak scaling: value = whole-job ELBO-steps/s, samples_per_sec
+= all ranks' images/s), replayed as HIP graphs -- one per step at N = 1, two around the RCCL all-reduces of
+the Adam gradients and the natural-gradient statistics at N > 1.  At N = 1 its `dp_world1_rccl` sub-record
+times that two-graph form through a world-1 RCCL group.
 
 Sub-record `c2` (BASELINE configs[1], N = 1 only): HIP Gram + blocked Cholesky inverse + log-det (the
 product route, lvae_spd_inv_chol_f32) vs PyTorch-ROCm Gram + torch.linalg.cholesky (+ cholesky_inverse)
@@ -773,8 +776,9 @@ def main():
     ap.add_argument("--P_b", type=int, default=5, help="Regime A: subjects per batch per rank")
     ap.add_argument("--M", type=int, default=120, help="Regime A: inducing points")
     ap.add_argument("--h-steps", dest="h_steps", type=int, default=100, help="Regime A timed steps")
-    # default: both regimes on one GPU; the exact-KL line alone at N > 1 (Regime A's data-parallel two-graph replay
-    # through RCCL is opt-in there: DESIGN.md section 5)
+    # default: both regimes at every N -- the exact-KL line (latent dims sharded over the ranks at N > 1) and its
+    # `regime_a` sub-record (BASELINE configs[3]: the Hensman step data parallel over subject mini-batches, two HIP
+    # graphs around the RCCL all-reduces at N > 1)
     ap.add_argument("--regime", choices=["auto", "both", "closed", "hensman"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-phase-timing", action="store_true")
@@ -787,9 +791,9 @@ def main():
     ap.add_argument("--rank-share", dest="rank_share", type=int, default=0,
                     help="one GPU: time rank 0's share of a W-rank latent-sharded step (L/W dims, N/W images; "
                          "collectives replaced by local stand-ins) -- the per-rank compute of the W-GPU line")
-    ap.add_argument("--dp-world1", dest="dp_world1", action="store_true",
-                    help="one GPU: also time Regime A's data-parallel step (two graphs around the all-reduces) "
-                         "through a world-1 RCCL group (opt-in: see DESIGN.md section 5 on this path)")
+    ap.add_argument("--no-dp-world1", dest="dp_world1", action="store_false",
+                    help="one GPU: skip timing Regime A's data-parallel step (two graphs around the all-reduces) "
+                         "through a world-1 RCCL group (the regime_a.dp_world1_rccl sub-record)")
     ap.add_argument("--vae-stream-priority", dest="vae_stream_priority", type=int, default=-1,
                     help="priority of the ConvVAE's stream in the closed step (lower = higher; 0 = default)")
     args = ap.parse_args()
@@ -797,7 +801,7 @@ def main():
     world, rank, local = setup_dist(force_group=args.sharded_world1)
     dev = torch.device("cuda", local)
     if args.regime == "auto":
-        args.regime = "both" if world == 1 else "closed"
+        args.regime = "both"
     res = None
     if args.regime in ("both", "closed"):
         res = run_closed(args, world, rank, dev)
