@@ -18,6 +18,7 @@ _CONV_DGRAD = os.environ.get("LVAE_CONV_DGRAD", "1") != "0"
 # LVAE_CONV_BWD_FORK=0: that layer's weight-gradient and input-gradient kernels one after the other on the
 # backward's stream instead of side by side (the weight gradient on a side stream, joined before returning)
 _CONV_BWD_FORK = os.environ.get("LVAE_CONV_BWD_FORK", "1") != "0"
+_FORK_UNDER_CAPTURE = os.environ.get("LVAE_FORK_UNDER_CAPTURE", "0") == "1"
 _SIDE_STREAMS = {}
 
 
@@ -109,10 +110,12 @@ class _ConvReluMaxPool2(torch.autograd.Function):
             dgrad = (ctx.needs_input_grad[0] and _CONV_DGRAD and Cin == 16 and H * W <= 1024
                      and lib.lvae_conv3x3_pool_dgrad_lds(C, H, W) <= 65536)
             cur = torch.cuda.current_stream(gy.device)
-            # (eager only: a fork inside a HIP graph capture crashed the capture's end -- test_gpu_rccl's
-            # test_graphed_closed_step_matches_eager; captured steps keep the one-stream order)
-            side = (_side_stream(gy.device) if dgrad and _CONV_BWD_FORK and not torch.cuda.is_current_stream_capturing()
-                    else None)
+            # (eager only: with this fork inside a HIP graph capture the process segfaults in torch.cuda.graph's
+            # capture_end, i.e. in the runtime's hipStreamEndCapture / graph instantiation -- still after r6's
+            # memset fix, so not the memset nodes (profiles/r6_fork_under_capture_segv.log,
+            # LVAE_FORK_UNDER_CAPTURE=1); captured steps keep the one-stream order)
+            side = (_side_stream(gy.device) if dgrad and _CONV_BWD_FORK and (
+                _FORK_UNDER_CAPTURE or not torch.cuda.is_current_stream_capturing()) else None)
             if side is not None:  # (the weight gradient beside the input gradient; joined below)
                 side.wait_stream(cur)
             with torch.cuda.stream(side if side is not None else cur):
