@@ -960,6 +960,7 @@ struct CiGemmArgs {
   int pre = 0;  // kCiLauum(KL): K^-1's lower tiles are in Kinv already (pipelined lauum): epilogue only
   const int* hbon = nullptr;  // kCiLauumKL: *hbon != 0 -> the binned hyper-gradient (kl_hyper.hip) runs: the full
                               // symmetric K^-1 (the mirror) instead of the S GEMM's B planes
+  const int* dimflag = nullptr;  // kCiLauum: only the dims l with dimflag[l] != 0 (the others' workgroups exit)
 };
 
 // one halving butterfly step over lane bit D (D <= 16): the lane keeps the half of its N partial sums
@@ -1072,6 +1073,7 @@ __device__ inline void ci_gemm_body(const CiGemmArgs& g, const CiScratch& S, con
     const int orig = bid, xcd = orig % 8, q8 = g.nwg / 8, r8 = g.nwg % 8;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
     l = wgid / g.per_dim;
+    if (g.dimflag && !g.dimflag[l]) return;  // (uniform, before any barrier)
     sx_tri_blocked(wgid % g.per_dim, nt, i, j);
     kb0 = i;
     kb1 = nt;
@@ -1683,6 +1685,25 @@ int ci_lauum_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv,
   LVAE_CHECK_LAUNCH();
   return 0;
 }
+
+// lauum for the dims with flag[l] != 0 only (device flags: the exact KL's early reduce refines diag K^-1 in fp64
+// for those dims before the full lauum runs in the backward, kl_closed.hip); K^-1 tiles + mirror into Kinv
+int ci_lauum_flagged_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const int* flag, hipStream_t st) {
+  if (np_ <= 0 || np_ % kSwB || np_ / kSwB > 64) return -1;
+  CiScratch S((char*)scratch, np_, L);
+  const int nt = S.nt, per = nt * (nt + 1) / 2, nwg = per * L;
+  const int64_t full = (int64_t)L * np_ * np_;
+  CiGemmArgs gl{YT, YT + full, YT, YT + full, nullptr, nullptr, nullptr, nullptr, Kinv, np_, nt, 0, per, nwg, 0};
+  gl.dimflag = flag;
+  ci_gemm_kernel<kCiLauum><<<nwg, 512, 0, st>>>(gl, S);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+int ci_pipe_mode_of(int np_, int L) { return ci_pipe_mode(np_, L); }
+
+// the per-tile split scales of Y (ysc(l, i, j), both plane orientations) in the factor's scratch
+const float* ci_ysc_ptr(void* scratch, int np_, int L) { return CiScratch((char*)scratch, np_, L).ysc; }
 
 // potrf alone (lvae_potrf_f32): A [L, np, np] -> L in A's lower tiles (fp32; zero strict upper part of the
 // diagonal tiles; the other upper tiles untouched), log|A|, info

@@ -8,7 +8,13 @@
 //                                                   chol_inv.hip)
 //   the binned residual's plan                     (kl_resid_bins_plan, on the side stream behind the
 //                                                   pivot chain; integer-coded covariates only)
-// reduce (needs mu, log v):
+// reduce (needs mu, log v), early form (the default for L > 2 dims per call, kl_early):
+//   a0 = Y^T (Y mu), d = diag K^-1                 (kl_ymv_kernel: triangular mat-vecs over the Y / Y^T planes,
+//                                                   d = the row sums of squares of Y^T; no K^-1)
+//   r = mu - K a0, a = a0 + Y^T (Y r)              (fp64 residual as below, then two more mat-vecs)
+//   the refinement gate on d; the flagged dims' K^-1 alone + their fp64 diag; kl_l
+//   -> lauum (K^-1 = Y^T Y, B planes) runs in the backward's hyper-parameter half, after d kl / d (mu, log v)
+// reduce, K^-1 form (pipelined factors, L <= 2: K^-1 is accumulated in the factor; LVAE_KL_EARLY=0):
 //   K^-1 = Y^T Y, the partials of a0 = K^-1 mu,    (ci_lauum_f32 with the KL epilogue: one pass over the
 //   and B = K^-1 diag(sqrt v) as fp16 hi / lo       K^-1 tiles while they are in registers; B only when a
 //   planes, one power-of-two scale per dim          backward follows)
@@ -27,6 +33,7 @@
 #include "common.hpp"
 #include "side_stream.hpp"
 #include "prof.hpp"
+#include "x3_c16.hpp"  // c16_off: the chunk-major Y / Y^T planes
 
 
 #ifndef LVAE_ALPHA_WG
@@ -64,6 +71,14 @@ bool kl_resid_bins_enabled(const lvae_kernel_spec* spec, int n);
 int kl_resid_bins_plan(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, void* wsbuf,
                        hipStream_t st);
 size_t kl_refine_bytes(int np_, int L);
+int kl_refine_gate(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, const double* params,
+                   const double* noise, const double* kdiag, double* est, int* flag, hipStream_t st);
+int kl_refine_apply(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, const double* params,
+                    const double* noise, const float* Kinv, double* kdiag, double* K64, double* part, const int* flag,
+                    hipStream_t st);
+int ci_lauum_flagged_f32(int np_, int L, void* scratch, const _Float16* YT, float* Kinv, const int* flag, hipStream_t st);
+const float* ci_ysc_ptr(void* scratch, int np_, int L);
+int ci_pipe_mode_of(int np_, int L);
 size_t kl_refine_part_bytes(int np_, int L);
 int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
                    const double* params, const double* noise, const float* Kinv, double* kdiag, double* K64,
@@ -86,6 +101,9 @@ struct KLWorkspace {
   const int* hbon;   // its device flag: on -> the lauum writes K^-1's mirror, the S GEMM and the table adjoint exit
   double* rest;      // [L] the refinement gate's estimate (sum_r s_r + noise) max (K^-1)_ii
   int* rflag;        // [L] 1: diag K^-1 refined
+  double* ypart;     // early reduce: [2][L][nt][np] fp64 partials of the triangular mat-vecs over the Y planes
+  double* yvec;      // early reduce: [L][np] t = Y mu, then u = Y r
+  double* K64e;      // early reduce: the refinement's fp64 K (the Y^T planes are still needed by the late lauum)
   size_t bytes;
   KLWorkspace(char* base, int np_, int L) {
     size_t off = 0;
@@ -120,6 +138,9 @@ struct KLWorkspace {
     hbon = base ? reinterpret_cast<const int*>(kl_hyper_dev(hb, np_, L)) : nullptr;  // (HbDev::on: its first member)
     rest = (double*)take((size_t)L * sizeof(double));
     rflag = (int*)take((size_t)L * sizeof(int));
+    ypart = (double*)take(2 * (size_t)L * (np_ / 256) * np_ * sizeof(double));
+    yvec = (double*)take((size_t)L * np_ * sizeof(double));
+    K64e = (double*)take(kl_refine_bytes(np_, L));
     bytes = off;
   }
 };
@@ -256,6 +277,73 @@ __global__ __launch_bounds__(256) void kl_alpha_reduce(const double* __restrict_
   alpha[o] = base[o] + acc;
 }
 
+// ---- the early reduce: K^-1 mu and diag K^-1 from Y = L^-1 before lauum (K^-1 = Y^T Y) ----------------------------
+// y = P x over one triangle of 256-tiles of a chunk-major plane pair (hi, lo; x3_c16.hpp): the Y planes' lower
+// tiles (R, C), C <= R (UPPER false: y = Y x), or the Y^T planes' upper tiles (R, C), C >= R (y = Y^T x); the
+// value of an entry is (hi + lo) / ysc(max(R, C), min(R, C)).  One 256-thread workgroup per (tile, dim), a thread
+// per row of the tile: every 16-deep chunk is one contiguous 8 KB run (256 rows x 32 B per plane), each row's
+// 16 halves un-swizzled (the two 8-half groups swapped when bit 3 of the row is set).  fp64 accumulation; the
+// tile's row sums go to part[l][C][row] (SUMSQ: the row sums of squares to part2 -- diag K^-1 = the row sums
+// of squares of Y^T), summed in a fixed order by kl_ymv_reduce.  HBM-bound: 4 B per element read once.
+template <bool UPPER, bool SUMSQ>
+__global__ __launch_bounds__(256) void kl_ymv_kernel(const _Float16* __restrict__ hi, const _Float16* __restrict__ lo,
+                                                     const float* __restrict__ ysc, int np_, const double* __restrict__ x,
+                                                     double* __restrict__ part, double* __restrict__ part2) {
+  __shared__ double xs[256];
+  const int l = blockIdx.y, tid = threadIdx.x, nt = np_ / 256;
+  int R, C;
+  alpha_tri_index(blockIdx.x, R, C);  // (R >= C)
+  if (UPPER) {
+    const int t = R;
+    R = C;
+    C = t;
+  }
+  xs[tid] = x[(int64_t)l * np_ + C * 256 + tid];
+  const float s = ysc[((int64_t)l * nt + max(R, C)) * nt + min(R, C)];
+  __syncthreads();
+  const int row = R * 256 + tid;
+  const bool sw = (tid >> 3) & 1;  // this row's two 8-half groups are stored swapped
+  // chunk 0 of column block C, this row (c16_off's layout without the swizzle: the row's 16 halves whole)
+  const int64_t base = (int64_t)l * np_ * np_ + ((int64_t)R * (np_ >> 4) + C * 16) * kC16Part + tid * 16;
+  const uint4* ph = reinterpret_cast<const uint4*>(hi + base);
+  const uint4* pl = reinterpret_cast<const uint4*>(lo + base);
+  constexpr int kChunkU4 = kC16Part / 8;  // uint4 per chunk (8 halves each)
+  double acc = 0.0, sq = 0.0;
+#pragma unroll 4
+  for (int c = 0; c < 16; ++c) {
+    const uint4 h0 = ph[c * kChunkU4], h1 = ph[c * kChunkU4 + 1];
+    const uint4 l0 = pl[c * kChunkU4], l1 = pl[c * kChunkU4 + 1];
+    // un-swizzle by whole 8-half groups (selects, no runtime-indexed register arrays: those go to scratch)
+    _Float16 hv[16], lv[16];
+    *reinterpret_cast<uint4*>(hv) = sw ? h1 : h0;
+    *reinterpret_cast<uint4*>(hv + 8) = sw ? h0 : h1;
+    *reinterpret_cast<uint4*>(lv) = sw ? l1 : l0;
+    *reinterpret_cast<uint4*>(lv + 8) = sw ? l0 : l1;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const double v = (double)((float)hv[kk] + (float)lv[kk]);
+      acc += v * xs[c * 16 + kk];
+      if (SUMSQ) sq += v * v;
+    }
+  }
+  const double inv = 1.0 / (double)s;
+  part[((int64_t)l * nt + C) * np_ + row] = acc * inv;
+  if (SUMSQ) part2[((int64_t)l * nt + C) * np_ + row] = sq * inv * inv;
+}
+
+// out[l][i] = (base ? base[l][i] : 0) + sum over the triangle's column blocks C of part[l][C][i] (fixed order: C
+// ascending); lower: C = 0 .. R, upper: C = R .. nt - 1 (R = i's row block).  Grid (np / 256, L).
+template <bool UPPER>
+__global__ __launch_bounds__(256) void kl_ymv_reduce(const double* __restrict__ part, const double* base, int np_,
+                                                     double* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x, l = blockIdx.y, nt = np_ / 256, R = blockIdx.x;
+  const double* p = part + (int64_t)l * nt * np_ + i;
+  double acc = 0.0;
+  for (int C = UPPER ? R : 0; C <= (UPPER ? nt - 1 : R); ++C) acc += p[(int64_t)C * np_];
+  const int64_t o = (int64_t)l * np_ + i;
+  out[o] = (base ? base[o] : 0.0) + acc;
+}
+
 __global__ __launch_bounds__(256) void kl_finalize_kernel(const double* __restrict__ muc, const double* __restrict__ logv,
                                                           int ld, const double* __restrict__ alpha,
                                                           const double* __restrict__ kdiag,
@@ -358,6 +446,41 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
   return 0;
 }
 
+// The early reduce (opt-in, LVAE_KL_EARLY=1; non-pipelined factors only, L > 2 dims per call): K^-1 mu and
+// diag K^-1 straight from Y = L^-1 while the Y and Y^T planes are fresh, before any lauum, so that d kl / d (mu,
+// log v) -- and the encoder's backward -- need no K^-1; lauum moves into the backward's hyper-parameter half.
+// Measured (r6, same box, headline step): d kl / d (mu, log v) 0.7 ms earlier, but the step 9.32-9.37 vs 9.20-9.25
+// ms: the encoder backward then runs beside lauum + the slab pass, whose grids hold every CU, and the four
+// mat-vec passes (~0.45 ms) add to a step that is bound by its total GPU work (profiles/r6_kl_early_ab.txt).
+// Read per call (tests compare both routes in one process); the forward and the backward of one KL must see the
+// same value.
+static bool kl_early(int np_, int L) {
+  const char* e = getenv("LVAE_KL_EARLY");
+  return e && atoi(e) != 0 && ci_pipe_mode_of(np_, L) == 0;
+}
+
+// t = Y x (lower) or a = base + Y^T x (upper, + the row sums of squares of Y^T: diag K^-1 into sumsq)
+static void kl_ymv(const KLWorkspace& ws, const float* ysc, int np_, int L, bool upper, const double* x,
+                   const double* base, double* out, double* sumsq, hipStream_t st) {
+  const int nt = np_ / 256, ntri = nt * (nt + 1) / 2;
+  const int64_t full = (int64_t)L * np_ * np_;
+  double* p2 = ws.ypart + (int64_t)L * nt * np_;
+  if (!upper) {
+    const _Float16* yh = reinterpret_cast<const _Float16*>(ws.A);  // the Y planes (A is dead after potrf)
+    kl_ymv_kernel<false, false><<<dim3(ntri, L), 256, 0, st>>>(yh, yh + full, ysc, np_, x, ws.ypart, nullptr);
+    kl_ymv_reduce<false><<<dim3(nt, L), 256, 0, st>>>(ws.ypart, base, np_, out);
+  } else {
+    const _Float16* th = ws.planes;  // the Y^T planes
+    if (sumsq) {
+      kl_ymv_kernel<true, true><<<dim3(ntri, L), 256, 0, st>>>(th, th + full, ysc, np_, x, ws.ypart, p2);
+      kl_ymv_reduce<true><<<dim3(nt, L), 256, 0, st>>>(p2, nullptr, np_, sumsq);
+    } else {
+      kl_ymv_kernel<true, false><<<dim3(ntri, L), 256, 0, st>>>(th, th + full, ysc, np_, x, ws.ypart, nullptr);
+    }
+    kl_ymv_reduce<true><<<dim3(nt, L), 256, 0, st>>>(ws.ypart, base, np_, out);
+  }
+}
+
 int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
                               const double* params, const double* noise, const double* mu, const double* logv,
                               int ld_mu, double* kl, void* workspace, int need_bwd, void* stream) {
@@ -375,12 +498,31 @@ int lvae_kl_closed_reduce_f32(const lvae_kernel_spec* spec, const double* x, int
   KLWorkspace ws((char*)workspace, np_, L);
   ProfScope ps(LVAE_PH_KL_REDUCE, st);
   kl_prep_kernel<<<dim3(cdiv(np_, 256), L), 256, 0, st>>>(mu, logv, ld_mu, n, np_, L, ws.mu, ws.v, ws.sv);
+  const bool rb_on = kl_resid_bins_enabled(spec, n);  // (the plan: the factor call's, joined on `st`)
+  if (kl_early(np_, L)) {
+    // a0 = Y^T (Y mu) and d = diag K^-1 (the row sums of squares of Y^T); r = mu - K a0 in fp64 from the
+    // covariates; a = a0 + Y^T (Y r); the refinement gate on d, and for the flagged dims (if any) their K^-1 alone
+    // (the other dims' lauum workgroups exit) and the fp64 diag refinement; the KL.  No K^-1 for unflagged dims.
+    const float* ysc = ci_ysc_ptr(ws.chol, np_, L);
+    kl_ymv(ws, ysc, np_, L, false, ws.mu, nullptr, ws.yvec, nullptr, st);
+    kl_ymv(ws, ysc, np_, L, true, ws.yvec, nullptr, ws.alpha, ws.kdiag, st);
+    LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res,
+                           rb_on ? ws.rb : nullptr, st));
+    kl_ymv(ws, ysc, np_, L, false, ws.res, nullptr, ws.yvec, nullptr, st);
+    kl_ymv(ws, ysc, np_, L, true, ws.yvec, ws.alpha, ws.alpha, nullptr, st);
+    LVAE_TRY(kl_refine_gate(spec, x, ldx, n, np_, L, params, noise, ws.kdiag, ws.rest, ws.rflag, st));
+    LVAE_TRY(ci_lauum_flagged_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.rflag, st));
+    LVAE_TRY(kl_refine_apply(spec, x, ldx, n, np_, L, params, noise, ws.Kinv, ws.kdiag, ws.K64e, ws.rpart, ws.rflag,
+                             st));
+    kl_finalize_kernel<<<L, 256, 0, st>>>(ws.mu, logv, ld_mu, ws.alpha, ws.kdiag, ws.logdet, n, np_, kl);
+    LVAE_CHECK_LAUNCH();
+    return 0;
+  }
   // K^-1 (+ the partials of a0 = K^-1 mu, + the B planes); a0, d; r = mu - K a0 in fp64 from the
   // covariates; a = a0 + K^-1 r
   LVAE_TRY(ci_lauum_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.mu, ws.sv, ws.apart, need_bwd ? ws.Bp : nullptr,
                         ws.bsc, st, ws.hbon));
   kl_alpha0_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(ws.apart, ws.Kinv, np_, ws.alpha, ws.kdiag);
-  const bool rb_on = kl_resid_bins_enabled(spec, n);  // (the plan: the factor call's, joined on `st`)
   LVAE_TRY(kl_gram_resid(spec, x, ldx, n, np_, L, params, noise, ws.alpha, ws.mu, ws.rpart, ws.res,
                          rb_on ? ws.rb : nullptr, st));
   {  // alpha = a0 + K^-1 r over the lower tiles of K^-1 (the residual's partials buffer is free again)
@@ -424,6 +566,12 @@ int lvae_kl_closed_bwd_hyper_f32(const lvae_kernel_spec* spec, const double* x, 
   hipStream_t st = (hipStream_t)stream;
   const int np_ = lvae_kl_closed_padded_n(n);
   KLWorkspace ws((char*)workspace, np_, L);
+  if (kl_early(np_, L)) {
+    // the early reduce left K^-1 to this half: lauum now (+ the B planes for the S GEMM when the binned route is off;
+    // the a0 partials it also writes are unused), beside the encoder's backward on the caller's other stream
+    ProfScope ps(LVAE_PH_KL_REDUCE, st);
+    LVAE_TRY(ci_lauum_f32(np_, L, ws.chol, ws.planes, ws.Kinv, ws.mu, ws.sv, ws.apart, ws.Bp, ws.bsc, st, ws.hbon));
+  }
   // S = K^-1 V K^-1 = B B^T into the (no longer needed) Y^T plane buffer, from the fp16 hi / lo planes
   // of B = K^-1 diag(sqrt v) the forward wrote (need_bwd; np is a multiple of 256: lvae_kl_closed_padded_n)
   float* S = reinterpret_cast<float*>(ws.planes);

@@ -295,9 +295,9 @@ size_t kl_refine_bytes(int np_, int L) { return (size_t)kl_refine_cap(L) * np_ *
 
 size_t kl_refine_part_bytes(int np_, int L) { return (size_t)L * (np_ / kRgT) * np_ * sizeof(double); }
 
-int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
-                   const double* params, const double* noise, const float* Kinv, double* kdiag, double* K64,
-                   double* part, double* est, int* flag, hipStream_t st) {
+// the gate alone: est, flag from kdiag (mode 0: both zero)
+int kl_refine_gate(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, const double* params,
+                   const double* noise, const double* kdiag, double* est, int* flag, hipStream_t st) {
   const int mode = refine_mode();
   if (mode == 0) {  // off: only the state lvae_kl_closed_refine_state reports
     if (zero_async(est, (size_t)L * sizeof(double), st) != 0 ||
@@ -305,13 +305,24 @@ int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n
       return LVAE_ERR_LAUNCH;
     return 0;
   }
+  if (!spec_bucket(spec) || L > kRfMaxL) return -1;
+  kl_refine_gate_kernel<<<L, 256, 0, st>>>(to_dev(spec), x, ldx, params, noise, kdiag, n, np_, mode, refine_tau(), est,
+                                           flag);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// the refinement of the flagged dims' diag K^-1 (kdiag) from the fp32 K^-1 in Kinv (the gate ran before)
+int kl_refine_apply(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L, const double* params,
+                    const double* noise, const float* Kinv, double* kdiag, double* K64, double* part, const int* flag,
+                    hipStream_t st) {
+  if (refine_mode() == 0) return 0;
   const int bucket = spec_bucket(spec);
   int qs = 0;
   for (int r = 0; r < spec->n_comp; ++r)
     for (int f = 0; f < spec->n_fac[r]; ++f) qs = spec->dim[r][f] + 1 > qs ? spec->dim[r][f] + 1 : qs;
   if (!bucket || qs > kRfQ || qs > ldx || np_ % kRgT || L > kRfMaxL) return -1;
   const DevSpec ds = to_dev(spec);
-  kl_refine_gate_kernel<<<L, 256, 0, st>>>(ds, x, ldx, params, noise, kdiag, n, np_, mode, refine_tau(), est, flag);
   const int cap = kl_refine_cap(L);
   for (int r0 = 0; r0 < L; r0 += cap) {  // (rounds with no flagged dims: launches that read the flags and exit)
     if (bucket == 1)
@@ -325,6 +336,13 @@ int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n
   kl_refine_diag_kernel<<<dim3(np_ / 256, L), 256, 0, st>>>(part, n, np_, flag, kdiag);
   LVAE_CHECK_LAUNCH();
   return 0;
+}
+
+int kl_refine_diag(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int np_, int L,
+                   const double* params, const double* noise, const float* Kinv, double* kdiag, double* K64,
+                   double* part, double* est, int* flag, hipStream_t st) {
+  LVAE_TRY(kl_refine_gate(spec, x, ldx, n, np_, L, params, noise, kdiag, est, flag, st));
+  return kl_refine_apply(spec, x, ldx, n, np_, L, params, noise, Kinv, kdiag, K64, part, flag, st);
 }
 
 }  // namespace lvae

@@ -563,6 +563,31 @@ def test_kl_closed_high_cond(hip):
             assert per[l][f"cuda:{key}"] < 1e-4, (l, key)
 
 
+@pytest.mark.parametrize("case", ["headline", "high_cond"])
+def test_kl_closed_early_route(hip, monkeypatch, case):
+    """The opt-in early reduce (LVAE_KL_EARLY=1, kl_closed.hip): a0 = Y^T (Y mu), diag K^-1 = the row sums of
+    squares of Y^T and a = a0 + Y^T (Y r) from the Y / Y^T planes before any lauum; the refinement gate on that
+    diagonal, and for the flagged dims their K^-1 alone (ci_lauum_flagged_f32) for the fp64 diag refinement; lauum
+    in the backward.  The headline workload and the high-cond draws of the tests above (some dims flagged), every
+    value and gradient within the north-star 1e-4 of the fp64 oracle."""
+    import lvae_amd as la
+    monkeypatch.setenv("LVAE_KL_EARLY", "1")
+    L, P = (16, 256) if case == "headline" else (8, 256)
+    rng = np.random.default_rng(16 if case == "headline" else 17)
+    k = la.generate_kernel(**CFG, latent_dim=L)
+    if case == "headline":
+        raw = _random_hypers(k, L, rng, scale=(0.3, 1.5), ell=(1.0, 4.0))
+        noise = torch.tensor(rng.uniform(0.5, 1.0, L))
+    else:
+        raw = _random_hypers(k, L, rng, scale=(0.2, 3.0), ell=(0.5, 6.0))
+        noise = torch.tensor(rng.uniform(0.05, 1.0, L))
+    worst, per = _kl_vs_oracle(P, L, raw, noise, seed=16 if case == "headline" else 17, oracle_dev="cuda",
+                               return_per_dim=True)
+    print(f"early route, {case}:", worst, "refined dims:", [l for l in range(L) if per[l]["refined"]])
+    for key, e in worst.items():
+        assert e < 1e-4, (key, e)
+
+
 @pytest.mark.parametrize("noise", [1e-3, 1e-4])
 def test_kl_closed_small_noise(hip, noise):
     """Small likelihood noise (N = 1024: cond(K) 1e3..1.3e5; K^-1 entries ~1/noise, which the
