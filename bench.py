@@ -83,6 +83,26 @@ def pmc_traffic(kernels, per_step=False):
         return None
 
 
+# MFMA utilisation per kernel from the committed rocprofv3 --pmc pass over this bench's closed step
+# (scripts/gpu_mfma_pmc.sh, scripts/mfma_pmc.py): SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+MFMA_PMC = os.path.join(ROOT, "profiles", "r6_mfma_pmc.json")
+MFMA_KERNELS = {"lauum + KL epilogue": "ci_gemm_kernel<3>", "trtri X step": "ci_gemm_kernel<0>",
+                "trtri Y step": "ci_gemm_kernel<1>", "potrf trailing update": "ci_update_kernel<2>",
+                "potrf panel": "ci_panel_kernel", "potrf pivot (split)": "ci_pivot_kernel<4>",
+                "binned hyper slab pass": "hb_slab_kernel"}
+
+
+def mfma_busy(name_part, path=MFMA_PMC):
+    """(mfma_busy_frac, dispatches) of the kernel whose name contains name_part in the committed MFMA PMC summary."""
+    try:
+        for k, v in json.load(open(path)).items():
+            if name_part in k.replace(" ", "") and "mfma_busy_frac" in v:
+                return v["mfma_busy_frac"], v["dispatches"]
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def kstats_avg_us(name_part, path=KSTATS):
     """(average launch duration in us, calls) of the kernel whose name contains name_part in the
     committed rocprofv3 stats CSV, or None."""
@@ -510,6 +530,21 @@ def run_closed(args, world, rank, dev):
                                      else "live HIP events", "launches_per_step": launches,
                 "achieved_event": ach_ev, "frac_event": ach_ev / HBM_PEAK_GBS,
                 "avg_launch_us_event": upd_ms / upd_n * 1e3, "padded_n": int(np_)}))
+        if headline_prof:
+            # north_star's "MFMA utilisation against the gfx950 peak": the matrix pipes' busy fraction per kernel
+            mu = {}
+            for what, kname in MFMA_KERNELS.items():
+                b = mfma_busy(kname)
+                if b:
+                    mu[what] = {"kernel": kname, "mfma_busy_frac": b[0], "dispatches_profiled": b[1]}
+            if mu:
+                res["mfma_utilisation"] = dict(mu, source=f"profiles/{os.path.basename(MFMA_PMC)} (rocprofv3 --pmc "
+                                               "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE over this bench's closed step; "
+                                               "busy / (1024 SIMDs x GRBM_GUI_ACTIVE / 8))")
+            for _, r in roofs:
+                b = mfma_busy(r["kernel"].split(" ")[0])
+                if b:
+                    r["mfma_busy_frac"] = b[0]
         roofs.sort(key=lambda r: -r[0])
         for i, (ms, r) in enumerate(roofs):
             r["gpu_ms_per_step"] = ms
