@@ -672,8 +672,7 @@ def run_c2(dev, reps=20):
     against PyTorch-ROCm fp32 Gram + torch.linalg.cholesky (rocSOLVER potrf) and + cholesky_inverse.
     gp_cholesky_gflops_hip is the potrf phase ALONE (the library's HIP events around its potrf
     sequence, LVAE_PH_POTRF), against torch.linalg.cholesky alone; the whole inverse is compared with
-    cholesky + cholesky_inverse.  The retired Gauss-Jordan sweep (lvae_spd_sweep_f32) is kept as a
-    labelled extra."""
+    cholesky + cholesky_inverse."""
     import lvae_amd as la
     from lvae_amd import _lib
     from lvae_amd.data import health_mnist_covariates
@@ -688,9 +687,6 @@ def run_c2(dev, reps=20):
     A = torch.empty(L, np_, np_, dtype=torch.float32, device=dev)
     Kinv = torch.empty_like(A)
     scr = torch.empty(int(lib.lvae_spd_inv_chol_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
-    with_sweep = os.environ.get("LVAE_BENCH_SWEEP") == "1"  # the retired sweep: opt-in extra
-    sscr = (torch.empty(int(lib.lvae_spd_sweep_scratch_size(np_, L)), dtype=torch.uint8, device=dev)
-            if with_sweep else None)
     logdet = torch.empty(L, dtype=torch.float64, device=dev)
     info = torch.empty(L, dtype=torch.int32, device=dev)
     noise = torch.ones(L, dtype=torch.float64, device=dev)
@@ -704,11 +700,6 @@ def run_c2(dev, reps=20):
         gram()
         _lib.check(lib.lvae_spd_inv_chol_f32(np_, L, _lib.ptr(A), _lib.ptr(scr), _lib.ptr(Kinv), _lib.ptr(logdet),
                                              _lib.ptr(info), _lib.stream_ptr()), "chol")
-
-    def hip_sweep():
-        gram()
-        _lib.check(lib.lvae_spd_sweep_f32(np_, L, _lib.ptr(A), _lib.ptr(sscr), _lib.ptr(Kinv), _lib.ptr(logdet),
-                                          _lib.ptr(info), _lib.stream_ptr()), "sweep")
 
     def torch_chol():
         return torch.linalg.cholesky(torch_gram_f32(params, X))
@@ -751,7 +742,6 @@ def run_c2(dev, reps=20):
     t_gram_torch = timed(lambda: torch_gram_f32(params, X))
     t_potrf_torch = timed(lambda: torch_potrf_only(Kt))
     t_chol, t_inv = timed(torch_chol), timed(torch_chol_inv)
-    t_sweep = timed(hip_sweep) if with_sweep else None
     # the exported N x N factor (lvae_potrf_f32 / _f64 through lvae_amd.linalg) on the same prebuilt Gram,
     # against torch.linalg.cholesky on it: the same input, the same output (L)
     import lvae_amd.linalg as LA
@@ -789,9 +779,6 @@ def run_c2(dev, reps=20):
                              "note": "the C-ABI N x N factor (potrf.hip) on the prebuilt Gram, returning L, vs "
                                      "torch.linalg.cholesky (rocSOLVER) on the same matrix; f32 includes the copy "
                                      "into the padded workspace and out of it"},
-            **({"extra_retired_sweep": {"hip_gram_sweep_inverse_ms": t_sweep,
-                                        "note": "lvae_spd_sweep_f32, the rounds 1-2 block Gauss-Jordan inverse; the "
-                                                "KL no longer uses it (LVAE_BENCH_SWEEP=1)"}} if with_sweep else {}),
             "note": "HIP: Gram + Cholesky route (K^-1 and log|K|); torch: PyTorch fp32 Gram + torch.linalg.cholesky "
                     "(rocSOLVER) [+ cholesky_inverse + log-det for the same outputs]"}
 

@@ -5,7 +5,7 @@
  * device memory inside, all work enqueued asynchronously on the caller's hipStream_t (passed as
  * void*), safe to call from several host threads.  Process-wide state is limited to (1) the
  * opt-in phase timer (lvae_prof_*) and (2) the blocked inverses' side stream (lvae_spd_inv_chol_f32,
- * lvae_kl_closed_*, lvae_spd_sweep_f32): ONE high-priority stream + seven events (fork, prep, c, and
+ * lvae_kl_closed_*): ONE high-priority stream + seven events (fork, prep, c, and
  * two pairs alternating by pass parity) per device, shared by every caller stream, created on first
  * use, kept for the process lifetime, and guarded by a mutex held for each call's whole enqueue
  * sequence (calls from different caller streams serialise on it).  The calls are graph-capturable (the side stream joins
@@ -21,8 +21,8 @@
  *   autograd of that Gram wrt (scale, lengthscale) -> lvae_gram_bwd_*
  *   torch.cholesky(K1) on N x N           -> lvae_potrf_f64 / _f32 (elbo_functions.py:26)
  *   torch.cholesky_solve(B, LK1)          -> lvae_potrs_f64 / _f32, lvae_trsm_* (elbo_functions.py:27-28)
- *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_spd_inv_chol_f32 (also
- *                                             lvae_spd_sweep_f32; elbo_functions.py:26-29)
+ *   torch.cholesky / cholesky_solve(I) / log-det on N x N -> lvae_spd_inv_chol_f32
+ *                                             (elbo_functions.py:26-29)
  *   KL_closed forward + autograd backward -> lvae_kl_closed_fwd_f32 / _bwd_f32 (elbo_functions.py:8-34)
  *   batched small fp64 factor + inverse   -> lvae_spd_inv_small_f64 (elbo_functions.py:176-186,
  *                                             training.py:130-134)
@@ -170,29 +170,15 @@ int lvae_kl_closed_refine_state(int n, int L, const void* workspace, double* est
  * factor's choice (int32: 1 = binned) to a device buffer, on `stream`.  No reference counterpart (diagnostic). */
 int lvae_kl_closed_hyper_state(int n, int L, const void* workspace, int32_t* on, void* stream);
 
-/* A^-1 and log|A| of L padded SPD matrices by a block symmetric sweep (Gauss-Jordan on SPD) with
- * 256-wide pivot blocks (the r1-r2 Regime B inverse; lvae_kl_closed_* now use lvae_spd_inv_chol_f32's
- * blocked Cholesky, which is ~100x more accurate at cond 1e5; kept as a C-ABI entry): per pivot block k,
- * A_kk <- -P^-1, A_ik <- A_ik P^-1, A_ij <- A_ij - A_ik P^-1 A_kj (P = A_kk); after the last block
- * A = -K^-1.  np % 256 == 0.  A [L, np, np] (lower 256-block tiles read, overwritten);
- * scratch: lvae_spd_sweep_scratch_size(np, L) bytes, 256-B aligned; Ainv [L, np, np] full
- * symmetric out; logdet [L]; info [L] LAPACK-style (first bad column + 1).  Pivot blocks are
- * inverted by a blocked Cholesky in LDS (fp32 MFMA); with lookahead, the next pivot and its
- * prep run on the internal side stream beside each interior update and are
- * joined back to `stream`.
- * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).        */
-size_t lvae_spd_sweep_scratch_size(int np_, int L);
-int lvae_spd_sweep_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,
-                       void* stream);
-
 /* A^-1 and log|A| of L padded SPD matrices by a blocked Cholesky factorisation, triangular inverse
  * and product (LAPACK potrf + trtri + lauum, 256-wide blocks; the inverse lvae_kl_closed_* use):
  * potrf's pivot blocks factored and inverted in LDS (fp32 MFMA), its panel / rank-256 trailing
  * updates and trtri / lauum's whole-block GEMMs on the f16 cores with the 3-product split; the next
- * pivot runs on a side stream beside each trailing update.  Same arguments and outputs as
- * lvae_spd_sweep_f32 (A overwritten, Ainv full symmetric, info LAPACK-style); scratch:
- * lvae_spd_inv_chol_scratch_size(np, L) bytes, 256-B aligned.  Backward-stable in the Cholesky sense:
- * |I - A Ainv| ~ cond(A) 2^-24, against ~100x that for the sweep at cond 1e5.
+ * pivot runs on a side stream beside each trailing update.  np % 256 == 0; A [L, np, np] (lower
+ * 256-block tiles read, overwritten); Ainv [L, np, np] full symmetric out; logdet [L]; info [L]
+ * LAPACK-style (first bad column + 1); scratch: lvae_spd_inv_chol_scratch_size(np, L) bytes, 256-B
+ * aligned.  Backward-stable in the Cholesky sense: |I - A Ainv| ~ cond(A) 2^-24 (the rounds 1-2 block
+ * Gauss-Jordan sweep, ~100x less accurate at cond 1e5, is retired: csrc/retired/spd_sweep.hip, not built).
  * Replaces torch.cholesky + cholesky_solve(I) + the log-det (elbo_functions.py:26-29).         */
 size_t lvae_spd_inv_chol_scratch_size(int np_, int L);
 int lvae_spd_inv_chol_f32(int np_, int L, float* A, void* scratch, float* Ainv, double* logdet, int32_t* info,

@@ -132,8 +132,6 @@ SIGNATURES = {
     "lvae_conv3x3_pool_wgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
     "lvae_conv3x3_pool_dgrad_lds": (_SZ, [_I32, _I32, _I32]),
     "lvae_conv3x3_pool_dgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
-    "lvae_spd_sweep_scratch_size": (_SZ, [_I32, _I32]),
-    "lvae_spd_sweep_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_spd_inv_chol_scratch_size": (_SZ, [_I32, _I32]),
     "lvae_spd_inv_chol_f32": (_I32, [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "lvae_potrf_f64": (_I32, [_I32, _I32, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP]),

@@ -176,18 +176,16 @@ def test_gram_batched_semantics(hip):
     assert rel(got, raw.grad) < 1e-12
 
 
-# the retired block sweep (spd_sweep.hip, rounds 1-2) is an opt-in extra: LVAE_TEST_SWEEP=1 adds it back
-import os as _os  # noqa: E402
-INV_KINDS = ["chol", "sweep"] if _os.environ.get("LVAE_TEST_SWEEP") == "1" else ["chol"]
+# (the rounds 1-2 block sweep, spd_sweep.hip, is retired and no longer built: csrc/retired/)
+INV_KINDS = ["chol"]
 
 
 def _spd_inverse(hip, kind, n, L, Ad):
     """A^-1 (both triangles), log|A|, info of the [L, n, n] fp32 lower triangles Ad through the C ABI:
-    kind 'chol' (blocked Cholesky + trtri + lauum, chol_inv.hip, the KL's inverse) or 'sweep'."""
+    kind 'chol' (blocked Cholesky + trtri + lauum, chol_inv.hip, the KL's inverse)."""
     import lvae_amd as la
     P = la._lib
-    size = hip.lvae_spd_inv_chol_scratch_size if kind == "chol" else hip.lvae_spd_sweep_scratch_size
-    fn = hip.lvae_spd_inv_chol_f32 if kind == "chol" else hip.lvae_spd_sweep_f32
+    size, fn = hip.lvae_spd_inv_chol_scratch_size, hip.lvae_spd_inv_chol_f32
     scr = torch.full((size(n, L) // 4,), float("nan"), device=DEV)
     Ai = torch.full_like(Ad, float("nan"))
     logdet = torch.zeros(L, dtype=torch.float64, device=DEV)
