@@ -49,11 +49,13 @@ X3_PRODUCTS = 3                 # f16 MFMA products per fp32-equivalent product 
 DTYPE = "f16x3-split (fp32-equivalent)"
 # Memory-side bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc.sh):
 # FETCH_SIZE x 2 (16-B/lane coalesced reads on gfx950, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r5_pmc_summary.json")
+# (LVAE_PROFILE_TAG: the round whose committed profile files price the line; scripts/gpu_evidence.sh writes them)
+TAG = os.environ.get("LVAE_PROFILE_TAG", "r6")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", f"{TAG}_pmc_summary.json")
 # The committed rocprofv3 --kernel-trace --stats summary of the default closed bench on the final tree
-# (scripts/gpu_r5g.sh): the roofline's `frac` is priced on its average launch duration of the dominant
+# (scripts/gpu_evidence.sh): the roofline's `frac` is priced on its average launch duration of the dominant
 # kernel, so that it recomputes from profiles/; the live HIP-event figure is reported beside it.
-KSTATS = os.path.join(ROOT, "profiles", "r5_headline_kernel_stats.csv")
+KSTATS = os.path.join(ROOT, "profiles", f"{TAG}_headline_kernel_stats.csv")
 # the Cholesky's trailing rank-256 update (chol_inv.hip): U2 alone (MODE kCiU2) when the lookahead chain
 # runs on the side stream (schedule (b), > CI_FUSE_MAX_L dims per call), else fused with U1 (kCiU12)
 CI_FUSE_MAX_L = 16
@@ -85,7 +87,7 @@ def pmc_traffic(kernels, per_step=False):
 
 # MFMA utilisation per kernel from the committed rocprofv3 --pmc pass over this bench's closed step
 # (scripts/gpu_mfma_pmc.sh, scripts/mfma_pmc.py): SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
-MFMA_PMC = os.path.join(ROOT, "profiles", "r6_mfma_pmc.json")
+MFMA_PMC = os.path.join(ROOT, "profiles", f"{TAG}_mfma_pmc.json")
 MFMA_KERNELS = {"lauum + KL epilogue": "ci_gemm_kernel<3>", "trtri X step": "ci_gemm_kernel<0>",
                 "trtri Y step": "ci_gemm_kernel<1>", "potrf trailing update": "ci_update_kernel<2>",
                 "potrf panel": "ci_panel_kernel", "potrf pivot (split)": "ci_pivot_kernel<4>",
