@@ -697,10 +697,11 @@ __device__ inline float ci_acc_absmax(const sx_f32x16 (&acc)[4][2]) {
 // pass-0 C operand: blocks i >= 1 of column 0 of A, each with the split scale of its exact max.
 // grid (nt - 1, L), 256 threads.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ci_prep0_kernel(const float* __restrict__ Aall, int np_, CiScratch S) {
+__global__ __launch_bounds__(256) void ci_prep0_kernel(const float* __restrict__ Aall, int np_, CiScratch S,
+                                                       int col = 0) {
   __shared__ uint32_t red;
-  const int l = blockIdx.y, i = blockIdx.x + 1, t = threadIdx.x;
-  const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_;
+  const int l = blockIdx.y, i = col + 1 + blockIdx.x, t = threadIdx.x;
+  const float* T = Aall + (int64_t)l * np_ * np_ + (int64_t)i * kSwB * np_ + (int64_t)col * kSwB;
   if (t == 0) red = 0u;
   float m = 0.f;
   for (int e = t; e < kSwBB / 4; e += 256) {
@@ -717,9 +718,9 @@ __global__ __launch_bounds__(256) void ci_prep0_kernel(const float* __restrict__
   for (int e = t; e < kSwBB / 4; e += 256) {
     const int r = e >> 6, c = (e & 63) * 4;
     const f32x4 v = *reinterpret_cast<const f32x4*>(T + (int64_t)r * np_ + c);
-    ci_split4(v, sc, S.Ch[0] + o + r * kSwB + c, S.Cl[0] + o + r * kSwB + c);
+    ci_split4(v, sc, S.Ch[col & 1] + o + r * kSwB + c, S.Cl[col & 1] + o + r * kSwB + c);
   }
-  if (t == 0) S.c_scale(l, 0, i) = sc;
+  if (t == 0) S.c_scale(l, col, i) = sc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -864,6 +865,304 @@ __global__ __launch_bounds__(512) void ci_update_kernel(float* __restrict__ Aall
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * ninv), rc, vo,
                                                 ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// The trailing update (U1 + U2 as ci_update_kernel<kCiU12>) with a deeper DMA pipeline (r6, opt-in LVAE_CI_URING=1:
+// measured slower, 211 vs 166 us per launch -- twice the barriers per tile and 32-B row pieces): 16-deep
+// K stages in a ring of 4 (4 x 32 KB of LDS, the same 128 KB as the 2 x 32-deep double buffer), each stage's DMA
+// issued THREE stages ahead, so that ~3 stages of MFMAs (~2.2 us) cover an HBM round trip instead of one (the
+// double-buffered form waits on most chunks' DMA: 0.26 MFMA-busy, 0.29 of HBM).  The A tile streams in 16 pieces
+// of 8 accumulator elements, each consumed three stages after its loads were issued; one counted vmcnt per stage
+// covers both (every stage issues a DMA -- past the last chunk a re-read into a dead buffer -- so the count is
+// uniform).  LDS rows of 16 halves (32 B): the two 8-half groups swapped on bit 3 of the row (the c16 planes'
+// swizzle), so a ds_read_b128 phase of 16 consecutive rows covers all 64 banks.
+// ------------------------------------------------------------------------------------------
+constexpr int kU16K = 16, kU16Part = kSwB * kU16K, kU16Ring = 4;
+
+// one stage's DMA: 4 parts x 256 rows x 32 B, one 1 KB instruction per part and wave (4 per thread)
+__device__ inline void u16_issue(const _Float16* __restrict__ ah, const _Float16* __restrict__ al,
+                                 const _Float16* __restrict__ bh, const _Float16* __restrict__ bl, int64_t ld, int k0,
+                                 _Float16* __restrict__ stage) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const _Float16* src[4] = {ah, al, bh, bl};
+  // wave w, instruction p: part p, rows 32 w .. 32 w + 31 (2 lanes per row); LDS image [row][16] linear per wave,
+  // the global source's 8-half group chosen so that physical group (lane & 1) holds logical group (lane & 1) ^ bit 3
+  const int row = 32 * w + (lane >> 1), g = (lane & 1) ^ ((row >> 3) & 1);
+  const int64_t go = (int64_t)row * ld + k0 + 8 * g;
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+    __builtin_amdgcn_global_load_lds((const void*)(src[p] + go), (void*)(stage + p * kU16Part + w * 512), 16, 0, 0);
+}
+
+__device__ inline sx_half8 u16_frag(const _Float16* __restrict__ part, int row, int h) {
+  return *reinterpret_cast<const sx_half8*>(part + row * kU16K + ((h ^ ((row >> 3) & 1)) << 3));
+}
+
+// one 16-deep stage: acc[a][b] += A rows x B rows (x3 products), the wave's 128 x 64 (sx_mma_stage's layout)
+__device__ inline void u16_mma_stage(const _Float16* __restrict__ cur, sx_f32x16 (&acc)[4][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 2) * 128, wn = (w & 3) * 64, r32 = lane & 31, kh = lane >> 5;
+  sx_half8 bH[2], bL[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    bH[b] = u16_frag(cur + 2 * kU16Part, wn + 32 * b + r32, kh);
+    bL[b] = u16_frag(cur + 3 * kU16Part, wn + 32 * b + r32, kh);
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const sx_half8 aH = u16_frag(cur, wm + 32 * a + r32, kh);
+    const sx_half8 aL = u16_frag(cur + kU16Part, wm + 32 * a + r32, kh);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH[b], acc[a][b], 0, 0, 0);
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL[b], acc[a][b], 0, 0, 0);
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH[b], acc[a][b], 0, 0, 0);
+    }
+  }
+}
+
+// MODE and arguments as ci_update_kernel (kCiU12 / kCiU2 / kCiU1)
+template <int MODE>
+__global__ __launch_bounds__(512) void ci_update_ring_kernel(float* __restrict__ Aall, CiScratch S, int np_, int k,
+                                                             int ntl, int nwg, int n1 = 0) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[kU16Ring * 4 * kU16Part];
+  __shared__ uint32_t red;
+  if (MODE != kCiU2 && threadIdx.x == 0) red = 0u;
+  const int nt = np_ / kSwB;
+  const bool u1 = MODE == kCiU1 || (MODE == kCiU12 && (int)blockIdx.x < n1 * (nwg / max(ntl, 1)));
+  int l, I, J;
+  if (MODE == kCiU12 && u1) {
+    l = blockIdx.x / n1;
+    I = k + 2 + blockIdx.x % n1;
+    J = k + 1;
+  } else {
+    const int orig = MODE == kCiU12 ? blockIdx.x - n1 * (nwg / ntl) : blockIdx.x;
+    const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    l = wgid / ntl;
+    const int t = wgid % ntl;
+    if constexpr (MODE == kCiU1) {
+      I = (ntl == nt - k - 1) ? k + 1 + t : k + 2 + t;
+      J = k + 1;
+    } else {
+      sx_tri_blocked(t, nt - k - 2, I, J);
+      I += k + 2;
+      J += k + 2;
+    }
+  }
+  const int64_t np2 = (int64_t)np_ * np_;
+  float* C = Aall + l * np2 + (int64_t)I * kSwB * np_ + J * kSwB;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int vo = (((w >> 2) * 128 + 4 * (lane >> 5)) * np_ + (w & 3) * 64 + (lane & 31)) * 4;
+  const int64_t oa = l * np2 + (int64_t)I * kSwB * np_ + k * kSwB, ob = l * np2 + (int64_t)J * kSwB * np_ + k * kSwB;
+  const float cs = S.lsc[((int64_t)l * S.nt + I) * S.nt + k] * S.lsc[((int64_t)l * S.nt + J) * S.nt + k];
+  const float ncs = -cs, ninv = -1.0f / cs;  // acc = L_I L_J^T - A (units of cs); the result is -acc / cs
+  const _Float16* ah = S.Lh + oa;
+  const _Float16* al = S.Ll + oa;
+  const _Float16* bh = S.Lh + ob;
+  const _Float16* bl = S.Ll + ob;
+  sx_f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  constexpr int CAUX = 2;
+  constexpr int nk = kSwB / kU16K;  // 16 stages; 128 A elements per thread, 8 per stage
+  float cv[4][8];
+  auto a_load = [&](int s, float (&dst)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = 8 * s + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      dst[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX));
+    }
+  };
+  auto a_add = [&](int s, const float (&src)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = 8 * s + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      acc[a][b][e] += src[q] * ncs;
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < kU16Ring - 1; ++s) u16_issue(ah, al, bh, bl, np_, s * kU16K, lds + s * 4 * kU16Part);
+#pragma unroll
+  for (int s = 0; s < nk; ++s) {
+    // issued after DMA s: DMA s+1, s+2 (4 each) and the A pieces s-3 .. s-1 (8 each) -- DMA s and A piece s-3 landed
+    if (s == 0) SX_WAIT_VM(8);
+    else if (s == 1) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+    else __builtin_amdgcn_s_waitcnt(0x4F78);              // vmcnt(24)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage s in LDS for every wave; every wave's reads of stage s-1 retired
+    const int sn = s + kU16Ring - 1 < nk ? s + kU16Ring - 1 : nk - 1;  // (past the end: a re-read into a dead buffer)
+    u16_issue(ah, al, bh, bl, np_, sn * kU16K, lds + ((s + kU16Ring - 1) % kU16Ring) * 4 * kU16Part);
+    a_load(s, cv[s & 3]);
+    if (s >= 3) a_add(s - 3, cv[(s - 3) & 3]);
+    __builtin_amdgcn_s_setprio(1);
+    u16_mma_stage(lds + (s % kU16Ring) * 4 * kU16Part, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  SX_WAIT_VM(0);
+#pragma unroll
+  for (int j = nk - 3; j < nk; ++j) a_add(j, cv[j & 3]);
+  if (u1 && I != J) {
+    // a block of column k+1 = block I of the next pass's C operand: straight to its planes
+    const float sc = x3_scale(sw_block_max(ci_acc_absmax(acc) * fabsf(ninv), &red));
+    const int64_t on = (int64_t)l * np_ * kSwB + (int64_t)I * kSwBB;
+    ci_planes_out(acc, ninv, sc, S.Ch[(k + 1) & 1] + on, S.Cl[(k + 1) & 1] + on, kSwB);
+    if (threadIdx.x == 0) S.c_scale(l, k + 1, I) = sc;
+  } else {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * ninv), rc, vo,
+                                                ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// U2 on 128 x 128 sub-tiles (r6, opt-in LVAE_CI_U128=1; measured slower in the step, see ci_factor_f32): A_IJ -=
+// L_Ik L_Jk^T for the lower tiles I >= J >= k+2,
+// each 256-tile as four 256-thread workgroups of 128 x 128 (the upper-right quarter of a diagonal tile skipped: no
+// reader needs A's strict upper part), K = 256 in 8 DMA-staged chunks of 32, double-buffered: 64 KB of LDS and
+// ~128 VGPRs per workgroup, so TWO workgroups share a CU and each one's HBM round trips and barriers hide under
+// the other's MFMAs (the 256-tile form holds a CU alone: 128 KB of LDS, 2 waves per SIMD, and stalls on every
+// chunk's DMA).  The A tile streams in 8 pieces of 8 accumulator elements inside the K loop, as in
+// ci_update_kernel.  Waves 2 x 2, 64 x 64 each = 2 x 2 blocks of v_mfma_f32_32x32x16_f16 x 3 products.
+// ------------------------------------------------------------------------------------------
+constexpr int kU8Rows = 128, kU8Part = kU8Rows * kSxBK;  // rows per operand part; halves per part and stage
+
+// one stage: 4 parts (A hi, A lo, B hi, B lo) x 8 blocks of 16 rows (1 KB each); wave w issues blocks 2w, 2w+1
+__device__ inline void u8_issue(const _Float16* __restrict__ ah, const _Float16* __restrict__ al,
+                                const _Float16* __restrict__ bh, const _Float16* __restrict__ bl, int64_t ld, int k0,
+                                _Float16* __restrict__ stage) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const _Float16* src[4] = {ah, al, bh, bl};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int blk = 2 * w + q;
+    const int row = 16 * blk + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3);  // logical chunk stored at physical chunk lane & 3 (sx_frag's)
+    const int64_t go = (int64_t)row * ld + k0 + 8 * c;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(src[p] + go), (void*)(stage + p * kU8Part + blk * 512), 16, 0, 0);
+  }
+}
+
+// one 32-deep stage of the wave's 64 x 64: acc[a][b] (a, b < 2) += A rows x B rows (three products each)
+__device__ inline void u8_mma_stage(const _Float16* __restrict__ cur, sx_f32x16 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64, r32 = lane & 31, kh = lane >> 5;
+#pragma unroll
+  for (int ks = 0; ks < kSxBK / 16; ++ks) {
+    const int c = 2 * ks + kh;
+    sx_half8 bH[2], bL[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      bH[b] = sx_frag(cur + 2 * kU8Part, wn + 32 * b + r32, c);
+      bL[b] = sx_frag(cur + 3 * kU8Part, wn + 32 * b + r32, c);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const sx_half8 aH = sx_frag(cur, wm + 32 * a + r32, c);
+      const sx_half8 aL = sx_frag(cur + kU8Part, wm + 32 * a + r32, c);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aL, bH[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bL[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(aH, bH[b], acc[a][b], 0, 0, 0);
+      }
+    }
+  }
+}
+
+// grid: 4 ntl L workgroups (ntl trailing 256-tiles per dim, pass k), XCD-contiguous like ci_update_kernel
+__global__ __launch_bounds__(256, 2) void ci_update128_kernel(float* __restrict__ Aall, CiScratch S, int np_, int k,
+                                                              int ntl, int nwg, int n1 = 0) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * kU8Part];
+  const int nt = np_ / kSwB;
+  const int orig = blockIdx.x, xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int per = 4 * (n1 + ntl), l = wgid / per, t = (wgid % per) >> 2, si = (wgid & 3) >> 1, sj = wgid & 1;
+  int I, J;
+  if (t < n1) {  // column k+1's tiles (without the pivot block): fp32 into A, split by ci_prep0_kernel(col k+1)
+    I = k + 2 + t;
+    J = k + 1;
+  } else {
+    sx_tri_blocked(t - n1, nt - k - 2, I, J);
+    I += k + 2;
+    J += k + 2;
+  }
+  if (I == J && si < sj) return;  // (uniform) the diagonal tile's upper-right quarter
+  const int64_t np2 = (int64_t)np_ * np_;
+  const int r0 = I * kSwB + si * kU8Rows, c0 = J * kSwB + sj * kU8Rows;
+  float* C = Aall + l * np2 + (int64_t)r0 * np_ + c0;
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(C, (short)0, 0x7fffffff, 0x00020000);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // accumulator element (a, e, b) of this lane: row (w >> 1) 64 + 32 a + (e & 3) + 8 (e >> 2) + 4 (lane >> 5),
+  // column (w & 1) 64 + 32 b + (lane & 31)
+  const int vo = (((w >> 1) * 64 + 4 * (lane >> 5)) * np_ + (w & 1) * 64 + (lane & 31)) * 4;
+  const int64_t oa = l * np2 + (int64_t)r0 * np_ + k * kSwB, ob = l * np2 + (int64_t)c0 * np_ + k * kSwB;
+  const float cs = S.lsc[((int64_t)l * S.nt + I) * S.nt + k] * S.lsc[((int64_t)l * S.nt + J) * S.nt + k];
+  const float ncs = -cs, ninv = -1.0f / cs;  // acc = L_I L_J^T - A (units of cs); the result is -acc / cs
+  const _Float16* ah = S.Lh + oa;
+  const _Float16* al = S.Ll + oa;
+  const _Float16* bh = S.Lh + ob;
+  const _Float16* bl = S.Ll + ob;
+  sx_f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sx_f32x16{};
+  constexpr int CAUX = 2;
+  constexpr int nk = kSwB / kSxBK;  // 8 chunks; 64 A elements per thread, 8 per chunk
+  float cv[2][8];
+  u8_issue(ah, al, bh, bl, np_, 0, lds);
+#pragma unroll
+  for (int s = 0; s < nk; ++s) {
+    if (s == 0) SX_WAIT_VM(0);
+    else __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): DMA s and A piece s - 2 landed (A piece s - 1 may fly)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nk) u8_issue(ah, al, bh, bl, np_, (s + 1) * kSxBK, lds + ((s + 1) & 1) * 4 * kU8Part);
+    if (s >= 2) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = 8 * (s - 2) + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+        acc[a][b][e] += cv[s & 1][q] * ncs;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = 8 * s + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      cv[s & 1][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rc, vo, ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX));
+    }
+    __builtin_amdgcn_s_setprio(1);
+    u8_mma_stage(lds + (s & 1) * 4 * kU8Part, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+#pragma unroll
+  for (int j = nk - 2; j < nk; ++j)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = 8 * j + q, a = i >> 5, e = (i >> 1) & 15, b = i & 1;
+      acc[a][b][e] += cv[j & 1][q] * ncs;
+    }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][e] * ninv), rc, vo,
+                                              ((32 * a + (e & 3) + 8 * (e >> 2)) * np_ + 32 * b) * 4, CAUX);
 }
 
 // D (the pivots' Y_kk planes) -> the diagonal tiles of the row-major Y planes (after potrf: the Y
@@ -1517,6 +1816,14 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
     // 5.70 vs 5.59 ms, L = 8 3.60 vs 3.53, L = 4 2.85 vs 2.87; profiles/r4_lookahead_ab.txt): the second
     // launch's tail and the extra launch outweigh the earlier pivot start.  Off by default.
     static const bool la = getenv("LVAE_CI_LOOKAHEAD") && atoi(getenv("LVAE_CI_LOOKAHEAD")) != 0;
+    // LVAE_CI_U128=0: the trailing update as whole 256-tiles fused with column m+1's (ci_update_kernel<kCiU12>)
+    // instead of the 128 x 128 sub-tile kernel (ci_update128_kernel)
+    const bool u128 = getenv("LVAE_CI_U128") && atoi(getenv("LVAE_CI_U128")) != 0;
+    // LVAE_CI_URING=1: the fused update on the 16-deep ring (ci_update_ring_kernel) instead of the double-buffered
+    // 32-deep stages (ci_update_kernel).  Both opt-in forms measured slower (r6, profiles/r6_update_ab.txt): the ring
+    // 211 vs 166 us per launch, the 128 x 128 sub-tiles 116 us for the trailing tiles but + 50 us for column k+1 as
+    // its own launch (9.21 vs 9.14 ms per step), or + a 70 us split pass with the column folded in (9.58-9.63 vs 9.22)
+    const bool uring = getenv("LVAE_CI_URING") && atoi(getenv("LVAE_CI_URING")) != 0;
     pipe = pmode > 0;
     if (fuse) {
       ci_pivot_kernel<1><<<L, 1024, 0, sd->s>>>(A, np_, 0, S, logdet, info, 0, L, g_pivot_prof);
@@ -1568,7 +1875,15 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
           } else {
             if (n2 > 0) {
               ProfScope pu(LVAE_PH_SWEEP_UPD, st);
-              ci_update_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
+              if (u128) {  // column m+1 and the trailing tiles as 128 x 128 sub-tiles, two workgroups per CU; then
+                           // column m+1's fp32 tiles split into pass m+1's C planes (each 256-tile's exact-max scale)
+                ci_update128_kernel<<<4 * (n1 + n2) * L, 256, 0, st>>>(A, S, np_, m, n2, 4 * (n1 + n2) * L, n1);
+                ci_prep0_kernel<<<dim3(n1, L), 256, 0, st>>>(A, np_, S, m + 1);
+              } else if (uring) {
+                ci_update_ring_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
+              } else {
+                ci_update_kernel<kCiU12><<<(n1 + n2) * L, 512, 0, st>>>(A, S, np_, m, n2, n2 * L, n1);
+              }
             }
             if (!ok(hipEventRecord(sd->u2p[m & 1], st))) return LVAE_ERR_LAUNCH;
           }
@@ -1605,7 +1920,10 @@ int ci_factor_f32(int np_, int L, float* A, void* scratch, _Float16* YT, float* 
         const int n2 = (nt - k - 2) * (nt - k - 1) / 2;
         if (n2 > 0) {
           ProfScope pu(LVAE_PH_SWEEP_UPD, st);
-          ci_update_kernel<kCiU2><<<n2 * L, 512, 0, st>>>(A, S, np_, k, n2, n2 * L);
+          if (u128)
+            ci_update128_kernel<<<4 * n2 * L, 256, 0, st>>>(A, S, np_, k, n2, 4 * n2 * L);
+          else
+            ci_update_kernel<kCiU2><<<n2 * L, 512, 0, st>>>(A, S, np_, k, n2, n2 * L);
         }
       }
       if (!ok(hipStreamWaitEvent(st, sd->prep, 0))) return LVAE_ERR_LAUNCH;  // the last pivot

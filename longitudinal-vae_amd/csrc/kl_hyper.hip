@@ -406,6 +406,13 @@ constexpr int kHbSlabThreads = 256, kHbSlabWaves = kHbSlabThreads / 64;
 #define LVAE_HB_FOLD 16
 #endif
 constexpr int kHbFold = LVAE_HB_FOLD;  // tiles summed in fp32 by the accumulators before the fp64 fold (power of 2)
+#ifndef LVAE_HB_DEPTH
+#define LVAE_HB_DEPTH 1
+#endif
+// K^-1 tiles in flight per workgroup (1, 2 or 4): deeper prefetch measured slower (r6, profiles/r6_slab_depth_ab.txt:
+// 681 / 708 / 1894 us per launch at 1 / 2 / 4; the extra registers cost the second workgroup per CU at 4)
+constexpr int kHbDepth = LVAE_HB_DEPTH;
+static_assert(kHbDepth == 1 || kHbDepth == 2 || kHbDepth == 4, "nt = np / 64 is a multiple of 4");
 
 struct HbPre {        // one tile's prefetch
   hb_f32x2 pk[8];     // K^-1 rows 8 (tid >> 5) + u, columns 2 (tid & 31) + 0, 1
@@ -632,7 +639,8 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
       }
     }
     __syncthreads();
-    fetch(I + 1 < nt ? I + 1 : nt - 1, p);  // (in flight under this tile's work and the other workgroup's)
+    // (kHbDepth tiles ahead, in flight under this tile's work and the other workgroup's)
+    fetch(I + kHbDepth < nt ? I + kHbDepth : nt - 1, p);
     if (!(dbg & 1) && it0) {
       auto onehot = [&](int g, int b0, int ks) {  // A operand: [bin b0 + (lane & 31)][rows 16 ks + 8 hh + 0..7]
         const unsigned mybin = (unsigned)(b0 + (lane & 31));
@@ -709,9 +717,15 @@ __global__ __launch_bounds__(kHbSlabThreads, 2) void hb_slab_kernel(GramTab tb, 
     __syncthreads();  // every reader of the planes, the window columns and the bins done before the next store
   };
 
-  HbPre pa;
-  fetch(0, pa);
-  for (int I = 0; I < nt; ++I) body(I, pa);
+  // kHbDepth prefetch buffers in rotation (static names: the loop is unrolled by kHbDepth; nt = np / 64 is a
+  // multiple of 4)
+  HbPre pre[kHbDepth];
+#pragma unroll
+  for (int u = 0; u < kHbDepth; ++u) fetch(u, pre[u]);
+  for (int I = 0; I < nt; I += kHbDepth) {
+#pragma unroll
+    for (int u = 0; u < kHbDepth; ++u) body(I + u, pre[u]);
+  }
   // (the last tile folds too; the scratch's stores and atomics complete and visible to
   // the workgroup before its epilogue reads them)
   __builtin_amdgcn_s_waitcnt(0);  // (vmcnt / lgkmcnt / expcnt 0: this wave's stores and atomics done)
