@@ -248,22 +248,41 @@ class HensmanStep:
         return out
 
 
+def _comm_capturable():
+    """RCCL collectives captured into the step's graph (one replay per step): opt-in, LVAE_GRAPH_COMM=1 with an
+    RCCL ("nccl") default process group.  Measured (r6): it matches the eager step (test_rccl_world1_graphed_hensman
+    _two_graphs[True]) and 100 back-to-back replays leave every info word clean (scripts/dp_replay_diag.py), but a
+    process that had replayed the two-graph form first and then the captured form aborted in its final
+    synchronise (profiles/r6_capture_comm_abort.log, cause not found) -- so the default stays two graphs around
+    the eager collectives, which the driver's multi-GPU run cannot lose to an abort."""
+    import os
+    import torch.distributed as dist
+    if os.environ.get("LVAE_GRAPH_COMM", "0") != "1":
+        return False
+    return dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+
+
 class GraphedStep:
     """A ClosedStep / HensmanStep replayed as HIP graphs.
 
     ``inputs`` are static device tensors (img, mask, X, eps) the caller refills in place between
     replays (e.g. ``index_select(..., out=)`` of the next batch).  With no communication the whole
-    step is one graph; with a ``grad_hook`` / ``ng_reduce`` (data parallel) the step is two graphs
-    around the eager collectives.  The optimiser must be capturable (torch.optim.Adam(...,
+    step is one graph; with a ``grad_hook`` / ``ng_reduce`` (data parallel) the step is two graphs around the
+    eager collectives, or (``capture_comm``, opt-in LVAE_GRAPH_COMM=1 over RCCL) one graph with the collectives
+    captured.  The optimiser must be capturable (torch.optim.Adam(...,
     capturable=True)); numerical-failure checks are deferred (set_sync_checks(False)) and
     ``check()`` reads the captured info arrays, which every replay rewrites.  shared_pool: capture the
     second graph into the first one's memory pool (diagnostics, scripts/dp_replay_diag.py)."""
 
-    def __init__(self, step, inputs, warmup=3, shared_pool=False):
+    def __init__(self, step, inputs, warmup=3, shared_pool=False, capture_comm=None):
         self.step, self.inputs = step, inputs
         if getattr(step, "gvae", None) is not None:
             step.gvae = None  # (the whole step is one graph here: no graphed ConvVAE parts inside the capture)
         comm = getattr(step, "grad_hook", None) is not None or getattr(step, "ng_reduce", None) is not None
+        if capture_comm is None:
+            capture_comm = _comm_capturable()
+        if comm and capture_comm:
+            comm = False  # the collectives are captured into the one graph with the rest of the step
         self.stream = torch.cuda.Stream()
         self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):  # warm-up: allocations, MIOpen / hipBLASLt plans, side streams
@@ -276,6 +295,7 @@ class GraphedStep:
         with torch.cuda.graph(self.g1, stream=self.stream):
             self.out = step.forward_backward(*inputs)
             if not comm:
+                step.communicate()  # (no-op without hooks; RCCL collectives captured as graph nodes otherwise)
                 step.apply()
         self.g2 = None
         if comm:

@@ -87,10 +87,12 @@ def _hensman_setup(L=4, M=40, T=16, P=32):
     return la, img, mask, X, z, batches, eps
 
 
-def test_rccl_world1_graphed_hensman_two_graphs(hip):
-    """The data-parallel Hensman step replayed as TWO HIP graphs with the RCCL all-reduces between
-    them (GradAllReduce of the Adam gradients, SUM all-reduce of the natural-gradient directions:
-    GraphedStep's comm path) against the eager single-process step, step after step."""
+@pytest.mark.parametrize("capture_comm", [False, True])
+def test_rccl_world1_graphed_hensman_two_graphs(hip, capture_comm):
+    """The data-parallel Hensman step replayed as HIP graphs with the RCCL all-reduces (GradAllReduce of the Adam
+    gradients, SUM all-reduce of the natural-gradient directions: GraphedStep's comm path) -- as TWO graphs around
+    the eager collectives, and (capture_comm) as ONE graph with the collectives captured -- against the eager
+    single-process step, step after step."""
     from lvae_amd.distributed import GradAllReduce, allreduce_tensors
     from lvae_amd.steps import GraphedStep, HensmanStep
     from lvae_amd.vae import ConvVAE
@@ -122,8 +124,8 @@ def test_rccl_world1_graphed_hensman_two_graphs(hip):
         with _NcclWorld1():
             graph_step, k0_g = make(True)
             s = (img[batches[0]].clone(), mask[batches[0]].clone(), X[batches[0]].clone(), eps)
-            g = GraphedStep(graph_step, s, warmup=1)
-            assert g.comm and g.g2 is not None
+            g = GraphedStep(graph_step, s, warmup=1, capture_comm=capture_comm)
+            assert (g.g2 is None) == capture_comm
             outs_g = []
             for b in batches:
                 torch.index_select(img, 0, b, out=s[0])
@@ -178,11 +180,11 @@ def test_rccl_world1_two_graphs_back_to_back(hip):
                       ng_reduce=lambda ts: allreduce_tensors(ts, average=False))
         return HensmanStep(vae, k0, k1, lik, opt, m, H, z, P, T, **kw), k0
 
-    def graphed(comm):
+    def graphed(comm, capture=False):
         step, k0 = make(comm)
         s = (img[batches[0]].clone(), mask[batches[0]].clone(), X[batches[0]].clone(), eps)
-        g = GraphedStep(step, s, warmup=1)
-        assert (g.g2 is not None) == comm
+        g = GraphedStep(step, s, warmup=1, capture_comm=capture)
+        assert (g.g2 is not None) == (comm and not capture)
         for i in range(n_steps):
             b = batches[i % len(batches)]
             torch.index_select(img, 0, b, out=s[0])
