@@ -398,11 +398,20 @@ def run_closed(args, world, rank, dev):
     sync_barrier(world)
     if clocks:
         clocks.__enter__()
+    # LVAE_BENCH_CPROFILE=path: the host side (Python) of the timed steps under cProfile (scripts/gpu_host_prof.sh)
+    cprof_path = os.environ.get("LVAE_BENCH_CPROFILE")
+    if cprof_path and rank == 0:
+        import cProfile
+        cprof = cProfile.Profile()
+        cprof.enable()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = run()
     sync_barrier(world)
     elapsed = time.perf_counter() - t0
+    if cprof_path and rank == 0:
+        cprof.disable()
+        cprof.dump_stats(cprof_path)
     if clocks:
         clocks.__exit__(None, None, None)
     if use_graph:

@@ -35,6 +35,8 @@
 #include "prof.hpp"
 #include "x3_c16.hpp"  // c16_off: the chunk-major Y / Y^T planes
 
+#include <atomic>
+
 
 #ifndef LVAE_ALPHA_WG
 #define LVAE_ALPHA_WG 4096
@@ -104,7 +106,7 @@ struct KLWorkspace {
   double* ypart;     // early reduce: [2][L][nt][np] fp64 partials of the triangular mat-vecs over the Y planes
   double* yvec;      // early reduce: [L][np] t = Y mu, then u = Y r
   double* K64e;      // early reduce: the refinement's fp64 K (the Y^T planes are still needed by the late lauum)
-  size_t bytes;
+  size_t bytes, bytes_base;
   KLWorkspace(char* base, int np_, int L) {
     size_t off = 0;
     auto take = [&](size_t b) {
@@ -138,6 +140,7 @@ struct KLWorkspace {
     hbon = base ? reinterpret_cast<const int*>(kl_hyper_dev(hb, np_, L)) : nullptr;  // (HbDev::on: its first member)
     rest = (double*)take((size_t)L * sizeof(double));
     rflag = (int*)take((size_t)L * sizeof(int));
+    bytes_base = off;  // (the early reduce's buffers below: sized only when it is on, lvae_kl_closed_workspace_size)
     ypart = (double*)take(2 * (size_t)L * (np_ / 256) * np_ * sizeof(double));
     yvec = (double*)take((size_t)L * np_ * sizeof(double));
     K64e = (double*)take(kl_refine_bytes(np_, L));
@@ -384,6 +387,12 @@ extern "C" {
 
 int lvae_kl_closed_padded_n(int n) { return ((n + 255) / 256) * 256; }
 
+static bool kl_early_env() {
+  const char* e = getenv("LVAE_KL_EARLY");
+  return e && atoi(e) != 0;
+}
+static std::atomic<bool> g_kl_early_sized{false};  // LVAE_KL_EARLY at the last workspace-size query
+
 // (kl_hyper.hip's state query: where the workspace keeps the binned hyper-gradient's region)
 size_t kl_hyper_offset_in_kl_ws(int np_, int L) {
   char* const fake = reinterpret_cast<char*>(uintptr_t(1) << 20);  // (offsets only: any aligned base)
@@ -393,7 +402,12 @@ size_t kl_hyper_offset_in_kl_ws(int np_, int L) {
 
 size_t lvae_kl_closed_workspace_size(int n, int L) {
   const int np_ = lvae_kl_closed_padded_n(n);
-  return KLWorkspace(nullptr, np_, L).bytes;
+  const KLWorkspace ws(nullptr, np_, L);
+  // the early reduce's buffers (the workspace's tail, ~0.3-0.6 GB) only when LVAE_KL_EARLY is on at this call; the
+  // decision is kept for the calls on the workspace sized here (kl_early)
+  const bool early = kl_early_env();
+  g_kl_early_sized.store(early);
+  return early ? ws.bytes : ws.bytes_base;
 }
 
 int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int ldx, int n, int L,
@@ -452,12 +466,9 @@ int lvae_kl_closed_factor_f32(const lvae_kernel_spec* spec, const double* x, int
 // Measured (r6, same box, headline step): d kl / d (mu, log v) 0.7 ms earlier, but the step 9.32-9.37 vs 9.20-9.25
 // ms: the encoder backward then runs beside lauum + the slab pass, whose grids hold every CU, and the four
 // mat-vec passes (~0.45 ms) add to a step that is bound by its total GPU work (profiles/r6_kl_early_ab.txt).
-// Read per call (tests compare both routes in one process); the forward and the backward of one KL must see the
-// same value.
-static bool kl_early(int np_, int L) {
-  const char* e = getenv("LVAE_KL_EARLY");
-  return e && atoi(e) != 0 && ci_pipe_mode_of(np_, L) == 0;
-}
+// The variable is read when the workspace is sized (tests compare both routes in one process) and that decision
+// holds for the forward and the backward on it: the early buffers exist only in a workspace sized with it on.
+static bool kl_early(int np_, int L) { return g_kl_early_sized.load() && ci_pipe_mode_of(np_, L) == 0; }
 
 // t = Y x (lower) or a = base + Y^T x (upper, + the row sums of squares of Y^T: diag K^-1 into sumsq)
 static void kl_ymv(const KLWorkspace& ws, const float* ysc, int np_, int L, bool upper, const double* x,
