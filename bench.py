@@ -407,6 +407,7 @@ def run_closed(args, world, rank, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = run()
+    t_enq = time.perf_counter() - t0  # (host enqueue of all steps; the GPU drains the rest below)
     sync_barrier(world)
     elapsed = time.perf_counter() - t0
     if cprof_path and rank == 0:
@@ -453,6 +454,9 @@ def run_closed(args, world, rank, dev):
                                       f"split {N // world}/rank, 1 all-gather + 2 all-reduces per step")}}
     if clocks and clocks.record():
         res["clock"] = clocks.record()
+    # host-side pacing: the loop's host time per step, and the queued GPU work left when the host finished (a
+    # drain of about one step or less: the host, not the GPU, paced the loop)
+    res["host"] = {"enqueue_ms_per_step": 1000.0 * t_enq / args.steps, "drain_ms": 1000.0 * (elapsed - t_enq)}
     if phase and Lr > 0:
         np_ = _lib.load().lvae_kl_closed_padded_n(N)
         potrf_ms = phase["potrf"][0] / args.steps
