@@ -319,6 +319,12 @@ int lvae_relu_maxpool2_bias_bwd_f32(const float* gy, const float* y, const uint8
  * output is never written.                                                                      */
 int lvae_conv1_relu_maxpool2_fwd_f32(const float* x, const float* w, const float* bias, int N, int C, int H, int W,
                                      float* y, uint8_t* idx, void* stream);
+/* The second encoder conv end to end (VAE.py:48-50): x [N, Cin, H, W], w [C, Cin, 3, 3], bias [C], padding 1 ->
+ * y = max_pool2d(relu(conv(x) + bias), 2, 2) and idx as above, in one pass (no full-resolution output, no
+ * layout transposes).  Cin == 16, H == W == 18 (the 36 x 36 images after the first pool), C % 16 == 0; -3 for
+ * other shapes (conv + lvae_relu_maxpool2_bias_fwd_f32 cover them).                             */
+int lvae_conv3x3_relu_maxpool2_fwd_f32(const float* x, const float* w, const float* bias, int N, int Cin, int C, int H,
+                                       int W, float* y, uint8_t* idx, void* stream);
 /* Weight and bias gradients of a 3x3 / stride-1 / padding-1 conv followed by the fused relu + pool
  * (the encoder convs), from the pooled gradient: dw [C, Cin, 3, 3] and db [C] as sums over the
  * pooled outputs of g * (the 3x3 input patch at the window's argmax) -- the full-resolution
@@ -345,6 +351,17 @@ int lvae_deconv2_sigmoid_fwd_f32(const float* z, const float* w, const float* bi
                                  float* out, void* stream);
 int lvae_deconv2_sigmoid_bwd_f32(const float* g, const float* out, const float* z, const float* w, int N, int Cin,
                                  int Hi, int Wi, float* gz, float* dw, float* db, void* workspace, void* stream);
+/* ConvVAE decoder's first transposed conv (VAE.py:73, 122): y = relu(ConvTranspose2d(Cin, Cout, 4, stride 2,
+ * padding 1)(x) + bias), x [N, Cin, Hi, Wi], w [Cin, Cout, 4, 4], bias [Cout] -> y [N, Cout, 2Hi, 2Wi] (relu:
+ * v < 0 -> 0, NaN kept).  Backward from gy = dLoss/dy and the saved y (mask y > 0): dx [N, Cin, Hi, Wi],
+ * dw [Cin, Cout, 4, 4], db [Cout] in one pass + a fixed-order partial sum (deterministic; workspace:
+ * lvae_deconv4s2_relu_bwd_workspace_size bytes).  Cin == 32, Cout == 16, Hi == Wi == 9; -3 otherwise.       */
+int lvae_deconv4s2_relu_fwd_f32(const float* x, const float* w, const float* bias, int N, int Cin, int Cout, int Hi,
+                                int Wi, float* y, void* stream);
+size_t lvae_deconv4s2_relu_bwd_workspace_size(int N, int Cin, int Cout);
+int lvae_deconv4s2_relu_bwd_f32(const float* gy, const float* y, const float* x, const float* w, int N, int Cin,
+                                int Cout, int Hi, int Wi, float* dx, float* dw, float* db, void* workspace,
+                                void* stream);
 
 /* GP posterior mean of the latents at test covariates (utils.py:115-211 batch_predict_varying_T,
  * called by MSE_test_GPapprox, model_test.py:85-143).  Prediction set laid out [P, T] by subject

@@ -584,6 +584,529 @@ __global__ __launch_bounds__(512) void conv3x3_pool_dgrad2_kernel(const float* _
   for (int c = 0; c < CI; ++c) *reinterpret_cast<vo_f32x2*>(gxn + (int64_t)c * H * W) = acc[c];
 }
 
+// ---- The second encoder conv end to end (VAE.py:48-50): conv3x3 (padding 1, CI input channels) + bias + relu +
+// 2x2 max pool, C = 16 k output channels, H = W input, in one pass.  Replaces MIOpen's conv (an implicit GEMM over
+// NHWC: NCHW -> NHWC transposes of the input and the weights and one back for its output) and
+// relu_maxpool2_bias_fwd's pass over the full-resolution output (written and read once: 170 MB at 4096 images).
+// IPB images per block are staged in LDS with a zero border.  Work item = (image, pooled position, group of 16
+// output channels); 64 consecutive items of a wave share the group, so W's addresses are uniform across the wave
+// (scalar loads, broadcast into the packed FMAs).  An item reads the 4 x 4 input patch under its window once per
+// input channel and keeps the window's 2 x 2 conv outputs of its 16 channels in packed accumulators (a window row's
+// two columns in one pair): per output sum_ci sum_ky sum_kx x w (this order) + b, then relu + first strict maximum
+// (scan order) exactly as relu_maxpool2_bias_fwd_kernel.
+template <int CI, int H, int IPB>
+__global__ __launch_bounds__(256) void conv3x3_relu_pool_fwd_kernel(const float* __restrict__ x,
+                                                                    const float* __restrict__ w,
+                                                                    const float* __restrict__ bias, int N, int C,
+                                                                    float* __restrict__ y, uint8_t* __restrict__ idx) {
+  constexpr int W = H, Wp = W + 2, HWp = (H + 2) * Wp, Ho = H / 2, Wo = W / 2, P = Ho * Wo, HW = H * W;
+  __shared__ float xl[IPB * CI * HWp];
+  const int t = threadIdx.x, n0 = blockIdx.x * IPB, ni = min(IPB, N - n0);
+  for (int e = t; e < IPB * CI * HWp; e += 256) xl[e] = 0.f;
+  __syncthreads();
+  const float* xb = x + (int64_t)n0 * CI * HW;
+  for (int e = t; e < ni * CI * HW; e += 256) {
+    const int pl = e / HW, r = e - pl * HW, rr = r / W;
+    xl[pl * HWp + (rr + 1) * Wp + (r - rr * W) + 1] = xb[e];
+  }
+  __syncthreads();
+  const int ntask = ni * P, nchunk = (ntask + 63) >> 6, ngrp = C >> 4, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform: W's loads scalar)
+  for (int ch = wave; ch < nchunk * ngrp; ch += 4) {
+    const int grp = ch % ngrp, task = (ch / ngrp) * 64 + lane;
+    const int tk = task < ntask ? task : ntask - 1;
+    const int img = tk / P, r = tk - img * P, i = r / Wo, j = r - i * Wo;
+    const float* xp = xl + img * CI * HWp + 2 * i * Wp + 2 * j;  // padded (2 i, 2 j) = input (2 i - 1, 2 j - 1)
+    const float* wg = w + (int64_t)grp * 16 * CI * 9;
+    vo_f32x2 acc[16][2];
+#pragma unroll
+    for (int co = 0; co < 16; ++co) acc[co][0] = acc[co][1] = vo_f32x2{0.f, 0.f};
+    for (int ci = 0; ci < CI; ++ci) {
+      const float* xc = xp + ci * HWp;
+      float p[4][4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) p[a][b] = xc[a * Wp + b];
+#pragma unroll
+      for (int co = 0; co < 16; ++co) {
+        const float* wc = wg + (co * CI + ci) * 9;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const float wv = wc[3 * ky + kx];
+            acc[co][0] = __builtin_elementwise_fma(vo_f32x2{p[ky][kx], p[ky][kx + 1]}, vo_f32x2{wv, wv}, acc[co][0]);
+            acc[co][1] =
+                __builtin_elementwise_fma(vo_f32x2{p[ky + 1][kx], p[ky + 1][kx + 1]}, vo_f32x2{wv, wv}, acc[co][1]);
+          }
+      }
+    }
+    if (task < ntask) {
+#pragma unroll
+      for (int co = 0; co < 16; ++co) {
+        const int c = grp * 16 + co;
+        const float bc = bias[c];
+        float m = acc[co][0][0] + bc;
+        uint8_t k = 0;
+        if (acc[co][0][1] + bc > m) m = acc[co][0][1] + bc, k = 1;
+        if (acc[co][1][0] + bc > m) m = acc[co][1][0] + bc, k = 2;
+        if (acc[co][1][1] + bc > m) m = acc[co][1][1] + bc, k = 3;
+        const int64_t o = ((int64_t)(n0 + img) * C + c) * P + r;
+        y[o] = m > 0.f ? m : 0.f;
+        idx[o] = k;
+      }
+    }
+  }
+}
+
+// ---- The decoder's first transposed conv (VAE.py:73, 122): relu(ConvTranspose2d(CI, CO, 4, stride 2, padding 1)(x)
+// + b), x [N, CI, HI, HI] -> [N, CO, 2 HI, 2 HI], in one pass (MIOpen's transposed conv with its transposes, then
+// bias_relu_fwd, before).  Output (2 iy + a, 2 ix + b) takes input rows iy, iy - 1 (a = 0: ky 1, 3) or iy + 1, iy
+// (a = 1: ky 0, 2), columns likewise: 4 taps per input channel (deconv2_sigmoid_fwd_kernel's indexing).  IPB images
+// per block in LDS with a zero border; item = (image, input position, group of 8 output channels), the group
+// uniform across a wave (W's row of 16 taps per (ci, co) by scalar loads); the item's 2 x 2 output block of its 8
+// channels in packed accumulators (the two columns of an output row in one pair).  relu as bias_relu_fwd: v < 0 ->
+// 0, NaN kept.
+template <int CI, int CO, int HI, int IPB>
+__global__ __launch_bounds__(256) void deconv4s2_relu_fwd_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ bias, int N,
+                                                                 float* __restrict__ y) {
+  constexpr int Wp = HI + 2, HWp = (HI + 2) * Wp, P = HI * HI, Wo = 2 * HI, PO = 4 * P, NG = CO / 8;
+  __shared__ float xl[IPB * CI * HWp];
+  const int t = threadIdx.x, n0 = blockIdx.x * IPB, ni = min(IPB, N - n0);
+  for (int e = t; e < IPB * CI * HWp; e += 256) xl[e] = 0.f;
+  __syncthreads();
+  const float* xb = x + (int64_t)n0 * CI * P;
+  for (int e = t; e < ni * CI * P; e += 256) {
+    const int pl = e / P, r = e - pl * P, rr = r / HI;
+    xl[pl * HWp + (rr + 1) * Wp + (r - rr * HI) + 1] = xb[e];
+  }
+  __syncthreads();
+  const int ntask = ni * P, nchunk = (ntask + 63) >> 6, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform: W's loads scalar)
+  for (int ch = wave; ch < nchunk * NG; ch += 4) {
+    const int grp = ch % NG, task = (ch / NG) * 64 + lane;
+    const int tk = task < ntask ? task : ntask - 1;
+    const int img = tk / P, q = tk - img * P, iy = q / HI, ix = q - iy * HI;
+    const float* xp = xl + img * CI * HWp + iy * Wp + ix;  // padded (iy, ix) = input (iy - 1, ix - 1)
+    vo_f32x2 acc[8][2];
+#pragma unroll
+    for (int co = 0; co < 8; ++co) acc[co][0] = acc[co][1] = vo_f32x2{0.f, 0.f};
+    for (int ci = 0; ci < CI; ++ci) {
+      const float* xc = xp + ci * HWp;
+      float v[3][3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[u][c] = xc[u * Wp + c];
+#pragma unroll
+      for (int co = 0; co < 8; ++co) {
+        const float* wc = w + ((int64_t)ci * CO + grp * 8 + co) * 16;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int ky = a == 0 ? 1 + 2 * u : 2 * u, ry = a == 0 ? 1 - u : 2 - u;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)  // b = 0: (kx 1 + 2 c, col 1 - c); b = 1: (kx 2 c, col 2 - c)
+              acc[co][a] = __builtin_elementwise_fma(vo_f32x2{v[ry][1 - c], v[ry][2 - c]},
+                                                     vo_f32x2{wc[ky * 4 + 1 + 2 * c], wc[ky * 4 + 2 * c]}, acc[co][a]);
+          }
+      }
+    }
+    if (task < ntask) {
+#pragma unroll
+      for (int co = 0; co < 8; ++co) {
+        const int c = grp * 8 + co;
+        const float bc = bias[c];
+        float* yo = y + ((int64_t)(n0 + img) * CO + c) * PO + (2 * iy) * Wo + 2 * ix;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          vo_f32x2 r2 = acc[co][a] + vo_f32x2{bc, bc};
+          r2[0] = r2[0] < 0.f ? 0.f : r2[0];
+          r2[1] = r2[1] < 0.f ? 0.f : r2[1];
+          *reinterpret_cast<vo_f32x2*>(yo + a * Wo) = r2;
+        }
+      }
+    }
+  }
+}
+
+// Its backward from d y and y: g = d y [y > 0] (act_bwd's mask: y <= 0 -> 0), then in one pass per block of `per`
+// images (IPB at a time in LDS: g with a zero border, x):
+//   dx[ci][iy][ix] = sum_co sum_{ky,kx} W[ci][co][ky][kx] g[co][2 iy - 1 + ky][2 ix - 1 + kx]   (written per image)
+//   dW[ci][co][ky][kx] = sum_n sum_{iy,ix} x[ci][iy][ix] g[co][2 iy - 1 + ky][2 ix - 1 + kx]     (block partials)
+//   db[co] = sum g                                                                                (block partials)
+// dx items = (image, input position, group of 8 input channels), the group uniform across a wave (W by scalar
+// loads), two channels per packed FMA.  dW: thread (co = t & 15, ci 4 ((t >> 4) & 7) + 0..3, position parity
+// t >> 7) keeps its 4 x 16 taps in packed accumulators over the block's images (tap pairs per FMA); the two
+// parities are separate partial rows.  Partials part[2 block + parity][CI CO 16 + CO], summed in a fixed order by
+// wgrad_sum_kernel: deterministic.  Replaces act_bwd (mask + bias sum), MIOpen's backward-data and backward-weights
+// convs and their five NCHW <-> NHWC transposes.
+template <int CI, int CO, int HI, int IPB>
+__global__ __launch_bounds__(256) void deconv4s2_relu_bwd_kernel(const float* __restrict__ gy,
+                                                                 const float* __restrict__ y,
+                                                                 const float* __restrict__ x,
+                                                                 const float* __restrict__ w, int N, int per,
+                                                                 float* __restrict__ dx, float* __restrict__ part) {
+  static_assert(CI == 32 && CO == 16, "the dW thread map: 16 output x 8 groups of 4 input channels x 2 parities");
+  constexpr int P = HI * HI, Wo = 2 * HI, PO = 4 * P, Gp = Wo + 2, GP = ((2 * HI + 2) * Gp) | 1, NG = CI / 8;
+  __shared__ float gl[IPB * CO * GP];  // (odd plane stride: the 16 co lanes of a dW read hit distinct banks)
+  __shared__ float xs[IPB * CI * P];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // (uniform: W's loads scalar)
+  const int wco = t & 15, wcg = (t >> 4) & 7, par = t >> 7;
+  const int nb0 = blockIdx.x * per, nb1 = min(N, nb0 + per);
+  for (int e = t; e < IPB * CO * GP; e += 256) gl[e] = 0.f;  // (the borders stay zero: each group rewrites the interior)
+  vo_f32x2 dacc[4][8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dacc[k][p] = vo_f32x2{0.f, 0.f};
+  float bacc = 0.f;
+  for (int g0 = nb0; g0 < nb1; g0 += IPB) {
+    const int ni = min(IPB, nb1 - g0);
+    __syncthreads();  // the previous group's readers are done
+    const int64_t ob = (int64_t)g0 * CO * PO;
+    for (int e = t; e < ni * CO * PO; e += 256) {
+      const int pl = e / PO, r = e - pl * PO, rr = r / Wo;
+      const float yv = y[ob + e], gv = gy[ob + e];
+      gl[pl * GP + (rr + 1) * Gp + (r - rr * Wo) + 1] = yv <= 0.f ? 0.f : gv;
+    }
+    const float* xb = x + (int64_t)g0 * CI * P;
+    for (int e = t; e < ni * CI * P; e += 256) xs[e] = xb[e];
+    __syncthreads();
+    // dx
+    const int ntask = ni * P, nchunk = (ntask + 63) >> 6;
+    for (int ch = wave; ch < nchunk * NG; ch += 4) {
+      const int grp = ch % NG, task = (ch / NG) * 64 + lane;
+      const int tk = task < ntask ? task : ntask - 1;
+      const int img = tk / P, q = tk - img * P, iy = q / HI, ix = q - iy * HI;
+      const float* gp = gl + img * CO * GP + (2 * iy) * Gp + 2 * ix;  // padded (2 iy, 2 ix) = (2 iy - 1, 2 ix - 1)
+      vo_f32x2 xa[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xa[k] = vo_f32x2{0.f, 0.f};
+      for (int co = 0; co < CO; ++co) {
+        float pt[16];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) pt[4 * a + c] = gp[co * GP + a * Gp + c];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float* w0 = w + ((int64_t)(grp * 8 + 2 * k) * CO + co) * 16;  // W[ci][co][:], W[ci + 1][co][:]
+#pragma unroll
+          for (int tp = 0; tp < 16; ++tp)
+            xa[k] = __builtin_elementwise_fma(vo_f32x2{pt[tp], pt[tp]}, vo_f32x2{w0[tp], w0[CO * 16 + tp]}, xa[k]);
+        }
+      }
+      if (task < ntask) {
+        float* dxo = dx + ((int64_t)(g0 + img) * CI + grp * 8) * P + q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dxo[(2 * k) * P] = xa[k][0];
+          dxo[(2 * k + 1) * P] = xa[k][1];
+        }
+      }
+    }
+    // dW, db
+    for (int img = 0; img < ni; ++img) {
+      const float* xi = xs + (img * CI + 4 * wcg) * P;
+      const float* gi = gl + (img * CO + wco) * GP;
+      for (int q = par; q < P; q += 2) {
+        const int iy = q / HI, ix = q - iy * HI;
+        float pt[16];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) pt[4 * a + c] = gi[(2 * iy + a) * Gp + 2 * ix + c];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float xv = xi[k * P + q];
+#pragma unroll
+          for (int p = 0; p < 8; ++p)
+            dacc[k][p] = __builtin_elementwise_fma(vo_f32x2{pt[2 * p], pt[2 * p + 1]}, vo_f32x2{xv, xv}, dacc[k][p]);
+        }
+      }
+      if (wcg == 0)
+        for (int r = par; r < PO; r += 2) {
+          const int rr = r / Wo;
+          bacc += gi[(rr + 1) * Gp + (r - rr * Wo) + 1];
+        }
+    }
+  }
+  constexpr int M = CI * CO * 16 + CO;
+  float* pb = part + (int64_t)(2 * blockIdx.x + par) * M;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float* pw = pb + ((4 * wcg + k) * CO + wco) * 16;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) *reinterpret_cast<vo_f32x2*>(pw + 2 * p) = dacc[k][p];
+  }
+  if (wcg == 0) pb[CI * CO * 16 + wco] = bacc;
+}
+
+// The same backward on the f32 MFMA (v_mfma_f32_32x32x2_f32: a k-ordered f32 fma chain, the VALU's numerics at
+// 2.3x its practical rate).  One image at a time in LDS: g (masked, zero border), x (positions padded to 96 with
+// zeros), and W^T [k = 16 co + tap][ci] loaded once per block.  With G [k][pos] = g[co][2 iy - 1 + ky][2 ix - 1 + kx]
+// (the im2col of g, gathered from LDS straight into the MFMA operands):
+//   dx^T [pos][ci] = sum_k G^T [pos][k] W^T [k][ci]   -- 3 tiles of 32 positions (81 valid), K = 256: waves 0..2;
+//   dW [ci][k]     = sum_pos x [ci][pos] G^T [pos][k] -- 8 tiles of 32 k, K = the positions of all the block's
+//                    images (accumulated in registers): one tile on each of waves 0..2, five on wave 3.
+// Per image 169 MFMAs on waves 0..2 and 205 on wave 3.  db from the staged g (16 pixel slices per channel, summed in
+// a fixed order at the end).  Block partials part[block][CI CO 16 + CO], wgrad_sum_kernel as before.
+typedef float vo_f32x16 __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void deconv4s2_relu_bwd_mfma_kernel(const float* __restrict__ gy,
+                                                                      const float* __restrict__ y,
+                                                                      const float* __restrict__ x,
+                                                                      const float* __restrict__ w, int N, int per,
+                                                                      float* __restrict__ dx, float* __restrict__ part) {
+  constexpr int CI = 32, CO = 16, HI = 9, P = HI * HI, Wo = 2 * HI, PO = 4 * P, Gp = Wo + 2;
+  constexpr int GP = ((2 * HI + 2) * Gp) | 1;  // (odd plane stride)
+  constexpr int XS = 97;                       // x plane stride: >= 82 positions, odd (the 32 ci lanes: distinct banks)
+  constexpr int K = CO * 16;
+  __shared__ float gl[CO * GP];
+  __shared__ float xs[CI * XS];
+  __shared__ float wt[K * CI];  // W^T [k][ci]
+  __shared__ float red[256];
+  const int t = threadIdx.x, lane = t & 63, l32 = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nb0 = blockIdx.x * per, nb1 = min(N, nb0 + per);
+  for (int e = t; e < CO * GP; e += 256) gl[e] = 0.f;
+  for (int e = t; e < CI * XS; e += 256) xs[e] = 0.f;
+  for (int e = t; e < K * CI; e += 256) {  // w [ci][k] -> wt [k][ci]
+    const int ci = e / K, k = e - ci * K;
+    wt[k * CI + ci] = w[e];
+  }
+  vo_f32x16 dwacc[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dwacc[j][r] = 0.f;
+  const int ntile = wave == 3 ? 5 : 1, tile0 = wave == 3 ? 3 : wave;
+  float bacc = 0.f;
+  const int bco = t & 15, bsl = t >> 4;
+  // the next image's y, d y and x in registers, loaded under the current image's MFMAs
+  constexpr int NG = (CO * PO + 255) / 256, NX = (CI * P + 255) / 256;
+  float pg[NG], px[NX];
+  auto fetch = [&](int n) {
+    const int64_t ob = (int64_t)n * CO * PO;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int e = t + 256 * k;
+      if (e < CO * PO) {
+        const float yv = y[ob + e], gv = gy[ob + e];
+        pg[k] = yv <= 0.f ? 0.f : gv;
+      }
+    }
+    const float* xn = x + (int64_t)n * CI * P;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const int e = t + 256 * k;
+      if (e < CI * P) px[k] = xn[e];
+    }
+  };
+  if (nb0 < nb1) fetch(nb0);
+  for (int n = nb0; n < nb1; ++n) {
+    __syncthreads();  // the previous image's readers are done (and the zeroing / W^T staged)
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int e = t + 256 * k;
+      if (e < CO * PO) {
+        const int co = e / PO, r = e - co * PO, rr = r / Wo;
+        gl[co * GP + (rr + 1) * Gp + (r - rr * Wo) + 1] = pg[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const int e = t + 256 * k;
+      if (e < CI * P) {
+        const int ci = e / P;
+        xs[ci * XS + (e - ci * P)] = px[k];
+      }
+    }
+    if (n + 1 < nb1) fetch(n + 1);
+    __syncthreads();
+    for (int r = bsl; r < PO; r += 16) {  // db: channel bco, pixel slice bsl
+      const int rr = r / Wo;
+      bacc += gl[bco * GP + (rr + 1) * Gp + (r - rr * Wo) + 1];
+    }
+    // dW: K = this image's positions, 2 per step (pos 81 of the last step: x is 0 there)
+#pragma unroll 2
+    for (int s = 0; s < (P + 1) / 2; ++s) {
+      const int pos = 2 * s + hi, pc = pos < P ? pos : P - 1, iy = pc / HI, ix = pc - iy * HI;
+      const float a = xs[l32 * XS + pos];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        if (j < ntile) {
+          const int kk = (tile0 + j) * 32 + l32, co = kk >> 4, ky = (kk >> 2) & 3, kx = kk & 3;
+          const float b = gl[co * GP + (2 * iy + ky) * Gp + 2 * ix + kx];
+          dwacc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, pos < P ? b : 0.f, dwacc[j], 0, 0, 0);
+        }
+      }
+    }
+    // dx: waves 0..2, positions 32 wave + 0..31
+    if (wave < 3) {
+      const int pos = 32 * wave + l32, pv = pos < P, pc = pv ? pos : P - 1, iy = pc / HI, ix = pc - iy * HI;
+      const float* gq = gl + (2 * iy) * Gp + 2 * ix;
+      vo_f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll 4
+      for (int s = 0; s < K / 2; ++s) {
+        const int k = 2 * s + hi, co = k >> 4, ky = (k >> 2) & 3, kx = k & 3;
+        const float a = gq[co * GP + ky * Gp + kx];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pv ? a : 0.f, wt[k * CI + l32], acc, 0, 0, 0);
+      }
+      float* dxn = dx + (int64_t)n * CI * P + l32 * P;  // column = ci (the lane), rows = positions
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pr = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (pr < P) dxn[pr] = acc[r];
+      }
+    }
+  }
+  constexpr int M = CI * K + CO;
+  float* pb = part + (int64_t)blockIdx.x * M;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    if (j < ntile) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = (r & 3) + 8 * (r >> 2) + 4 * hi;
+        pb[ci * K + (tile0 + j) * 32 + l32] = dwacc[j][r];
+      }
+    }
+  }
+  red[t] = bacc;
+  __syncthreads();
+  if (t < CO) {
+    float s = 0.f;
+    for (int sl = 0; sl < 16; ++sl) s += red[sl * 16 + t];
+    pb[CI * K + t] = s;
+  }
+}
+
+// The second encoder conv's weight and bias gradients on the f32 MFMA (v_mfma_f32_16x16x4_f32), dense over the
+// routed full-resolution gradient g0 (gy at each window's argmax where y > 0, 0 at the other three positions):
+//   dW [co][k = 9 ci + 3 ky + kx] = sum_n sum_pos g0[co][pos] x[ci][pos + (ky - 1, kx - 1)],  db[co] = sum g0.
+// conv3x3_pool_wgrad_kernel reads one x patch per nonzero g0 with no reuse (LDS-bound: one read per FMA); here
+// every operand read feeds 16 MACs and the 3 zeros of a window ride along (4x the MACs at 2.3x the rate, a fraction
+// of the LDS traffic).  Per image in LDS: g0 [co][324] and x with a zero border; the next image's pooled gradient,
+// y, idx and x prefetched into registers under the MFMAs.  Every wave owns all 2 x 9 tiles (16 co x 16 k) over its
+// quarter of the positions (steps of 4, s = wave mod 4): 2 A reads + 9 B gathers per 18 MFMAs, no branches; the
+// four quarters are separate partial rows.  Partials part[4 block + wave][C 144 + C] (conv3x3_pool_wgrad_kernel's
+// row layout), summed in a fixed order by wgrad_sum_kernel.
+__global__ __launch_bounds__(256) void conv3x3_pool_wgrad_mfma_kernel(const float* __restrict__ gy,
+                                                                      const float* __restrict__ y,
+                                                                      const uint8_t* __restrict__ idx,
+                                                                      const float* __restrict__ x, int N, int per,
+                                                                      float* __restrict__ part) {
+  constexpr int CI = 16, C = 32, H = 18, W = 18, Ho = 9, Wo = 9, P = Ho * Wo, PF = H * W, Wp = W + 2;
+  constexpr int XP = ((H + 2) * Wp) | 1, GS = PF | 1, K2 = CI * 9, NT = K2 / 16;
+  __shared__ float g0[C * GS];
+  __shared__ float xl[CI * XP];
+  __shared__ float red[256];
+  const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, kq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nb0 = blockIdx.x * per, nb1 = min(N, nb0 + per);
+  for (int e = t; e < CI * XP; e += 256) xl[e] = 0.f;  // (the border stays zero)
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t acc[2][NT];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[m][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // B gather offsets (k = 16 j + l16 -> ci, ky, kx): padded (a + ky, b + kx) of plane ci
+  int boff[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int k = 16 * j + l16, ci = k / 9, r9 = k - 9 * ci;
+    boff[j] = ci * XP + (r9 / 3) * Wp + (r9 % 3);
+  }
+  float bacc = 0.f;
+  const int bco = t & 31, bsl = t >> 5;
+  constexpr int NGP = (C * P + 255) / 256, NXP = (CI * PF + 255) / 256;
+  float pg[NGP], px[NXP];
+  int pk[NGP];
+  auto fetch = [&](int n) {
+    const int64_t ob = (int64_t)n * C * P;
+#pragma unroll
+    for (int k = 0; k < NGP; ++k) {
+      const int e = t + 256 * k;
+      if (e < C * P) {
+        const float yv = y[ob + e], gv = gy[ob + e];
+        pg[k] = yv > 0.f ? gv : 0.f;
+        pk[k] = idx[ob + e];
+      }
+    }
+    const float* xn = x + (int64_t)n * CI * PF;
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) {
+      const int e = t + 256 * k;
+      if (e < CI * PF) px[k] = xn[e];
+    }
+  };
+  if (nb0 < nb1) fetch(nb0);
+  for (int n = nb0; n < nb1; ++n) {
+    __syncthreads();  // the previous image's readers are done (and the zeroing)
+#pragma unroll
+    for (int k = 0; k < NGP; ++k) {
+      const int e = t + 256 * k;
+      if (e < C * P) {
+        const int co = e / P, r = e - co * P, i = r / Wo, j = r - i * Wo;
+        float* q = g0 + co * GS + (2 * i) * W + 2 * j;
+        q[0] = pk[k] == 0 ? pg[k] : 0.f;
+        q[1] = pk[k] == 1 ? pg[k] : 0.f;
+        q[W] = pk[k] == 2 ? pg[k] : 0.f;
+        q[W + 1] = pk[k] == 3 ? pg[k] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) {
+      const int e = t + 256 * k;
+      if (e < CI * PF) {
+        const int ci = e / PF, r = e - ci * PF, rr = r / W;
+        xl[ci * XP + (rr + 1) * Wp + (r - rr * W) + 1] = px[k];
+      }
+    }
+    if (n + 1 < nb1) fetch(n + 1);
+    __syncthreads();
+    for (int r = bsl; r < PF; r += 8) bacc += g0[bco * GS + r];  // db: channel bco, slice bsl
+#pragma unroll 2
+    for (int s = wave; s < PF / 4; s += 4) {
+      const int pos = 4 * s + kq, a = pos / W, b = pos - a * W;
+      const float a0 = g0[l16 * GS + pos], a1 = g0[(16 + l16) * GS + pos];
+      const float* xb = xl + a * Wp + b;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const float bv = xb[boff[j]];
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc[1][j], 0, 0, 0);
+      }
+    }
+  }
+  constexpr int M = C * K2 + C;
+  float* pb = part + (int64_t)(4 * blockIdx.x + wave) * M;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pb[(16 * m + kq * 4 + r) * K2 + 16 * j + l16] = acc[m][j][r];
+  red[t] = bacc;
+  __syncthreads();
+  if (t < C) {  // db into wave 0's row; the other rows' db slots zero
+    float s = 0.f;
+    for (int sl = 0; sl < 8; ++sl) s += red[sl * 32 + t];
+    pb[C * K2 + t] = s;
+  } else if (t >= 64 && (t & 63) < C) {
+    pb[C * K2 + (t & 63)] = 0.f;
+  }
+}
+
 }  // namespace lvae
 
 using namespace lvae;
@@ -694,8 +1217,18 @@ static int wgrad_per(int N) {
   return v > 0 ? v : imgs_per_block(N);
 }
 
+// the second encoder conv's shape takes the dense f32-MFMA form (LVAE_WGRAD_MFMA=0: the sparse VALU form; read
+// once, so the workspace size query and the launch agree): 4 partial rows per block of 2 wgrad_per images
+static bool wgrad_mfma(int C, int Cin, int H, int W) {
+  static const bool on = !getenv("LVAE_WGRAD_MFMA") || atoi(getenv("LVAE_WGRAD_MFMA")) != 0;
+  return on && Cin == 16 && C == 32 && H == 18 && W == 18;
+}
+
 size_t lvae_conv3x3_pool_wgrad_workspace_size(int N, int C, int Cin) {
-  return N <= 0 || C <= 0 || Cin <= 0 ? 0 : sizeof(float) * ((size_t)C * Cin * 9 + C) * (size_t)cdiv(N, wgrad_per(N));
+  if (N <= 0 || C <= 0 || Cin <= 0) return 0;
+  const size_t rows = (size_t)cdiv(N, wgrad_per(N)), rows2 = 4 * (size_t)cdiv(N, 2 * wgrad_per(N));
+  // (the MFMA form's rows when the shape can take it: H, W are not arguments here)
+  return sizeof(float) * ((size_t)C * Cin * 9 + C) * (wgrad_mfma(C, Cin, 18, 18) && rows2 > rows ? rows2 : rows);
 }
 
 int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* idx, const float* x, int N, int C,
@@ -715,6 +1248,15 @@ int lvae_conv3x3_pool_wgrad_f32(const float* gy, const float* y, const uint8_t* 
   const int per = wgrad_per(N), nb = (int)cdiv(N, per), m = Q * 9 + C;
   float* part = (float*)workspace;
   const int Ho = H / 2, Wo = W / 2;
+  // the second encoder conv's shape: the dense f32-MFMA form (LVAE_WGRAD_MFMA=0: the sparse VALU form), twice the
+  // images per block (fewer partial rows than the workspace holds)
+  if (wgrad_mfma(C, Cin, H, W)) {
+    const int nb2 = (int)cdiv(N, 2 * per);
+    conv3x3_pool_wgrad_mfma_kernel<<<nb2, 256, 0, st>>>(gy, y, idx, x, N, 2 * per, part);
+    wgrad_sum_kernel<<<cdiv(m, 64), 256, 0, st>>>(part, 4 * nb2, m, Q * 9, dw, db);
+    LVAE_CHECK_LAUNCH();
+    return 0;
+  }
   switch (NP) {
     case 1: conv3x3_pool_wgrad_kernel<1><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, per, part); break;
     case 2: conv3x3_pool_wgrad_kernel<2><<<nb, 256, lds, st>>>(gy, y, idx, x, N, C, Cin, Ho, Wo, per, part); break;
@@ -757,6 +1299,75 @@ int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* 
     const int nthr = (int)cdiv((int64_t)H * W, 64) * 64;
     conv3x3_pool_dgrad_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2,
                                                                          dgrad_cc(C), gx);
+  }
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// The fused second-conv forward: Cin 16, H = W = 18 (the ConvVAE's 36 x 36 images after the first pool), C a
+// multiple of 16; -3 for other shapes (the caller keeps MIOpen's conv + relu_maxpool2_bias_fwd for them).
+int lvae_conv3x3_relu_maxpool2_fwd_f32(const float* x, const float* w, const float* bias, int N, int Cin, int C, int H,
+                                       int W, float* y, uint8_t* idx, void* stream) {
+  if (!x || !w || !bias || !y || !idx) return -1;
+  if (N < 0 || Cin <= 0 || C <= 0 || H < 2 || W < 2 || (H & 1) || (W & 1)) return -2;
+  if (Cin != 16 || H != 18 || W != 18 || C % 16) return -3;
+  if (N == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (N >= 2048)  // (3 images a block: 243 of 256 lanes busy; below 2048 images, one: more blocks to fill the GPU)
+    conv3x3_relu_pool_fwd_kernel<16, 18, 3><<<cdiv(N, 3), 256, 0, st>>>(x, w, bias, N, C, y, idx);
+  else
+    conv3x3_relu_pool_fwd_kernel<16, 18, 1><<<N, 256, 0, st>>>(x, w, bias, N, C, y, idx);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// The fused first decoder transposed conv: Cin 32, Cout 16, Hi = Wi = 9, kernel 4, stride 2, padding 1 (-3 otherwise)
+int lvae_deconv4s2_relu_fwd_f32(const float* x, const float* w, const float* bias, int N, int Cin, int Cout, int Hi,
+                                int Wi, float* y, void* stream) {
+  if (!x || !w || !bias || !y) return -1;
+  if (N < 0 || Cin <= 0 || Cout <= 0 || Hi <= 0 || Wi <= 0) return -2;
+  if (Cin != 32 || Cout != 16 || Hi != 9 || Wi != 9) return -3;
+  if (N == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (N >= 2048)
+    deconv4s2_relu_fwd_kernel<32, 16, 9, 3><<<cdiv(N, 3), 256, 0, st>>>(x, w, bias, N, y);
+  else
+    deconv4s2_relu_fwd_kernel<32, 16, 9, 1><<<N, 256, 0, st>>>(x, w, bias, N, y);
+  LVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// images per block of the backward (a multiple of its 2 images in LDS): 8 at 4096+ images (512 blocks, 2 per CU),
+// fewer below so that the grid still covers the GPU
+static int deconv4s2_per(int N) { return N >= 4096 ? 8 : N >= 2048 ? 4 : 2; }
+
+size_t lvae_deconv4s2_relu_bwd_workspace_size(int N, int Cin, int Cout) {
+  if (N <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  return sizeof(float) * 2 * (size_t)cdiv(N, deconv4s2_per(N)) * ((size_t)Cin * Cout * 16 + Cout);
+}
+
+int lvae_deconv4s2_relu_bwd_f32(const float* gy, const float* y, const float* x, const float* w, int N, int Cin,
+                                int Cout, int Hi, int Wi, float* dx, float* dw, float* db, void* workspace,
+                                void* stream) {
+  if (!gy || !y || !x || !w || !dx || !dw || !db || !workspace) return -1;
+  if (N < 0 || Cin <= 0 || Cout <= 0 || Hi <= 0 || Wi <= 0) return -2;
+  if (Cin != 32 || Cout != 16 || Hi != 9 || Wi != 9) return -3;
+  hipStream_t st = (hipStream_t)stream;
+  if (N == 0) {
+    (void)zero_async(dw, sizeof(float) * Cin * Cout * 16, st);
+    (void)zero_async(db, sizeof(float) * Cout, st);
+    return 0;
+  }
+  const int per = deconv4s2_per(N), nb = (int)cdiv(N, per), m = Cin * Cout * 16 + Cout;
+  float* part = (float*)workspace;
+  // LVAE_DECONV_MFMA=0: the VALU form (deconv4s2_relu_bwd_kernel, two partial rows per block)
+  static const bool mfma = !getenv("LVAE_DECONV_MFMA") || atoi(getenv("LVAE_DECONV_MFMA")) != 0;
+  if (mfma) {
+    deconv4s2_relu_bwd_mfma_kernel<<<nb, 256, 0, st>>>(gy, y, x, w, N, per, dx, part);
+    wgrad_sum_kernel<<<cdiv(m, 64), 256, 0, st>>>(part, nb, m, Cin * Cout * 16, dw, db);
+  } else {
+    deconv4s2_relu_bwd_kernel<32, 16, 9, 2><<<nb, 256, 0, st>>>(gy, y, x, w, N, per, dx, part);
+    wgrad_sum_kernel<<<cdiv(m, 64), 256, 0, st>>>(part, 2 * nb, m, Cin * Cout * 16, dw, db);
   }
   LVAE_CHECK_LAUNCH();
   return 0;

@@ -130,6 +130,11 @@ SIGNATURES = {
     "lvae_deconv2_sigmoid_fwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP]),
     "lvae_deconv2_sigmoid_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP]),
     "lvae_conv3x3_pool_wgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP]),
+    "lvae_conv3x3_relu_maxpool2_fwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
+    "lvae_deconv4s2_relu_fwd_f32": (_I32, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
+    "lvae_deconv4s2_relu_bwd_workspace_size": (_SZ, [_I32, _I32, _I32]),
+    "lvae_deconv4s2_relu_bwd_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP,
+                                            _VP]),
     "lvae_conv3x3_pool_dgrad_lds": (_SZ, [_I32, _I32, _I32]),
     "lvae_conv3x3_pool_dgrad_f32": (_I32, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     "lvae_spd_inv_chol_scratch_size": (_SZ, [_I32, _I32]),

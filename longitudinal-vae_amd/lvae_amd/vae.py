@@ -19,6 +19,9 @@ _CONV_DGRAD = os.environ.get("LVAE_CONV_DGRAD", "1") != "0"
 # backward's stream instead of side by side (the weight gradient on a side stream, joined before returning)
 _CONV_BWD_FORK = os.environ.get("LVAE_CONV_BWD_FORK", "1") != "0"
 _FORK_UNDER_CAPTURE = os.environ.get("LVAE_FORK_UNDER_CAPTURE", "0") == "1"
+# LVAE_CONV_FUSED=0: the second encoder conv's forward and the first decoder transposed conv (forward and backward)
+# on MIOpen (+ the fused bias / relu / pool passes) instead of the direct HIP kernels (vae_ops.hip)
+_CONV2_FUSED = os.environ.get("LVAE_CONV_FUSED", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -83,6 +86,16 @@ class _ConvReluMaxPool2(torch.autograd.Function):
             _lib.check(lib.lvae_conv1_relu_maxpool2_fwd_f32(_lib.ptr(xc), _lib.ptr(wc), _lib.ptr(b), N, C, H, W,
                                                              _lib.ptr(y), _lib.ptr(idx), _lib.stream_ptr()),
                        "conv1_relu_maxpool2_fwd")
+        elif _CONV2_FUSED and x.shape[1] == 16 and x.shape[2] == x.shape[3] == 18 and weight.shape[0] % 16 == 0:
+            # the second conv end to end: one direct HIP pass (no MIOpen conv, no layout transposes, no
+            # full-resolution output)
+            xc, wc = x.contiguous(), weight.contiguous()
+            N, C, H, W = x.shape[0], weight.shape[0], x.shape[2], x.shape[3]
+            y = torch.empty(N, C, H // 2, W // 2, dtype=x.dtype, device=x.device)
+            idx = torch.empty(N, C, H // 2, W // 2, dtype=torch.uint8, device=x.device)
+            _lib.check(lib.lvae_conv3x3_relu_maxpool2_fwd_f32(_lib.ptr(xc), _lib.ptr(wc), _lib.ptr(b), N, x.shape[1], C,
+                                                               H, W, _lib.ptr(y), _lib.ptr(idx), _lib.stream_ptr()),
+                       "conv3x3_relu_maxpool2_fwd")
         else:
             y0 = F.conv2d(x, weight, None, 1, 1).contiguous()
             N, C, H, W = y0.shape
@@ -269,14 +282,34 @@ class _LinearAct(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def _deconv4s2_fused(x, weight, stride, padding, output_padding, dilation, groups):
+    """The shapes lvae_deconv4s2_relu_fwd / _bwd_f32 take: the ConvVAE's deconv1 (32 -> 16, 4 x 4, stride 2,
+    padding 1) on 9 x 9 inputs."""
+    return (_CONV2_FUSED and x.dim() == 4 and tuple(x.shape[1:]) == (32, 9, 9) and tuple(weight.shape) == (32, 16, 4, 4)
+            and tuple(stride) == (2, 2) and tuple(padding) == (1, 1) and tuple(output_padding) == (0, 0)
+            and tuple(dilation) == (1, 1) and groups == 1)
+
+
 class _DeconvRelu(torch.autograd.Function):
-    """relu(ConvTranspose2d(x)) (VAE.py:73, 122): the transposed conv without its bias on MIOpen, then bias +
-    ReLU in place as one HIP pass; backward: the pre-activation and bias gradients in one HIP pass, the
-    input / weight gradients from MIOpen's convolution backward."""
+    """relu(ConvTranspose2d(x)) (VAE.py:73, 122).  The ConvVAE's shape (32 -> 16, 4 x 4, stride 2, padding 1, 9 x 9
+    inputs): one direct HIP pass each way (lvae_deconv4s2_relu_fwd / _bwd_f32: the backward returns the input,
+    weight and bias gradients together from the masked output gradient).  Other shapes: the transposed conv
+    without its bias on MIOpen, then bias + ReLU in place as one HIP pass; backward: the pre-activation and bias
+    gradients in one HIP pass, the input / weight gradients from MIOpen's convolution backward."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, output_padding, dilation, groups):
         from . import _lib
+        ctx.fused = _deconv4s2_fused(x, weight, stride, padding, output_padding, dilation, groups)
+        if ctx.fused:
+            xc, wc = x.contiguous(), weight.contiguous()
+            N = x.shape[0]
+            y = torch.empty(N, 16, 18, 18, dtype=x.dtype, device=x.device)
+            _lib.check(_lib.lib().lvae_deconv4s2_relu_fwd_f32(_lib.ptr(xc), _lib.ptr(wc), _lib.ptr(bias.contiguous()), N,
+                                                               32, 16, 9, 9, _lib.ptr(y), _lib.stream_ptr()),
+                       "deconv4s2_relu_fwd")
+            ctx.save_for_backward(xc, wc, y)
+            return y
         y = F.conv_transpose2d(x, weight, None, stride, padding, output_padding, groups, dilation).contiguous()
         N, C = y.shape[0], y.shape[1]
         _lib.check(_lib.lib().lvae_bias_relu_fwd_f32(_lib.ptr(y), _lib.ptr(bias.contiguous()), N, C,
@@ -288,8 +321,21 @@ class _DeconvRelu(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        stride, padding, output_padding, dilation, groups = ctx.conf
         gy = gy.contiguous()
+        if ctx.fused:
+            from . import _lib
+            lib = _lib.lib()
+            N = x.shape[0]
+            dx = torch.empty_like(x)
+            dw = torch.empty_like(w)
+            db = torch.empty(16, dtype=x.dtype, device=x.device)
+            ws = torch.empty(lib.lvae_deconv4s2_relu_bwd_workspace_size(N, 32, 16) // 4 + 1, dtype=torch.float32,
+                             device=x.device)
+            _lib.check(lib.lvae_deconv4s2_relu_bwd_f32(_lib.ptr(gy), _lib.ptr(y), _lib.ptr(x), _lib.ptr(w), N, 32, 16,
+                                                        9, 9, _lib.ptr(dx), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                                        _lib.stream_ptr()), "deconv4s2_relu_bwd")
+            return dx if ctx.needs_input_grad[0] else None, dw, db, None, None, None, None, None
+        stride, padding, output_padding, dilation, groups = ctx.conf
         g, db = _act_bwd(gy, y, True, y.shape[0], y.shape[1], y.shape[2] * y.shape[3])
         dx, dw, _ = torch.ops.aten.convolution_backward(g, x, w, None, list(stride), list(padding), list(dilation),
                                                         True, list(output_padding), groups,

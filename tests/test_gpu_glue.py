@@ -152,10 +152,11 @@ def test_linear_act_fused_nan(hip):
     assert torch.equal(torch.isnan(x.grad), torch.isnan(xr.grad))
 
 
-@pytest.mark.parametrize("N", [4096, 37])
+@pytest.mark.parametrize("N", [4096, 37, 1, 2049, 2050])
 def test_deconv_relu_fused(hip, N):
-    """The decoder's relu(ConvTranspose2d(32, 16, 4, 2, 1)) (VAE.py:73, 122): MIOpen's transposed conv without
-    bias, bias + ReLU fused (glue.hip bias_act) forward, the pre-activation and bias gradients fused backward.
+    """The decoder's relu(ConvTranspose2d(32, 16, 4, 2, 1)) (VAE.py:73, 122): one direct HIP pass each way
+    (vae_ops.hip deconv4s2_relu: the 1 / 3 images-per-block forward grids, the 2 / 4 / 8 images-per-block backward
+    with ragged last blocks).
     The output against fp64, and the input / weight / bias gradients against fp64 through the same ReLU mask
     (y > 0 of the GPU forward: at 21M outputs a few pre-activations sit within rounding of 0, where a flipped mask
     is a tie-break, not an error).  MIOpen's Winograd solvers, off by default since r5, had put dx 4.3e-2 from
@@ -181,3 +182,25 @@ def test_deconv_relu_fused(hip, N):
     print(N, errs)
     for k, e in errs.items():
         assert e < 1e-5, (k, e)
+
+
+def test_deconv4s2_relu_abi(hip):
+    """lvae_deconv4s2_relu_fwd / _bwd_f32 directly: -3 for the shapes they do not take, and the backward's
+    zero-image call writes zero weight / bias gradients."""
+    from lvae_amd import _lib
+    x = torch.randn(2, 32, 9, 9, device="cuda")
+    w = torch.randn(32, 16, 4, 4, device="cuda")
+    b = torch.randn(16, device="cuda")
+    y = torch.empty(2, 16, 18, 18, device="cuda")
+    assert hip.lvae_deconv4s2_relu_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), 2, 16, 16, 9, 9, _lib.ptr(y),
+                                           _lib.stream_ptr()) == -3
+    assert hip.lvae_deconv4s2_relu_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), 2, 32, 16, 8, 8, _lib.ptr(y),
+                                           _lib.stream_ptr()) == -3
+    dw = torch.full_like(w, float("nan"))
+    db = torch.full_like(b, float("nan"))
+    ws = torch.empty(16, device="cuda")
+    assert hip.lvae_deconv4s2_relu_bwd_f32(_lib.ptr(y), _lib.ptr(y), _lib.ptr(x), _lib.ptr(w), 0, 32, 16, 9, 9,
+                                           _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws),
+                                           _lib.stream_ptr()) == 0
+    torch.cuda.synchronize()
+    assert float(dw.abs().max()) == 0.0 and float(db.abs().max()) == 0.0

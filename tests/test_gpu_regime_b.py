@@ -377,6 +377,9 @@ def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw, xgrad):
     if cin == 1:
         rc = hip.lvae_conv1_relu_maxpool2_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), n, cout, hw, hw,
                                                   _lib.ptr(y2), _lib.ptr(idx), _lib.stream_ptr())
+    elif cin == 16 and hw == 18 and cout % 16 == 0:  # (the second conv's fused forward)
+        rc = hip.lvae_conv3x3_relu_maxpool2_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), n, cin, cout, hw, hw,
+                                                    _lib.ptr(y2), _lib.ptr(idx), _lib.stream_ptr())
     else:
         y0 = F.conv2d(x, w, None, 1, 1).contiguous()
         rc = hip.lvae_relu_maxpool2_bias_fwd_f32(_lib.ptr(y0), _lib.ptr(b), n, cout, hw, hw, _lib.ptr(y2),
@@ -393,6 +396,39 @@ def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw, xgrad):
     tols = [1e-5] + ([1e-5] if xgrad else []) + [5e-5, 5e-5]
     errs = [rel(a, r) for a, r in zip(got, ref)]
     assert all(e < tol for e, tol in zip(errs, tols)), errs
+
+
+@pytest.mark.parametrize("n,c", [(1, 32), (5, 16), (2047, 32), (2050, 32), (4096, 32), (4, 48)])
+def test_conv3x3_relu_maxpool2_fused_vs_fp64(hip, n, c):
+    """lvae_conv3x3_relu_maxpool2_fwd_f32 (the second encoder conv + bias + relu + 2x2 pool in one pass, VAE.py:48-50)
+    vs fp64 conv2d on the same inputs: y within 1e-5 of its max of the fp64 relu-max; idx the fp64 argmax wherever
+    the window's top two fp64 values are apart by more than fp32 rounding (a near-tie may go either way); the
+    one-image-per-block (< 2048 images) and three-images-per-block grids, ragged last blocks.  Unsupported shapes
+    return -3."""
+    from lvae_amd import _lib
+    import torch.nn.functional as F
+    gen = torch.Generator(device=DEV).manual_seed(n + c)
+    cin, hw, ho = 16, 18, 9
+    x = torch.randn(n, cin, hw, hw, device=DEV, generator=gen).clamp_min(0.0)  # (post-relu inputs, like the model's)
+    w = torch.randn(c, cin, 3, 3, device=DEV, generator=gen) * 0.1
+    b = torch.randn(c, device=DEV, generator=gen) * 0.1
+    y = torch.full((n, c, ho, ho), float("nan"), device=DEV)
+    idx = torch.full((n, c, ho, ho), 255, dtype=torch.uint8, device=DEV)
+    rc = hip.lvae_conv3x3_relu_maxpool2_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), n, cin, c, hw, hw, _lib.ptr(y),
+                                                _lib.ptr(idx), _lib.stream_ptr())
+    assert rc == 0
+    z64 = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    win = z64.view(n, c, ho, 2, ho, 2).permute(0, 1, 2, 4, 3, 5).reshape(n, c, ho, ho, 4)
+    ref = F.max_pool2d(F.relu(z64), 2, 2)
+    assert rel(y, ref) < 1e-5
+    top2 = win.topk(2, dim=-1).values
+    clear = (top2[..., 0] - top2[..., 1]) > 1e-5 * float(z64.abs().max())
+    assert int(idx.max()) <= 3
+    assert torch.equal(idx.long()[clear], win.argmax(-1)[clear])
+    assert hip.lvae_conv3x3_relu_maxpool2_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), n, 8, c, hw, hw, _lib.ptr(y),
+                                                  _lib.ptr(idx), _lib.stream_ptr()) == -3
+    assert hip.lvae_conv3x3_relu_maxpool2_fwd_f32(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), n, cin, 24, hw, hw,
+                                                  _lib.ptr(y), _lib.ptr(idx), _lib.stream_ptr()) == -3
 
 
 @pytest.mark.parametrize("n,c,hw", [(3, 4, 8), (37, 32, 18), (2, 8, 30), (513, 32, 18), (4, 20, 12)])
