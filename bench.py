@@ -91,7 +91,10 @@ MFMA_PMC = os.path.join(ROOT, "profiles", f"{TAG}_mfma_pmc.json")
 MFMA_KERNELS = {"lauum + KL epilogue": "ci_gemm_kernel<3>", "trtri X step": "ci_gemm_kernel<0>",
                 "trtri Y step": "ci_gemm_kernel<1>", "potrf trailing update": "ci_update_kernel<2>",
                 "potrf panel": "ci_panel_kernel", "potrf pivot (split)": "ci_pivot_kernel<4>",
-                "binned hyper slab pass": "hb_slab_kernel"}
+                "binned hyper slab pass": "hb_slab_kernel",
+                "conv2 weight gradient (f32 MFMA)": "conv3x3_pool_wgrad_mfma_kernel",
+                "conv2 input gradient (f32 MFMA)": "conv3x3_pool_dgrad_mfma_kernel",
+                "deconv1 backward (f32 MFMA)": "deconv4s2_relu_bwd_mfma_kernel"}
 
 
 def mfma_busy(name_part, path=MFMA_PMC):

@@ -1107,6 +1107,95 @@ __global__ __launch_bounds__(256) void conv3x3_pool_wgrad_mfma_kernel(const floa
   }
 }
 
+// The second encoder conv's input gradient on the f32 MFMA (v_mfma_f32_16x16x4_f32), dense over the routed
+// full-resolution gradient g0 (as conv3x3_pool_wgrad_mfma_kernel's):
+//   gx^T [pos][ci] = sum_{k = 9 co + 3 ky + kx} g0[co][pos + (1 - ky, 1 - kx)] W[co][ci][ky][kx]   (K = 288).
+// One image per iteration in LDS: g0 with a zero border and W^T [k][ci] (once per block); the next image's pooled
+// gradient, y and idx prefetched into registers.  Position tiles of 16 (324 -> 21, padded to 24: 6 per wave, the
+// same k per lane for the wave's 6 tiles: one W^T read and one offset computation per 6 MFMAs).  Output rows
+// 16 tile + 4 (lane >> 4) + 0..3: four consecutive positions of one channel per lane (one 16-byte store).
+__global__ __launch_bounds__(256) void conv3x3_pool_dgrad_mfma_kernel(const float* __restrict__ gy,
+                                                                      const float* __restrict__ y,
+                                                                      const uint8_t* __restrict__ idx,
+                                                                      const float* __restrict__ w, int N, int per,
+                                                                      float* __restrict__ gx) {
+  constexpr int CI = 16, C = 32, H = 18, W = 18, Ho = 9, Wo = 9, P = Ho * Wo, PF = H * W, Wp = W + 2;
+  constexpr int GP = ((H + 2) * Wp) | 1, K = C * 9, TPW = 6;
+  __shared__ float g0[C * GP];
+  __shared__ float wt[K * CI];  // W^T [k][ci]
+  const int t = threadIdx.x, lane = t & 63, l16 = lane & 15, kq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nb0 = blockIdx.x * per, nb1 = min(N, nb0 + per);
+  for (int e = t; e < C * GP; e += 256) g0[e] = 0.f;  // (the border stays zero)
+  for (int e = t; e < C * CI * 9; e += 256) {       // w [co][ci][tap] -> wt [9 co + tap][ci]
+    const int co = e / (CI * 9), r = e - co * CI * 9, ci = r / 9, tap = r - 9 * ci;
+    wt[(9 * co + tap) * CI + ci] = w[e];
+  }
+  // the wave's position tiles: 16 (wave + 4 j) + l16 (A rows); padded (a + 2, b + 2) - (ky, kx) is the read
+  int aoff[TPW];
+  bool aval[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int pos = 16 * (wave + 4 * j) + l16, pc = pos < PF ? pos : PF - 1, a = pc / W, b = pc - a * W;
+    aoff[j] = (a + 2) * Wp + b + 2;
+    aval[j] = pos < PF;
+  }
+  constexpr int NGP = (C * P + 255) / 256;
+  float pg[NGP];
+  int pk[NGP];
+  auto fetch = [&](int n) {
+    const int64_t ob = (int64_t)n * C * P;
+#pragma unroll
+    for (int k = 0; k < NGP; ++k) {
+      const int e = t + 256 * k;
+      if (e < C * P) {
+        const float yv = y[ob + e], gv = gy[ob + e];
+        pg[k] = yv > 0.f ? gv : 0.f;
+        pk[k] = idx[ob + e];
+      }
+    }
+  };
+  if (nb0 < nb1) fetch(nb0);
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  for (int n = nb0; n < nb1; ++n) {
+    __syncthreads();  // the previous image's readers are done (and the zeroing / W^T staged)
+#pragma unroll
+    for (int k = 0; k < NGP; ++k) {
+      const int e = t + 256 * k;
+      if (e < C * P) {
+        const int co = e / P, r = e - co * P, i = r / Wo, j = r - i * Wo;
+        float* q = g0 + co * GP + (2 * i + 1) * Wp + 2 * j + 1;
+        q[0] = pk[k] == 0 ? pg[k] : 0.f;
+        q[1] = pk[k] == 1 ? pg[k] : 0.f;
+        q[Wp] = pk[k] == 2 ? pg[k] : 0.f;
+        q[Wp + 1] = pk[k] == 3 ? pg[k] : 0.f;
+      }
+    }
+    if (n + 1 < nb1) fetch(n + 1);
+    __syncthreads();
+    f32x4_t acc[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int s = 0; s < K / 4; ++s) {
+      const int k = 4 * s + kq, co = (k * 57) >> 9, r9 = k - 9 * co, ky = (r9 * 11) >> 5, kx = r9 - 3 * ky;
+      const float* gk = g0 + co * GP - ky * Wp - kx;
+      const float bv = wt[k * CI + l16];
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const float av = gk[aoff[j]];
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aval[j] ? av : 0.f, bv, acc[j], 0, 0, 0);
+      }
+    }
+    float* gxn = gx + ((int64_t)n * CI + l16) * PF;  // column = ci (lane & 15)
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int p0 = 16 * (wave + 4 * j) + 4 * kq;
+      if (p0 < PF) *reinterpret_cast<f32x4_t*>(gxn + p0) = acc[j];
+    }
+  }
+}
+
 }  // namespace lvae
 
 using namespace lvae;
@@ -1292,7 +1381,12 @@ int lvae_conv3x3_pool_dgrad_f32(const float* gy, const float* y, const uint8_t* 
   // vs 244-256 us at the headline shape; the step is unchanged, the weight-gradient kernel beside it is the longer
   // of the two; profiles/r5_conv_dgrad_ab.txt)
   static const bool pair = !getenv("LVAE_DGRAD_PAIR") || atoi(getenv("LVAE_DGRAD_PAIR")) != 0;
-  if (pair && dgrad_cc(C) == C) {
+  // the second encoder conv's shape: the dense f32-MFMA form (LVAE_DGRAD_MFMA=0: the VALU kernels below)
+  static const bool mfma = !getenv("LVAE_DGRAD_MFMA") || atoi(getenv("LVAE_DGRAD_MFMA")) != 0;
+  if (mfma && C == 32 && H == 18 && W == 18) {
+    const int per = N >= 4096 ? 8 : N >= 2048 ? 4 : N >= 1024 ? 2 : 1;
+    conv3x3_pool_dgrad_mfma_kernel<<<cdiv(N, per), 256, 0, (hipStream_t)stream>>>(gy, y, idx, w, N, per, gx);
+  } else if (pair && dgrad_cc(C) == C) {
     const int nthr = (int)cdiv((int64_t)H * W / 2, 64) * 64;
     conv3x3_pool_dgrad2_kernel<16><<<N, nthr, lds, (hipStream_t)stream>>>(gy, y, idx, w, C, H / 2, W / 2, gx);
   } else {
