@@ -159,8 +159,10 @@ class LatentShardedClosedStep:
         return net, rl, nl, gp
 
     def __call__(self, img, mask, X, eps=None):
+        from .steps import bwd_thread_ctx
         if img.is_cuda and self.hip:
-            return self._step_overlapped(img, mask, X, eps)
+            with bwd_thread_ctx():
+                return self._step_overlapped(img, mask, X, eps)
         return self._step_plain(img, mask, X, eps)
 
     def _step_overlapped(self, img, mask, X, eps):

@@ -11,10 +11,24 @@ assigns each gradient instead of filling it with zeros and adding, two kernels l
 split into ``forward_backward`` (everything up to the gradients) and ``apply`` (optimiser + state
 updates) so that a data-parallel all-reduce can sit between two captured graphs.
 """
+import contextlib
+import os
+
 import torch
 
 from .elbo import (KL_closed_batched, kl_closed_prefactor, minibatch_KLD_upper_bound, natural_gradient_update,
                    natural_gradient_update_, take_pending)
+
+
+# LVAE_BWD_ON_CALLER=0: the closed steps' backward on autograd's per-device worker thread (torch's default) instead
+# of the calling thread.  On the caller the step's host side is shorter: at one W = 8 rank's share, whose step the
+# host's enqueue paces, 3.52-3.54 vs 3.71-3.76 ms (profiles/r6_bwd_thread_ab.txt)
+_BWD_ON_CALLER = os.environ.get("LVAE_BWD_ON_CALLER", "1") != "0"
+
+
+def bwd_thread_ctx():
+    """The context the closed steps run their backward passes in (see _BWD_ON_CALLER)."""
+    return torch.autograd.set_multithreading_enabled(False) if _BWD_ON_CALLER else contextlib.nullcontext()
 
 
 def _graph_vae_default():
@@ -46,6 +60,10 @@ class ClosedStep:
         return s
 
     def forward_backward(self, img, mask, X, eps=None):
+        with bwd_thread_ctx():
+            return self._forward_backward(img, mask, X, eps)
+
+    def _forward_backward(self, img, mask, X, eps=None):
         self.opt.zero_grad(set_to_none=True)
         if img.is_cuda:
             # The Gram and its inverse need only the covariates and hyperparameters: they are

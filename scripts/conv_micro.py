@@ -65,3 +65,14 @@ print(f"conv2 wgrad {t:7.1f} us  {2 * N * 32 * 324 * 144 / t / 1e6:6.1f} TFLOP/s
 gx2 = torch.empty_like(x2)
 t = timed(lambda: lib.lvae_conv3x3_pool_dgrad_f32(P(gp), P(yp), P(ip), P(w2), N, 32, 16, 18, 18, P(gx2), st()))
 print(f"conv2 dgrad {t:7.1f} us  {2 * N * 32 * 324 * 144 / t / 1e6:6.1f} TFLOP/s (dense-equivalent)")
+# the first encoder conv's weight / bias gradients (1 input channel, 16 channels, 36 x 36)
+x1 = torch.rand(N, 1, 36, 36, device=dev)
+g1 = torch.randn(N, 16, 18, 18, device=dev)
+i1 = torch.randint(0, 4, (N, 16, 18, 18), device=dev, dtype=torch.int32).to(torch.uint8)
+y1 = torch.randn(N, 16, 18, 18, device=dev).clamp_min(0.0)
+dw1 = torch.empty(16, 1, 3, 3, device=dev)
+db1 = torch.empty(16, device=dev)
+ws1 = torch.empty(lib.lvae_conv3x3_pool_wgrad_workspace_size(N, 16, 1) // 4 + 1, device=dev)
+t = timed(lambda: lib.lvae_conv3x3_pool_wgrad_f32(P(g1), P(y1), P(i1), P(x1), N, 16, 1, 36, 36, P(dw1), P(db1), P(ws1),
+                                                  st()))
+print(f"conv1 wgrad {t:7.1f} us  {2 * N * 16 * 1296 * 9 / t / 1e6:6.1f} TFLOP/s (dense-equivalent)")

@@ -4,7 +4,7 @@
 # (KERNELS set) rocprofv3 kernel stats of a short "new" run filtered by KERNELS.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 OUT=gpurun_out; mkdir -p $OUT
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
   for v in old new; do
     if [ $v = old ]; then E="$OLD_ENV"; else E=""; fi
     timeout -k 10 300 env $E python3 bench.py --regime closed --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-c2 \

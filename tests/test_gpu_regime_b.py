@@ -345,7 +345,7 @@ def test_relu_maxpool2_bias_kernels_match_torch(hip, n, c, hw):
 
 @pytest.mark.parametrize("n,cin,cout,hw,xgrad", [(5, 1, 16, 36, True), (37, 16, 32, 18, True), (37, 1, 16, 36, False),
                                                (3, 1, 4, 8, False), (520, 16, 32, 18, True), (600, 1, 16, 36, False),
-                                               (2050, 16, 32, 18, True)])
+                                               (2050, 16, 32, 18, True), (2051, 1, 16, 36, False)])
 def test_conv_relu_maxpool2_bias_matches_torch(hip, n, cin, cout, hw, xgrad):
     """Encoder conv with its bias folded into the fused relu + pool pass (bias gradient from its
     backward, weight / input gradients from aten.convolution_backward; for the first conv, whose
