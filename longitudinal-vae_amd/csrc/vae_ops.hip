@@ -1407,8 +1407,14 @@ int lvae_conv3x3_relu_maxpool2_fwd_f32(const float* x, const float* w, const flo
   if (Cin != 16 || H != 18 || W != 18 || C % 16) return -3;
   if (N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (N >= 2048)  // (3 images a block: 243 of 256 lanes busy; below 2048 images, one: more blocks to fill the GPU)
+  // (3 images a block: 243 of 256 lanes busy; below 2048 images, one: more blocks to fill the GPU.
+  // LVAE_CONV2_IPB = 1 / 2 / 3 forces one, for A/B runs)
+  static const int ipb_env = getenv("LVAE_CONV2_IPB") ? atoi(getenv("LVAE_CONV2_IPB")) : 0;
+  const int ipb = ipb_env >= 1 && ipb_env <= 3 ? ipb_env : N >= 2048 ? 3 : 1;
+  if (ipb == 3)
     conv3x3_relu_pool_fwd_kernel<16, 18, 3><<<cdiv(N, 3), 256, 0, st>>>(x, w, bias, N, C, y, idx);
+  else if (ipb == 2)
+    conv3x3_relu_pool_fwd_kernel<16, 18, 2><<<cdiv(N, 2), 256, 0, st>>>(x, w, bias, N, C, y, idx);
   else
     conv3x3_relu_pool_fwd_kernel<16, 18, 1><<<N, 256, 0, st>>>(x, w, bias, N, C, y, idx);
   LVAE_CHECK_LAUNCH();
@@ -1423,8 +1429,12 @@ int lvae_deconv4s2_relu_fwd_f32(const float* x, const float* w, const float* bia
   if (Cin != 32 || Cout != 16 || Hi != 9 || Wi != 9) return -3;
   if (N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (N >= 2048)
+  static const int ipb_env = getenv("LVAE_DECONV_IPB") ? atoi(getenv("LVAE_DECONV_IPB")) : 0;  // (A/B runs)
+  const int ipb = ipb_env >= 1 && ipb_env <= 3 ? ipb_env : N >= 2048 ? 3 : 1;
+  if (ipb == 3)
     deconv4s2_relu_fwd_kernel<32, 16, 9, 3><<<cdiv(N, 3), 256, 0, st>>>(x, w, bias, N, y);
+  else if (ipb == 2)
+    deconv4s2_relu_fwd_kernel<32, 16, 9, 2><<<cdiv(N, 2), 256, 0, st>>>(x, w, bias, N, y);
   else
     deconv4s2_relu_fwd_kernel<32, 16, 9, 1><<<N, 256, 0, st>>>(x, w, bias, N, y);
   LVAE_CHECK_LAUNCH();
